@@ -1,0 +1,245 @@
+"""ORACLE — test infrastructure only.
+
+ctypes front-end to ``liboracle.so`` (the scalar C++ restatement of the reference's
+OpenCV calls, see ``orb_ref.cpp``, ``bf_ref.cpp``, ``sgbm_ref.cpp``, ``pnp_ref.cpp``).
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module, and only as the checker / CPU baseline — never as the product.
+
+Reference call sites restated here (all in ``ros_ws/src/stereo_slam.py``):
+  :84,232-233,240-241  ORB_create() / detectAndCompute        -> orb_detect_compute
+  :85,234,242          BFMatcher(NORM_HAMMING, True).match    -> bf_match
+  :108-123             StereoSGBM 3-way compute + 0/-1 -> 0.1  -> sgbm / disparity_map
+  :265-289             depth, back-projection, 0.1<Z<1000      -> backproject
+  :294-306             solvePnPRansac + Rodrigues + chain      -> solve_pnp_ransac / frame_pose
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_i16p = ctypes.POINTER(ctypes.c_int16)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_f64p = ctypes.POINTER(ctypes.c_double)
+
+
+def build(force: bool = False) -> str:
+    """Compile liboracle.so with the committed Makefile (host g++ only)."""
+    if force or not os.path.exists(_LIB):
+        subprocess.check_call(["make", "-s", "-C", _HERE] + (["-B"] if force else []))
+    return _LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = ctypes.CDLL(_LIB)
+        L.ref_orb_detect_compute.restype = ctypes.c_int
+        L.ref_orb_pyramid.restype = ctypes.c_int
+        L.ref_fast_detect.restype = ctypes.c_int
+        L.ref_retain_best.restype = ctypes.c_int
+        L.ref_fast_atan2.restype = ctypes.c_float
+        L.ref_fast_atan2.argtypes = [ctypes.c_float, ctypes.c_float]
+        L.ref_bf_match.restype = ctypes.c_int
+        L.ref_solve_pnp_ransac.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+# ----------------------------------------------------------------------------- ORB
+def orb_detect_compute(img: np.ndarray, nfeatures: int = 500, fast_threshold: int = 20):
+    """Returns (kp f32[N,6] = x,y,size,angle,response,octave, desc u8[N,32])."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    H, W = img.shape
+    cap = max(4 * nfeatures, 64)
+    while True:
+        kp = np.zeros((cap, 6), np.float32)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = lib().ref_orb_detect_compute(_p(img, _u8p), H, W, W, nfeatures, fast_threshold,
+                                         _p(kp, _f32p), _p(desc, _u8p), cap)
+        if n >= 0:
+            return kp[:n].copy(), desc[:n].copy()
+        cap = -n
+
+
+def orb_pyramid(img: np.ndarray, nlevels: int = 8, blurred: bool = False):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    H, W = img.shape
+    sizes = np.zeros((nlevels, 2), np.int32)
+    total = lib().ref_orb_pyramid(_p(img, _u8p), H, W, W, nlevels, None, _p(sizes, _i32p), int(blurred))
+    buf = np.zeros(total, np.uint8)
+    lib().ref_orb_pyramid(_p(img, _u8p), H, W, W, nlevels, _p(buf, _u8p), _p(sizes, _i32p), int(blurred))
+    out, off = [], 0
+    for w, h in sizes:
+        out.append(buf[off:off + w * h].reshape(h, w))
+        off += w * h
+    return out
+
+
+def fast_score_map(img: np.ndarray, threshold: int = 20) -> np.ndarray:
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    H, W = img.shape
+    out = np.zeros((H, W), np.uint8)
+    lib().ref_fast_score_map(_p(img, _u8p), H, W, W, threshold, _p(out, _u8p))
+    return out
+
+
+def fast_detect(img: np.ndarray, threshold: int = 20) -> np.ndarray:
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    H, W = img.shape
+    cap = 1 << 16
+    while True:
+        out = np.zeros((cap, 3), np.int32)
+        n = lib().ref_fast_detect(_p(img, _u8p), H, W, W, threshold, _p(out, _i32p), cap)
+        if n >= 0:
+            return out[:n].copy()
+        cap = -n
+
+
+def retain_best(resp: np.ndarray, keep: int) -> np.ndarray:
+    resp = np.ascontiguousarray(resp, dtype=np.float32)
+    out = np.zeros(len(resp), np.int32)
+    n = lib().ref_retain_best(_p(resp, _f32p), len(resp), keep, _p(out, _i32p))
+    return out[:n].copy()
+
+
+def fast_atan2(y: float, x: float) -> float:
+    return lib().ref_fast_atan2(y, x)
+
+
+def features_per_level(nfeatures: int = 500, nlevels: int = 8) -> np.ndarray:
+    out = np.zeros(nlevels, np.int32)
+    lib().ref_features_per_level(nfeatures, nlevels, _p(out, _i32p))
+    return out
+
+
+# ----------------------------------------------------------------------------- BF
+def bf_match(d0: np.ndarray, d1: np.ndarray):
+    """Returns int32[M,3] rows (queryIdx, trainIdx, distance), ascending queryIdx."""
+    d0 = np.ascontiguousarray(d0, dtype=np.uint8)
+    d1 = np.ascontiguousarray(d1, dtype=np.uint8)
+    n = min(len(d0), len(d1))
+    q = np.zeros(max(n, 1), np.int32)
+    t = np.zeros(max(n, 1), np.int32)
+    d = np.zeros(max(n, 1), np.int32)
+    m = lib().ref_bf_match(_p(d0, _u8p), len(d0), _p(d1, _u8p), len(d1), _p(q, _i32p), _p(t, _i32p), _p(d, _i32p))
+    return np.stack([q[:m], t[:m], d[:m]], 1)
+
+
+# ----------------------------------------------------------------------------- SGBM
+def sgbm(L: np.ndarray, R: np.ndarray, num_disp: int = 96, block: int = 7, P1: int = 392, P2: int = 1568,
+         min_disp: int = 0, raw: bool = False):
+    L = np.ascontiguousarray(L, dtype=np.uint8)
+    R = np.ascontiguousarray(R, dtype=np.uint8)
+    H, W = L.shape
+    out = np.zeros((H, W), np.int16)
+    rawo = np.zeros((H, W), np.int16)
+    lib().ref_sgbm(_p(L, _u8p), _p(R, _u8p), H, W, W, min_disp, num_disp, block, P1, P2, _p(out, _i16p),
+                   _p(rawo, _i16p))
+    return (out, rawo) if raw else out
+
+
+def sgbm_row_cost(L, R, y, num_disp=96):
+    L = np.ascontiguousarray(L, dtype=np.uint8)
+    R = np.ascontiguousarray(R, dtype=np.uint8)
+    H, W = L.shape
+    width1 = W - num_disp
+    out = np.zeros((width1, num_disp), np.int16)
+    lib().ref_sgbm_row_cost(_p(L, _u8p), _p(R, _u8p), H, W, W, y, num_disp, _p(out, _i16p))
+    return out
+
+
+def disparity_map(disp16: np.ndarray) -> np.ndarray:
+    """stereo_slam.py:117-121: /16 in float32, 0.0 and -1.0 -> 0.1."""
+    d = disp16.astype(np.float32) / 16
+    d[d == 0.0] = 0.1
+    d[d == -1.0] = 0.1
+    return d
+
+
+# ----------------------------------------------------------------------------- pose
+def backproject(disp_f32: np.ndarray, mk0: np.ndarray, mk1: np.ndarray, K: np.ndarray, baseline: float):
+    """stereo_slam.py:265-289 in float64, exactly as numpy evaluates it."""
+    cx, cy, fx, fy = K[0, 2], K[1, 2], K[0, 0], K[1, 1]
+    depth = fx * baseline / disp_f32
+    X = mk0[:, 0]
+    Y = mk0[:, 1]
+    Z = depth[Y.astype(int), X.astype(int)]
+    X = ((X - cx) / fx) * Z
+    Y = ((Y - cy) / fy) * Z
+    P = np.column_stack((X, Y, Z))
+    valid = (Z > 0.1) & (Z < 1000)
+    return P[valid], mk1[valid], valid
+
+
+def solve_pnp_ransac(P3: np.ndarray, p2: np.ndarray, K: np.ndarray, dist: np.ndarray, reproj: float = 1.0,
+                     confidence: float = 0.99, iters: int = 1000):
+    P3 = np.ascontiguousarray(P3, dtype=np.float64)
+    p2 = np.ascontiguousarray(p2, dtype=np.float32)
+    K = np.ascontiguousarray(K, dtype=np.float64)
+    dist = np.ascontiguousarray(np.resize(np.asarray(dist, np.float64), 5))
+    n = len(P3)
+    rv = np.zeros(3)
+    tv = np.zeros(3)
+    mask = np.zeros(max(n, 1), np.uint8)
+    ni = np.zeros(1, np.int32)
+    bg = np.zeros(1, np.int32)
+    ok = lib().ref_solve_pnp_ransac(_p(P3, _f64p), _p(p2, _f32p), n, _p(K, _f64p), _p(dist, _f64p), iters,
+                                    ctypes.c_float(reproj), ctypes.c_double(confidence), _p(rv, _f64p),
+                                    _p(tv, _f64p), _p(mask, _u8p), _p(ni, _i32p), _p(bg, _i32p))
+    return bool(ok), rv, tv, np.nonzero(mask[:n])[0].astype(np.int32), int(ni[0]), int(bg[0])
+
+
+def rodrigues(rvec: np.ndarray) -> np.ndarray:
+    rvec = np.ascontiguousarray(rvec, dtype=np.float64).reshape(3)
+    R = np.zeros(9)
+    lib().ref_rodrigues(_p(rvec, _f64p), _p(R, _f64p))
+    return R.reshape(3, 3)
+
+
+def project_points(P3, rvec, tvec, K, dist):
+    P3 = np.ascontiguousarray(P3, dtype=np.float64)
+    rvec = np.ascontiguousarray(rvec, dtype=np.float64).reshape(3)
+    tvec = np.ascontiguousarray(tvec, dtype=np.float64).reshape(3)
+    K = np.ascontiguousarray(K, dtype=np.float64)
+    dist = np.ascontiguousarray(np.resize(np.asarray(dist, np.float64), 5))
+    uv = np.zeros((len(P3), 2))
+    lib().ref_project_points(_p(P3, _f64p), len(P3), _p(rvec, _f64p), _p(tvec, _f64p), _p(K, _f64p),
+                             _p(dist, _f64p), _p(uv, _f64p))
+    return uv
+
+
+def frame_pose(prevL, prevR, curL, K, dist, baseline, nfeatures=500):
+    """One stereo_slam.py ORB-branch iteration (:232-303).  Returns a dict with every
+    intermediate (for parity tests) and the 4x4 relative transform (or None)."""
+    kp0, d0 = orb_detect_compute(prevL, nfeatures)
+    kp1, d1 = orb_detect_compute(curL, nfeatures)
+    m = bf_match(d0, d1) if len(d0) and len(d1) else np.zeros((0, 3), np.int32)
+    mk0 = kp0[:, :2].astype(np.float32)[m[:, 0]]
+    mk1 = kp1[:, :2].astype(np.float32)[m[:, 1]]
+    disp16 = sgbm(prevL, prevR)
+    disp = disparity_map(disp16)
+    P3, p2, valid = backproject(disp, mk0, mk1, K, baseline)
+    out = dict(kp0=kp0, d0=d0, kp1=kp1, d1=d1, matches=m, disp16=disp16, P3=P3, p2=p2, T=None)
+    if len(P3) >= 6:
+        ok, rv, tv, inl, ni, bg = solve_pnp_ransac(P3, p2, K, dist)
+        out.update(ok=ok, rvec=rv, tvec=tv, inliers=inl)
+        T = np.eye(4)
+        T[:3, :3] = rodrigues(rv)
+        T[:3, 3] = tv
+        out["T"] = T
+    return out
