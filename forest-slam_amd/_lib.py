@@ -1,0 +1,247 @@
+"""ctypes binding of libfvo.so (include/fvo.h) with torch tensors as the buffer type.
+
+The product path: every call lands in a hand-written HIP kernel.  There is no CPU
+fallback — if the library or the GPU is missing, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfvo.so")
+
+KP_STRIDE = 8
+DESC_BYTES = 32
+
+_lib = None
+
+
+class FvoConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("width", "height", "max_batch", "nfeatures")] + [
+        ("scale_factor", ctypes.c_float)] + [(n, ctypes.c_int32) for n in (
+            "nlevels", "edge_threshold", "first_level", "wta_k", "score_type", "patch_size", "fast_threshold",
+            "min_disparity", "num_disparities", "block_size", "P1", "P2", "disp12_max_diff", "pre_filter_cap",
+            "uniqueness_ratio", "sgbm_stripes", "kp_capacity")]
+
+
+# name -> (restype, argtypes); mirrors include/fvo.h
+_P = ctypes.c_void_p
+_I = ctypes.c_int32
+_L = ctypes.c_int64
+SIGNATURES = {
+    "fvo_abi_version": (ctypes.c_int, []),
+    "fvo_config_default": (None, [ctypes.POINTER(FvoConfig), _I, _I]),
+    "fvo_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(FvoConfig), ctypes.POINTER(_P)]),
+    "fvo_destroy": (None, [_P]),
+    "fvo_last_error": (ctypes.c_char_p, [_P]),
+    "fvo_kp_capacity": (ctypes.c_int, [_P]),
+    "fvo_workspace_bytes": (ctypes.c_int64, [_P]),
+    "fvo_orb_detect_compute": (ctypes.c_int, [_P, _P, _I, _L, _I, _P, _P, _P, _I, _P]),
+    "fvo_bf_match": (ctypes.c_int, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
+    "fvo_sgbm": (ctypes.c_int, [_P, _P, _P, _I, _L, _I, _P, _P]),
+    "fvo_backproject": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, _P, ctypes.c_double, _P, _P, _P, _P]),
+    "fvo_pnp_ransac": (ctypes.c_int, [_P, _P, _P, _P, _I, _I, _P, _P, ctypes.c_float, ctypes.c_double, _I, _P, _P,
+                                      _P, _P, _P, _P]),
+    "fvo_test_retain_best": (ctypes.c_int, [_P, _P, _I, _I, _P, _P, _P]),
+    "fvo_debug_buffer": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
+}
+
+
+def load(path: str = LIB_PATH):
+    """Load libfvo.so (raises if it is missing: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise RuntimeError(f"libfvo.so not found at {path}: run __graft_entry__.build() "
+                               "(python -m forest_slam_amd.build); the HIP path has no CPU fallback")
+        L = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.fvo_abi_version() != 1:
+            raise RuntimeError("libfvo.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def _ptr(t: torch.Tensor | None):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("libfvo takes device tensors")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _i32(x, dev):
+    return torch.as_tensor(x, dtype=torch.int32, device=dev)
+
+
+class Context:
+    """One fvo context (device workspace) for a fixed image size and max batch."""
+
+    def __init__(self, width: int, height: int, max_batch: int = 1, device: int | str | torch.device | None = None,
+                 **params):
+        if not torch.cuda.is_available():
+            raise RuntimeError("forest_slam_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.L = load()
+        dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        if dev.type != "cuda":
+            raise RuntimeError("device must be a cuda (ROCm) device")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        cfg = FvoConfig()
+        self.L.fvo_config_default(ctypes.byref(cfg), width, height)
+        cfg.max_batch = max_batch
+        for k, v in params.items():
+            if not hasattr(cfg, k):
+                raise TypeError(f"unknown fvo_config field {k}")
+            setattr(cfg, k, v)
+        self.cfg = cfg
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            rc = self.L.fvo_create(dev.index, ctypes.byref(cfg), ctypes.byref(h))
+        if rc != 0 or not h.value:
+            raise RuntimeError("fvo_create failed (see stderr)")
+        self.h = h
+        self.kp_cap = self.L.fvo_kp_capacity(h)
+        self.width, self.height, self.max_batch = width, height, max_batch
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.L.fvo_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise RuntimeError("libfvo: " + self.L.fvo_last_error(self.h).decode())
+
+    @property
+    def workspace_bytes(self) -> int:
+        return int(self.L.fvo_workspace_bytes(self.h))
+
+    # ------------------------------------------------------------------ stages
+    def orb(self, images: torch.Tensor, out=None):
+        """images u8 [B,H,W] (or [H,W]) on device -> (kp f32[B,cap,8], desc u8[B,cap,32], counts i32[B])."""
+        if images.dim() == 2:
+            images = images[None]
+        if images.dtype != torch.uint8:
+            raise TypeError("images must be uint8")
+        images = images.contiguous()
+        B, H, W = images.shape
+        if (H, W) != (self.height, self.width):
+            raise ValueError(f"context is {self.width}x{self.height}, got {W}x{H}")
+        cap = self.kp_cap
+        if out is None:
+            kp = torch.empty((B, cap, KP_STRIDE), dtype=torch.float32, device=self.device)
+            desc = torch.empty((B, cap, DESC_BYTES), dtype=torch.uint8, device=self.device)
+            cnt = torch.empty((B,), dtype=torch.int32, device=self.device)
+        else:
+            kp, desc, cnt = out
+        self._check(self.L.fvo_orb_detect_compute(self.h, _ptr(images), B, H * W, W, _ptr(kp), _ptr(desc),
+                                                  _ptr(cnt), cap, _stream(self.device)))
+        return kp, desc, cnt
+
+    def bf_match(self, d0, n0, d1, n1, out=None):
+        """Cross-checked Hamming matching; d* u8 [B,cap,32], n* i32 [B]."""
+        B, cap = d0.shape[0], d0.shape[1]
+        if out is None:
+            m = torch.empty((B, cap, 3), dtype=torch.int32, device=self.device)
+            nm = torch.empty((B,), dtype=torch.int32, device=self.device)
+        else:
+            m, nm = out
+        self._check(self.L.fvo_bf_match(self.h, _ptr(d0.contiguous()), _ptr(n0), _ptr(d1.contiguous()), _ptr(n1), B,
+                                        cap, _ptr(m), _ptr(nm), _stream(self.device)))
+        return m, nm
+
+    def sgbm(self, left, right, out=None):
+        if left.dim() == 2:
+            left, right = left[None], right[None]
+        left, right = left.contiguous(), right.contiguous()
+        B, H, W = left.shape
+        if out is None:
+            out = torch.empty((B, H, W), dtype=torch.int16, device=self.device)
+        self._check(self.L.fvo_sgbm(self.h, _ptr(left), _ptr(right), B, H * W, W, _ptr(out), _stream(self.device)))
+        return out
+
+    def backproject(self, disp, kp0, kp1, matches, nmatch, K, baseline, out=None):
+        B, cap = matches.shape[0], matches.shape[1]
+        if out is None:
+            P3 = torch.empty((B, cap, 3), dtype=torch.float32, device=self.device)
+            p2 = torch.empty((B, cap, 2), dtype=torch.float32, device=self.device)
+            n = torch.empty((B,), dtype=torch.int32, device=self.device)
+        else:
+            P3, p2, n = out
+        Kh = (ctypes.c_double * 9)(*[float(v) for v in K.reshape(-1)])
+        self._check(self.L.fvo_backproject(self.h, _ptr(disp), _ptr(kp0), _ptr(kp1), _ptr(matches), _ptr(nmatch), B,
+                                           cap, Kh, float(baseline), _ptr(P3), _ptr(p2), _ptr(n),
+                                           _stream(self.device)))
+        return P3, p2, n
+
+    def pnp_ransac(self, P3, p2, n, K, dist, reproj=1.0, confidence=0.99, iterations=1000, out=None):
+        B, cap = P3.shape[0], P3.shape[1]
+        if out is None:
+            rvec = torch.empty((B, 3), dtype=torch.float64, device=self.device)
+            tvec = torch.empty((B, 3), dtype=torch.float64, device=self.device)
+            T = torch.empty((B, 4, 4), dtype=torch.float64, device=self.device)
+            st = torch.empty((B,), dtype=torch.int32, device=self.device)
+            inl = torch.empty((B, cap), dtype=torch.uint8, device=self.device)
+        else:
+            rvec, tvec, T, st, inl = out
+        Kh = (ctypes.c_double * 9)(*[float(v) for v in K.reshape(-1)])
+        dh = (ctypes.c_double * 5)(*([float(v) for v in list(dist)[:5]] + [0.0] * (5 - min(5, len(dist)))))
+        self._check(self.L.fvo_pnp_ransac(self.h, _ptr(P3), _ptr(p2), _ptr(n), B, cap, Kh, dh, float(reproj),
+                                          float(confidence), int(iterations), _ptr(rvec), _ptr(tvec), _ptr(T),
+                                          _ptr(st), _ptr(inl), _stream(self.device)))
+        return rvec, tvec, T, st, inl
+
+    def debug_buffer(self, which: int) -> torch.Tensor:
+        """Host copy (u8 CPU tensor) of an internal workspace buffer (fvo_debug_buffer)."""
+        p = ctypes.c_void_p()
+        nb = ctypes.c_int64()
+        self._check(self.L.fvo_debug_buffer(self.h, which, ctypes.byref(p), ctypes.byref(nb)))
+        torch.cuda.synchronize(self.device)
+        host = torch.empty((nb.value,), dtype=torch.uint8)
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        if hip.hipMemcpy(ctypes.c_void_p(host.data_ptr()), p, nb.value, 2) != 0:  # 2 = DeviceToHost
+            raise RuntimeError("hipMemcpy failed")
+        return host
+
+    def geometry(self):
+        """Pyramid level (w, h, offset) list, mirroring OpenCV ORB's layer sizes."""
+        import numpy as np
+        sf = float(np.float32(self.cfg.scale_factor))
+        out, off = [], 0
+        for l in range(self.cfg.nlevels):
+            s = np.float32(sf ** l)
+            inv = np.float32(1.0) / s
+            w = int(np.rint(np.float32(self.width) * inv))
+            h = int(np.rint(np.float32(self.height) * inv))
+            out.append((w, h, off))
+            off += w * h
+        return out, off
+
+    def test_retain_best(self, keys: torch.Tensor, keep: int):
+        keys = keys.to(self.device, torch.float32).contiguous()
+        n = keys.numel()
+        idx = torch.empty((max(n, 1),), dtype=torch.int32, device=self.device)
+        nout = torch.empty((1,), dtype=torch.int32, device=self.device)
+        self._check(self.L.fvo_test_retain_best(self.h, _ptr(keys), n, keep, _ptr(idx), _ptr(nout),
+                                                _stream(self.device)))
+        k = int(nout.item())
+        return idx[:k].clone()

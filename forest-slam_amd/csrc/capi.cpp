@@ -1,0 +1,163 @@
+// extern "C" entry points of libfvo.so (include/fvo.h).  Thin: argument checks, context
+// lifetime, dispatch to the per-stage launchers.  No allocation in the hot calls.
+#include <cstdio>
+#include <cstring>
+
+#include "fvo_internal.h"
+
+int fvo_fail(fvo_ctx* ctx, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return -1;
+}
+
+extern "C" {
+
+int fvo_abi_version(void) { return FVO_ABI_VERSION; }
+
+void fvo_config_default(fvo_config* c, int32_t width, int32_t height) {
+  std::memset(c, 0, sizeof(*c));
+  c->width = width;
+  c->height = height;
+  c->max_batch = 1;
+  c->nfeatures = 500;
+  c->scale_factor = 1.2f;
+  c->nlevels = 8;
+  c->edge_threshold = 31;
+  c->first_level = 0;
+  c->wta_k = 2;
+  c->score_type = 0;
+  c->patch_size = 31;
+  c->fast_threshold = 20;
+  c->min_disparity = 0;
+  c->num_disparities = 6 * 16;
+  c->block_size = 7;
+  c->P1 = 8 * 7 * 7;
+  c->P2 = 32 * 7 * 7;
+  c->disp12_max_diff = 0;
+  c->pre_filter_cap = 0;
+  c->uniqueness_ratio = 0;
+  c->sgbm_stripes = 4;
+  c->kp_capacity = 0;
+}
+
+static void release(fvo_ctx* c) {
+  void* ptrs[] = {c->pyr,        c->blur,      c->score,     c->rowcnt,   c->rowoff,  c->cand,     c->hel,
+                  c->ncand,      c->nsel1,     c->nsel2,     c->koff,     c->scratch, c->rt.xofs,  c->rt.xc1,
+                  c->rt.yofs,    c->rt.yc1,    c->umax,      c->bf_sidx,  c->bf_sdist, c->bf_tidx, c->sg_cost,
+                  c->sg_L,       c->sg_V,      c->sg_raw,    c->sg_d2,    c->sg_d2c,  c->pnp_hyp,  c->pnp_good,
+                  c->pnp_sub,    c->pnp_niters};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+}
+
+int fvo_create(int device, const fvo_config* cfg, fvo_ctx** out) {
+  if (!cfg || !out) return -1;
+  *out = nullptr;
+  fvo_ctx* c = new fvo_ctx();
+  c->device = device;
+  c->cfg = *cfg;
+  auto bail = [&](int rc) {
+    std::fprintf(stderr, "fvo_create: %s\n", c->err.c_str());
+    release(c);
+    delete c;
+    return rc;
+  };
+  if (hipSetDevice(device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(-1); }
+  if (cfg->width < 64 || cfg->height < 64 || cfg->max_batch < 1) { c->err = "bad image size or max_batch"; return bail(-1); }
+  int rc;
+  if ((rc = orb_init(c)) || (rc = bf_init(c)) || (rc = sgbm_init(c)) || (rc = pose_init(c))) return bail(rc);
+  *out = c;
+  return 0;
+}
+
+void fvo_destroy(fvo_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  release(c);
+  delete c;
+}
+
+const char* fvo_last_error(const fvo_ctx* c) { return c ? c->err.c_str() : "null context"; }
+int fvo_kp_capacity(const fvo_ctx* c) { return c ? c->kp_cap : 0; }
+int64_t fvo_workspace_bytes(const fvo_ctx* c) { return c ? c->ws_bytes : 0; }
+
+static int check_batch(fvo_ctx* c, int32_t batch) {
+  if (!c) return -1;
+  if (batch < 0 || batch > c->cfg.max_batch) return fvo_fail(c, "batch exceeds max_batch");
+  return 0;
+}
+
+int fvo_orb_detect_compute(fvo_ctx* c, const uint8_t* images, int32_t batch, int64_t image_stride, int32_t pitch,
+                           float* keypoints, uint8_t* descriptors, int32_t* counts, int32_t cap, fvo_stream stream) {
+  if (check_batch(c, batch)) return -1;
+  if (batch == 0) return 0;
+  if (!images || !keypoints || !descriptors || !counts) return fvo_fail(c, "null pointer argument");
+  if (pitch < c->cfg.width || image_stride < (int64_t)pitch * c->cfg.height) return fvo_fail(c, "bad pitch/stride");
+  if (cap < 1) return fvo_fail(c, "cap must be >= 1");
+  return orb_run(c, images, batch, image_stride, pitch, keypoints, descriptors, counts, cap, (hipStream_t)stream);
+}
+
+int fvo_bf_match(fvo_ctx* c, const uint8_t* query, const int32_t* n_query, const uint8_t* train,
+                 const int32_t* n_train, int32_t batch, int32_t cap, int32_t* matches, int32_t* n_matches,
+                 fvo_stream stream) {
+  if (check_batch(c, batch)) return -1;
+  if (batch == 0) return 0;
+  if (!query || !n_query || !train || !n_train || !matches || !n_matches) return fvo_fail(c, "null pointer argument");
+  if (cap < 1 || cap > c->kp_cap) return fvo_fail(c, "cap must be in [1, fvo_kp_capacity()]");
+  return bf_run(c, query, n_query, train, n_train, batch, cap, matches, n_matches, (hipStream_t)stream);
+}
+
+int fvo_sgbm(fvo_ctx* c, const uint8_t* left, const uint8_t* right, int32_t batch, int64_t image_stride,
+             int32_t pitch, int16_t* disparity, fvo_stream stream) {
+  if (check_batch(c, batch)) return -1;
+  if (batch == 0) return 0;
+  if (!left || !right || !disparity) return fvo_fail(c, "null pointer argument");
+  if (pitch < c->cfg.width || image_stride < (int64_t)pitch * c->cfg.height) return fvo_fail(c, "bad pitch/stride");
+  return sgbm_run(c, left, right, batch, image_stride, pitch, disparity, (hipStream_t)stream);
+}
+
+int fvo_backproject(fvo_ctx* c, const int16_t* disparity, const float* kp0, const float* kp1, const int32_t* matches,
+                    const int32_t* n_matches, int32_t batch, int32_t cap, const double* K, double baseline,
+                    double* points3d, float* points2d, int32_t* n_points, fvo_stream stream) {
+  if (check_batch(c, batch)) return -1;
+  if (batch == 0) return 0;
+  if (!disparity || !kp0 || !kp1 || !matches || !n_matches || !K || !points3d || !points2d || !n_points)
+    return fvo_fail(c, "null pointer argument");
+  if (cap < 1) return fvo_fail(c, "cap must be >= 1");
+  return backproject_run(c, disparity, kp0, kp1, matches, n_matches, batch, cap, K, baseline, points3d, points2d,
+                         n_points, (hipStream_t)stream);
+}
+
+int fvo_pnp_ransac(fvo_ctx* c, const double* points3d, const float* points2d, const int32_t* n_points, int32_t batch,
+                   int32_t cap, const double* K, const double* dist, float reprojection_error, double confidence,
+                   int32_t iterations, double* rvec, double* tvec, double* T, int32_t* status, uint8_t* inliers,
+                   fvo_stream stream) {
+  if (check_batch(c, batch)) return -1;
+  if (batch == 0) return 0;
+  if (!points3d || !points2d || !n_points || !K || !dist || !rvec || !tvec || !T || !status)
+    return fvo_fail(c, "null pointer argument");
+  if (cap < 1) return fvo_fail(c, "cap must be >= 1");
+  if (iterations < 1 || iterations > c->pnp_max_iters) return fvo_fail(c, "iterations out of range");
+  if (!(confidence > 0 && confidence < 1)) return fvo_fail(c, "confidence must be in (0,1)");
+  return pnp_run(c, points3d, points2d, n_points, batch, cap, K, dist, reprojection_error, confidence, iterations,
+                 rvec, tvec, T, status, inliers, (hipStream_t)stream);
+}
+
+// Debug/test hook: device pointer + size of an internal workspace buffer of the last call.
+// which: 0 pyramid, 1 blurred pyramid, 2 FAST score map (all [max_batch][total_px] u8),
+//        3 per-level candidate counts, 4 after retainBest(2n), 5 after retainBest(n) (i32 [B][L]).
+int fvo_debug_buffer(fvo_ctx* c, int which, void** ptr, int64_t* bytes) {
+  if (!c || !ptr || !bytes) return -1;
+  const int64_t B = c->cfg.max_batch;
+  switch (which) {
+    case 0: *ptr = c->pyr; *bytes = B * c->g.total_px; return 0;
+    case 1: *ptr = c->blur; *bytes = B * c->g.total_px; return 0;
+    case 2: *ptr = c->score; *bytes = B * c->g.total_px; return 0;
+    case 3: *ptr = c->ncand; *bytes = B * c->g.nlevels * 4; return 0;
+    case 4: *ptr = c->nsel1; *bytes = B * c->g.nlevels * 4; return 0;
+    case 5: *ptr = c->nsel2; *bytes = B * c->g.nlevels * 4; return 0;
+    default: return fvo_fail(c, "unknown debug buffer");
+  }
+}
+
+}  // extern "C"

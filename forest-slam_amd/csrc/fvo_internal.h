@@ -1,0 +1,126 @@
+// Internal declarations shared by the HIP translation units of libfvo.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/fvo.h"
+
+#define FVO_MAX_LEVELS 12
+
+// Pyramid geometry computed on the host exactly as OpenCV's ORB does
+// (orb.cpp detectAndCompute: getScale, cvRound(cols * (1.f/scale))).
+struct OrbGeom {
+  int nlevels;
+  int w[FVO_MAX_LEVELS], h[FVO_MAX_LEVELS];
+  float scale[FVO_MAX_LEVELS];         // layerScale
+  int64_t off[FVO_MAX_LEVELS + 1];      // plane offsets inside one image's pyramid
+  int row0[FVO_MAX_LEVELS + 1];         // first global row of each level
+  int nfeat[FVO_MAX_LEVELS];            // nfeaturesPerLevel
+  int64_t cand_off[FVO_MAX_LEVELS + 1]; // candidate-array offsets per level (per image)
+  int64_t total_px;
+  int total_rows;
+  int64_t cand_total;
+};
+
+// Constant tables for the INTER_LINEAR_EXACT pyramid resize (per level, per axis).
+struct ResizeTab {
+  int32_t* xofs;  // per level l>=1: w[l] entries: source index, -1 left clamp, -2 right clamp
+  int32_t* xc1;   // ufixedpoint16 weight of ofs+1 (weight of ofs is 256 - c1)
+  int32_t* yofs;
+  int32_t* yc1;
+  int64_t xoff[FVO_MAX_LEVELS], yoff[FVO_MAX_LEVELS];
+};
+
+struct fvo_ctx {
+  int device = 0;
+  fvo_config cfg{};
+  OrbGeom g{};
+  std::string err;
+  int kp_cap = 0;
+  int64_t ws_bytes = 0;
+  // ORB workspace (per image b < max_batch)
+  uint8_t* pyr = nullptr;     // [B][total_px]
+  uint8_t* blur = nullptr;    // [B][total_px]
+  uint8_t* score = nullptr;   // [B][total_px]
+  int32_t* rowcnt = nullptr;  // [B][total_rows]
+  int32_t* rowoff = nullptr;  // [B][total_rows]
+  uint32_t* cand = nullptr;   // [B][cand_total] packed (score<<24 | y<<12 | x)
+  uint64_t* hel = nullptr;    // [B][cand_total] (harris float bits << 32 | packed)
+  int32_t* ncand = nullptr;   // [B][L]
+  int32_t* nsel1 = nullptr;   // [B][L]
+  int32_t* nsel2 = nullptr;   // [B][L]
+  int32_t* koff = nullptr;    // [B][L+1]
+  int32_t* scratch = nullptr; // [B*L][2*maxcand] selection position lists
+  int64_t scratch_per = 0;
+  ResizeTab rt{};
+  int32_t* umax = nullptr;    // IC angle row extents
+  // BF workspace
+  int32_t* bf_sidx = nullptr; // [B][cap]
+  int32_t* bf_sdist = nullptr;
+  int32_t* bf_tidx = nullptr;
+  // SGBM workspace
+  uint16_t* sg_cost = nullptr;  // [B][H + extra][width1][D]
+  uint16_t* sg_L = nullptr;     // [B][H][width1][D] left->right pass
+  uint16_t* sg_V = nullptr;     // [B][H][width1][D] top-down pass (output rows)
+  int16_t* sg_raw = nullptr;    // [B][H][W] pre-median disparity
+  int16_t* sg_d2 = nullptr;     // [B][H][W] right-view disparity (pseudo LR check)
+  int32_t* sg_d2c = nullptr;    // [B][H][W] packed cost/x for disp2
+  int sg_extra_rows = 0;
+  // pose workspace
+  double* pnp_hyp = nullptr;    // [B][iters][6]
+  int32_t* pnp_good = nullptr;  // [B][iters]
+  int32_t* pnp_sub = nullptr;   // [B][iters][5]
+  int32_t* pnp_niters = nullptr; // [B]
+  int32_t pnp_max_iters = 0;
+};
+
+// Error helpers: set ctx->err and return negative status.
+int fvo_fail(fvo_ctx* ctx, const std::string& msg);
+#define FVO_HIP(ctx, expr)                                                                 \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess) return fvo_fail(ctx, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define FVO_LAUNCH_CHECK(ctx) FVO_HIP(ctx, hipGetLastError())
+
+// Per-module init/launchers (defined in the .hip files).
+int orb_init(fvo_ctx* ctx);
+int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride, int pitch, float* kp, uint8_t* desc,
+            int32_t* counts, int cap, hipStream_t s);
+int bf_init(fvo_ctx* ctx);
+int bf_run(fvo_ctx* ctx, const uint8_t* q, const int32_t* nq, const uint8_t* t, const int32_t* nt, int batch, int cap,
+           int32_t* matches, int32_t* nmatch, hipStream_t s);
+int sgbm_init(fvo_ctx* ctx);
+int sgbm_run(fvo_ctx* ctx, const uint8_t* L, const uint8_t* R, int batch, int64_t image_stride, int pitch,
+             int16_t* disp, hipStream_t s);
+int pose_init(fvo_ctx* ctx);
+int backproject_run(fvo_ctx* ctx, const int16_t* disp, const float* kp0, const float* kp1, const int32_t* matches,
+                    const int32_t* nmatch, int batch, int cap, const double* K, double baseline, double* P3, float* p2,
+                    int32_t* npts, hipStream_t s);
+int pnp_run(fvo_ctx* ctx, const double* P3, const float* p2, const int32_t* npts, int batch, int cap, const double* K,
+            const double* dist, float reproj, double conf, int iters, double* rvec, double* tvec, double* T,
+            int32_t* status, uint8_t* inliers, hipStream_t s);
+
+template <typename T>
+int fvo_alloc(fvo_ctx* ctx, T** p, size_t n) {
+  size_t bytes = n * sizeof(T);
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc((void**)p, bytes);
+  if (e != hipSuccess) return fvo_fail(ctx, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+  ctx->ws_bytes += (int64_t)bytes;
+  return 0;
+}
+
+// ---------------------------------------------------------------- device helpers
+__device__ __forceinline__ int wave_lane() { return (int)(threadIdx.x & 63); }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}

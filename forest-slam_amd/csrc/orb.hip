@@ -1,0 +1,861 @@
+// ORB detectAndCompute for gfx950 — replaces cv2.ORB_create() + orb.detectAndCompute
+// (ros_ws/src/stereo_slam.py:84, :232-233, :240-241).  Batched over images.
+//
+// Stages (one launch each, all images of the batch at once):
+//   pyramid      level 0 copy + 7 INTER_LINEAR_EXACT downscales (ufixedpoint16 weights)
+//   fast_score   FAST-9/16 corner test + cornerScore<16> -> u8 score map (all levels)
+//   nms_count    3x3 strict-max NMS + 31-px border filter, per-row counts
+//   row_scan     per-level exclusive scan of row counts
+//   nms_compact  ordered (row-major) compaction -> packed candidates (score<<24|y<<12|x)
+//   select       KeyPointsFilter::retainBest(2n_l) — block-parallel, bit-identical to
+//                libstdc++'s nth_element + partition element order (see select_block)
+//   harris       7x7 Harris response per candidate (wave per keypoint)
+//   select       retainBest(n_l) on the Harris responses
+//   finalize     per-image level offsets / counts
+//   angle        intensity-centroid angle (fastAtan2) + keypoint records
+//   blur         GaussianBlur 7x7 sigma 2 (8-bit fixed-point separable, REFLECT_101)
+//   brief        steered rBRIEF, one wave per keypoint, 4 ballots = 32 bytes
+// All float expressions are evaluated in the order OpenCV writes them; the library is
+// compiled with -ffp-contract=off so no FMA contraction changes a rounding.
+#include <cmath>
+#include <cstring>
+
+#include "fvo_internal.h"
+#include "orb_pattern.inc"
+
+namespace {
+
+__constant__ int c_row0[FVO_MAX_LEVELS + 1];
+__constant__ int c_w[FVO_MAX_LEVELS];
+__constant__ int c_h[FVO_MAX_LEVELS];
+__constant__ long long c_off[FVO_MAX_LEVELS + 1];
+__constant__ long long c_cand_off[FVO_MAX_LEVELS + 1];
+__constant__ float c_scale[FVO_MAX_LEVELS];
+__constant__ int c_nfeat[FVO_MAX_LEVELS];
+__constant__ int c_umax[20];
+__constant__ signed char c_pattern[256 * 4];
+
+constexpr int kSelThreads = 512;
+
+__device__ __forceinline__ int level_of_row(int r, int nlevels) {
+  int l = 0;
+#pragma unroll
+  for (int k = 1; k < FVO_MAX_LEVELS; ++k)
+    if (k < nlevels && r >= c_row0[k]) l = k;
+  return l;
+}
+
+// ------------------------------------------------------------------ pyramid
+__global__ void k_copy_level0(const uint8_t* __restrict__ img, int64_t stride, int pitch, uint8_t* __restrict__ pyr,
+                              int64_t total, int W, int H) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x;
+  int y = blockIdx.y;
+  int b = blockIdx.z;
+  if (x >= W) return;
+  pyr[b * total + (int64_t)y * W + x] = img[b * stride + (int64_t)y * pitch + x];
+}
+
+__global__ void k_resize(uint8_t* __restrict__ pyr, int64_t total, int l, const int32_t* __restrict__ xofs,
+                         const int32_t* __restrict__ xc1, const int32_t* __restrict__ yofs,
+                         const int32_t* __restrict__ yc1) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x;
+  int y = blockIdx.y;
+  int b = blockIdx.z;
+  int w = c_w[l];
+  if (x >= w) return;
+  int sw = c_w[l - 1], sh = c_h[l - 1];
+  const uint8_t* src = pyr + b * total + c_off[l - 1];
+  uint8_t* dst = pyr + b * total + c_off[l];
+  int ox = xofs[x], cx1 = xc1[x], cx0 = 256 - cx1;
+  auto hrow = [&](int r) -> uint32_t {
+    const uint8_t* s = src + (int64_t)r * sw;
+    if (ox == -1) return (uint32_t)s[0] << 8;
+    if (ox == -2) return (uint32_t)s[sw - 1] << 8;
+    return (uint32_t)cx0 * s[ox] + (uint32_t)cx1 * s[ox + 1];
+  };
+  int oy = yofs[y];
+  uint32_t v;
+  if (oy < 0) {
+    v = (hrow(oy == -1 ? 0 : sh - 1) + 128u) >> 8;
+  } else {
+    int cy1 = yc1[y], cy0 = 256 - cy1;
+    v = (hrow(oy) * (uint32_t)cy0 + hrow(oy + 1) * (uint32_t)cy1 + 32768u) >> 16;
+  }
+  dst[(int64_t)y * w + x] = (uint8_t)(v > 255u ? 255u : v);
+}
+
+// ------------------------------------------------------------------ FAST
+__constant__ int c_cdx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+__constant__ int c_cdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+
+__global__ void k_fast_score(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ score, int64_t total, int nlevels,
+                             int thr) {
+  int r = blockIdx.y;
+  int l = level_of_row(r, nlevels);
+  int y = r - c_row0[l];
+  int x = blockIdx.x * blockDim.x + threadIdx.x;
+  int w = c_w[l], h = c_h[l];
+  if (x >= w) return;
+  int b = blockIdx.z;
+  const uint8_t* im = pyr + b * total + c_off[l];
+  uint8_t* sc = score + b * total + c_off[l];
+  int out = 0;
+  if (x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
+    int v = im[(int64_t)y * w + x];
+    int p[16];
+    unsigned bright = 0, dark = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      p[k] = im[(int64_t)(y + c_cdy[k]) * w + x + c_cdx[k]];
+      bright |= (unsigned)(p[k] > v + thr) << k;
+      dark |= (unsigned)(p[k] < v - thr) << k;
+    }
+    auto has9 = [](unsigned m) {
+      unsigned mm = m | (m << 16);
+      unsigned c = mm;
+#pragma unroll
+      for (int j = 1; j <= 8; ++j) c &= mm >> j;
+      return (c & 0xFFFFu) != 0;
+    };
+    if (has9(bright) || has9(dark)) {
+      // cornerScore<16>: max(t, max over 9-arcs of min(v-p), max over 9-arcs of min(p-v)) - 1
+      int a0 = thr, b0 = thr;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        int mn = 1 << 20, mx = 1 << 20;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+          int d = v - p[(s + j) & 15];
+          mn = min(mn, d);
+          mx = min(mx, -d);
+        }
+        a0 = max(a0, mn);
+        b0 = max(b0, mx);
+      }
+      out = max(a0, b0) - 1;
+    }
+  }
+  sc[(int64_t)y * w + x] = (uint8_t)out;
+}
+
+__device__ __forceinline__ bool nms_keep(const uint8_t* sc, int w, int x, int y) {
+  const uint8_t* p = sc + (int64_t)y * w + x;
+  int s = p[0];
+  if (!s) return false;
+  return s > p[-w - 1] && s > p[-w] && s > p[-w + 1] && s > p[-1] && s > p[1] && s > p[w - 1] && s > p[w] &&
+         s > p[w + 1];
+}
+
+__global__ void k_nms_count(const uint8_t* __restrict__ score, int32_t* __restrict__ rowcnt, int64_t total,
+                            int total_rows, int nlevels, int edge) {
+  int r = blockIdx.x;
+  int b = blockIdx.y;
+  int l = level_of_row(r, nlevels);
+  int y = r - c_row0[l];
+  int w = c_w[l], h = c_h[l];
+  __shared__ int s_part[16];
+  int cnt = 0;
+  if (y >= edge && y < h - edge) {
+    const uint8_t* sc = score + b * total + c_off[l];
+    for (int x = edge + (int)threadIdx.x; x < w - edge; x += blockDim.x) cnt += nms_keep(sc, w, x, y);
+  }
+  cnt = wave_sum(cnt);
+  if (wave_lane() == 0) s_part[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += s_part[i];
+    rowcnt[(int64_t)b * total_rows + r] = t;
+  }
+}
+
+__global__ void k_row_scan(const int32_t* __restrict__ rowcnt, int32_t* __restrict__ rowoff,
+                           int32_t* __restrict__ ncand, int total_rows, int nlevels) {
+  int l = blockIdx.x, b = blockIdx.y;
+  int r0 = c_row0[l], h = c_h[l];
+  const int32_t* rc = rowcnt + (int64_t)b * total_rows + r0;
+  int32_t* ro = rowoff + (int64_t)b * total_rows + r0;
+  __shared__ int s_w[16];
+  __shared__ int s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (int base = 0; base < h; base += blockDim.x) {
+    int i = base + threadIdx.x;
+    int v = i < h ? rc[i] : 0;
+    int inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      int t = __shfl_up(inc, o, 64);
+      if (wave_lane() >= o) inc += t;
+    }
+    if (wave_lane() == 63) s_w[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    int wpre = 0, tot = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+      if (k < (int)(threadIdx.x >> 6)) wpre += s_w[k];
+      tot += s_w[k];
+    }
+    if (i < h) ro[i] = s_carry + wpre + inc - v;
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ncand[b * nlevels + l] = s_carry;
+}
+
+__global__ void k_nms_compact(const uint8_t* __restrict__ score, const int32_t* __restrict__ rowoff,
+                              uint32_t* __restrict__ cand, int64_t total, int64_t cand_total, int total_rows,
+                              int nlevels, int edge) {
+  int r = blockIdx.x;
+  int b = blockIdx.y;
+  int l = level_of_row(r, nlevels);
+  int y = r - c_row0[l];
+  int w = c_w[l], h = c_h[l];
+  if (y < edge || y >= h - edge) return;
+  const uint8_t* sc = score + b * total + c_off[l];
+  uint32_t* out = cand + b * cand_total + c_cand_off[l];
+  __shared__ int s_w[16];
+  __shared__ int s_carry;
+  if (threadIdx.x == 0) s_carry = rowoff[(int64_t)b * total_rows + r];
+  __syncthreads();
+  for (int base = edge; base < w - edge; base += blockDim.x) {
+    int x = base + threadIdx.x;
+    bool k = x < w - edge && nms_keep(sc, w, x, y);
+    unsigned long long m = __ballot(k);
+    int pre = __popcll(m & ((1ull << wave_lane()) - 1ull));
+    if (wave_lane() == 0) s_w[threadIdx.x >> 6] = __popcll(m);
+    __syncthreads();
+    int wpre = 0, tot = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+      if (i < (int)(threadIdx.x >> 6)) wpre += s_w[i];
+      tot += s_w[i];
+    }
+    if (k) {
+      uint32_t s = sc[(int64_t)y * w + x];
+      out[s_carry + wpre + pre] = (s << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry += tot;
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ retainBest
+// Element views: key() is the KeyPoint.response the comparator looks at.
+struct ElemFast {
+  typedef uint32_t T;
+  __device__ static float key(uint32_t e) { return (float)(e >> 24); }
+};
+struct ElemHarris {
+  typedef uint64_t T;
+  __device__ static float key(uint64_t e) { return __uint_as_float((uint32_t)(e >> 32)); }
+};
+
+struct SelShared {
+  int wsum[2][kSelThreads / 64];
+  int carry[2];
+  int cnt;
+  int lo, hi, cut;
+};
+
+// Block-wide two-flag exclusive scan; returns prefixes, updates per-flag running carries
+// (uniform), tot[] = chunk totals.
+__device__ __forceinline__ void scan2(SelShared& sh, int f0, int f1, int& p0, int& p1) {
+  const int lane = wave_lane(), wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  unsigned long long m0 = __ballot(f0), m1 = __ballot(f1);
+  unsigned long long below = (1ull << lane) - 1ull;
+  int w0 = __popcll(m0 & below), w1 = __popcll(m1 & below);
+  if (lane == 0) { sh.wsum[0][wid] = __popcll(m0); sh.wsum[1][wid] = __popcll(m1); }
+  __syncthreads();
+  int a0 = 0, a1 = 0, t0 = 0, t1 = 0;
+  for (int i = 0; i < nw; ++i) {
+    int v0 = sh.wsum[0][i], v1 = sh.wsum[1][i];
+    if (i < wid) { a0 += v0; a1 += v1; }
+    t0 += v0; t1 += v1;
+  }
+  p0 = sh.carry[0] + a0 + w0;
+  p1 = sh.carry[1] + a1 + w1;
+  __syncthreads();
+  if (threadIdx.x == 0) { sh.carry[0] += t0; sh.carry[1] += t1; }
+  __syncthreads();
+}
+
+__device__ __forceinline__ int block_count(SelShared& sh, int f) {
+  unsigned long long m = __ballot(f);
+  if (wave_lane() == 0) sh.wsum[0][threadIdx.x >> 6] = __popcll(m);
+  __syncthreads();
+  int t = 0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh.wsum[0][i];
+  __syncthreads();
+  return t;
+}
+
+// Compact positions i in [first,last) with predicate A (ascending into SA) and B
+// (ascending into SB).  Returns counts.
+template <class E, class PA, class PB>
+__device__ void compact2(SelShared& sh, const typename E::T* a, int first, int last, int* SA, int* SB, PA pa, PB pb,
+                         int& nA, int& nB) {
+  if (threadIdx.x == 0) { sh.carry[0] = 0; sh.carry[1] = 0; }
+  __syncthreads();
+  for (int base = first; base < last; base += blockDim.x) {
+    int i = base + threadIdx.x;
+    int fa = 0, fb = 0;
+    if (i < last) {
+      float k = E::key(a[i]);
+      fa = pa(k);
+      fb = pb(k);
+    }
+    int p0, p1;
+    scan2(sh, fa, fb, p0, p1);
+    if (fa) SA[p0] = i;
+    if (fb) SB[p1] = i;
+  }
+  nA = sh.carry[0];
+  nB = sh.carry[1];
+  __syncthreads();
+}
+
+// Pair the k-th A position (ascending) with the k-th B position from the right while
+// A_k < B_k; swap each pair.  This is exactly the set of swaps a sequential Hoare scan
+// (libstdc++ __unguarded_partition / bidirectional __partition) performs.  Returns k*.
+template <class E>
+__device__ int pair_swap(SelShared& sh, typename E::T* a, const int* SA, int nA, const int* SB, int nB) {
+  int m = min(nA, nB);
+  int c = 0;
+  for (int base = 0; base < m; base += blockDim.x) {
+    int k = base + threadIdx.x;
+    int f = k < m && SA[k] < SB[nB - 1 - k];
+    c += block_count(sh, f);
+  }
+  for (int k = threadIdx.x; k < c; k += blockDim.x) {
+    int i = SA[k], j = SB[nB - 1 - k];
+    typename E::T t = a[i];
+    a[i] = a[j];
+    a[j] = t;
+  }
+  __syncthreads();
+  return c;
+}
+
+// ---- serial pieces (lane 0), libstdc++ semantics with comp(x,y) = key(x) > key(y)
+template <class E>
+__device__ void move_median_to_first(typename E::T* a, int result, int ia, int ib, int ic) {
+  auto cmp = [&](int x, int y) { return E::key(a[x]) > E::key(a[y]); };
+  auto sw = [&](int x, int y) { typename E::T t = a[x]; a[x] = a[y]; a[y] = t; };
+  if (cmp(ia, ib)) {
+    if (cmp(ib, ic)) sw(result, ib);
+    else if (cmp(ia, ic)) sw(result, ic);
+    else sw(result, ia);
+  } else if (cmp(ia, ic)) sw(result, ia);
+  else if (cmp(ib, ic)) sw(result, ic);
+  else sw(result, ib);
+}
+
+template <class E>
+__device__ void insertion_sort(typename E::T* a, int first, int last) {
+  if (first == last) return;
+  for (int i = first + 1; i != last; ++i) {
+    typename E::T v = a[i];
+    float kv = E::key(v);
+    if (kv > E::key(a[first])) {
+      for (int j = i; j > first; --j) a[j] = a[j - 1];
+      a[first] = v;
+    } else {
+      int j = i, nx = i - 1;
+      while (kv > E::key(a[nx])) { a[j] = a[nx]; j = nx; --nx; }
+      a[j] = v;
+    }
+  }
+}
+
+template <class E>
+__device__ void adjust_heap(typename E::T* f, int hole, int len, typename E::T value) {
+  const int top = hole;
+  int second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (E::key(f[second]) > E::key(f[second - 1])) second--;
+    f[hole] = f[second];
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    f[hole] = f[second - 1];
+    hole = second - 1;
+  }
+  int parent = (hole - 1) / 2;
+  float kv = E::key(value);
+  while (hole > top && E::key(f[parent]) > kv) {
+    f[hole] = f[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  f[hole] = value;
+}
+
+template <class E>
+__device__ void heap_select(typename E::T* a, int first, int middle, int last) {
+  typename E::T* f = a + first;
+  int len = middle - first;
+  if (len >= 2) {
+    for (int parent = (len - 2) / 2;; --parent) {
+      adjust_heap<E>(f, parent, len, f[parent]);
+      if (parent == 0) break;
+    }
+  }
+  for (int i = middle; i < last; ++i) {
+    if (E::key(a[i]) > E::key(f[0])) {
+      typename E::T v = a[i];
+      a[i] = f[0];
+      adjust_heap<E>(f, 0, len, v);
+    }
+  }
+}
+
+__device__ __forceinline__ int ilog2(int n) { return 31 - __clz(n); }
+
+// KeyPointsFilter::retainBest(a[0..n), keep) executed by one workgroup.  Returns the
+// surviving count; a[] is left in OpenCV's element order.
+template <class E>
+__device__ int select_block(SelShared& sh, typename E::T* a, int n, int keep, int* SA, int* SB) {
+  if (keep < 0 || n <= keep) return n;
+  if (keep == 0) return 0;
+  const int nth = keep - 1;
+  int lo = 0, hi = n, depth = 2 * ilog2(n);
+  bool heaped = false;
+  while (hi - lo > 3) {
+    if (depth == 0) {
+      if (threadIdx.x == 0) {
+        heap_select<E>(a, lo, nth + 1, hi);
+        typename E::T t = a[lo]; a[lo] = a[nth]; a[nth] = t;
+      }
+      __syncthreads();
+      heaped = true;
+      break;
+    }
+    --depth;
+    if (threadIdx.x == 0) move_median_to_first<E>(a, lo, lo + 1, lo + (hi - lo) / 2, hi - 1);
+    __syncthreads();
+    const float P = E::key(a[lo]);
+    int nL, nR;
+    compact2<E>(sh, a, lo + 1, hi, SA, SB, [P](float k) { return k <= P; }, [P](float k) { return k >= P; }, nL, nR);
+    int ks = pair_swap<E>(sh, a, SA, nL, SB, nR);
+    int Lk = ks < nL ? SA[ks] : hi;
+    int Rk = ks > 0 ? SB[nR - ks] : hi;
+    int cut = min(Lk, Rk);
+    if (cut <= nth) lo = cut; else hi = cut;
+  }
+  if (!heaped) {
+    if (threadIdx.x == 0) insertion_sort<E>(a, lo, hi);
+    __syncthreads();
+  }
+  const float amb = E::key(a[nth]);
+  int nF, nG;
+  compact2<E>(sh, a, keep, n, SA, SB, [amb](float k) { return !(k >= amb); }, [amb](float k) { return k >= amb; },
+              nF, nG);
+  pair_swap<E>(sh, a, SA, nF, SB, nG);
+  return keep + nG;
+}
+
+template <class E>
+__global__ __launch_bounds__(kSelThreads) void k_select(typename E::T* __restrict__ arr,
+                                                        const int32_t* __restrict__ nin, int32_t* __restrict__ nout,
+                                                        int32_t* __restrict__ scratch, int64_t scratch_per,
+                                                        int64_t cand_total, int nlevels, int keep_mult) {
+  int l = blockIdx.x, b = blockIdx.y;
+  __shared__ SelShared sh;
+  typename E::T* a = arr + b * cand_total + c_cand_off[l];
+  int n = nin[b * nlevels + l];
+  int* SA = scratch + (int64_t)(b * nlevels + l) * scratch_per;
+  int* SB = SA + scratch_per / 2;
+  int r = select_block<E>(sh, a, n, keep_mult * c_nfeat[l], SA, SB);
+  if (threadIdx.x == 0) nout[b * nlevels + l] = r;
+}
+
+// ------------------------------------------------------------------ Harris
+__global__ void k_harris(const uint8_t* __restrict__ pyr, const uint32_t* __restrict__ cand,
+                         const int32_t* __restrict__ nsel, uint64_t* __restrict__ hel, int64_t total,
+                         int64_t cand_total, int nlevels) {
+  int l = blockIdx.y, b = blockIdx.z;
+  int n = nsel[b * nlevels + l];
+  int wpb = blockDim.x >> 6;
+  int lane = wave_lane();
+  const uint8_t* im = pyr + b * total + c_off[l];
+  int w = c_w[l];
+  const uint32_t* cin = cand + b * cand_total + c_cand_off[l];
+  uint64_t* hout = hel + b * cand_total + c_cand_off[l];
+  for (int i = blockIdx.x * wpb + (threadIdx.x >> 6); i < n; i += gridDim.x * wpb) {
+    uint32_t e = cin[i];
+    int x0 = e & 0xFFF, y0 = (e >> 12) & 0xFFF;
+    int A = 0, B = 0, C = 0;
+    if (lane < 49) {
+      int x = x0 - 3 + lane % 7, y = y0 - 3 + lane / 7;
+      const uint8_t* p = im + (int64_t)y * w + x;
+      int Ix = (p[1] - p[-1]) * 2 + (p[-w + 1] - p[-w - 1]) + (p[w + 1] - p[w - 1]);
+      int Iy = (p[w] - p[-w]) * 2 + (p[w - 1] - p[-w - 1]) + (p[w + 1] - p[-w + 1]);
+      A = Ix * Ix; B = Iy * Iy; C = Ix * Iy;
+    }
+    A = wave_sum(A); B = wave_sum(B); C = wave_sum(C);
+    if (lane == 0) {
+      const float harris_k = 0.04f;
+      const float scale = 1.f / ((1 << 2) * 7 * 255.f);
+      const float sss = scale * scale * scale * scale;
+      float resp = ((float)A * B - (float)C * C - harris_k * ((float)A + B) * ((float)A + B)) * sss;
+      hout[i] = ((uint64_t)__float_as_uint(resp) << 32) | e;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ finalize + angle
+__global__ void k_offsets(const int32_t* __restrict__ nsel2, int32_t* __restrict__ koff, int32_t* __restrict__ counts,
+                          int batch, int nlevels, int cap) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  int s = 0;
+  for (int l = 0; l < nlevels; ++l) {
+    koff[b * (nlevels + 1) + l] = s;
+    s += nsel2[b * nlevels + l];
+  }
+  koff[b * (nlevels + 1) + nlevels] = s;
+  counts[b] = s <= cap ? s : -s;
+}
+
+__device__ __forceinline__ float fast_atan2_deg(float y, float x) {
+  const float k = (float)(180 / 3.14159265358979323846);
+  const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k, p5 = 0.1555786518463281f * k,
+              p7 = -0.04432655554792128f * k;
+  const float eps = (float)2.220446049250313080847e-16;
+  float ax = fabsf(x), ay = fabsf(y), a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + eps);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = ax / (ay + eps);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+__global__ void k_angle(const uint8_t* __restrict__ pyr, const uint64_t* __restrict__ hel,
+                        const int32_t* __restrict__ nsel2, const int32_t* __restrict__ koff, float* __restrict__ kp,
+                        int64_t total, int64_t cand_total, int nlevels, int cap, int patch) {
+  int l = blockIdx.y, b = blockIdx.z;
+  int n = nsel2[b * nlevels + l];
+  int base = koff[b * (nlevels + 1) + l];
+  int wpb = blockDim.x >> 6, lane = wave_lane();
+  const uint8_t* im = pyr + b * total + c_off[l];
+  int w = c_w[l];
+  const uint64_t* hin = hel + b * cand_total + c_cand_off[l];
+  const int half = patch / 2;
+  for (int i = blockIdx.x * wpb + (threadIdx.x >> 6); i < n; i += gridDim.x * wpb) {
+    if (base + i >= cap) break;
+    uint64_t e = hin[i];
+    int x0 = (int)(e & 0xFFF), y0 = (int)((e >> 12) & 0xFFF);
+    float resp = __uint_as_float((uint32_t)(e >> 32));
+    const uint8_t* c = im + (int64_t)y0 * w + x0;
+    int m10 = 0, m01 = 0;
+    int u = lane - half;
+    if (lane <= 2 * half) {
+      m10 += u * c[u];
+      for (int v = 1; v <= half; ++v) {
+        int d = c_umax[v];
+        if (u >= -d && u <= d) {
+          int vp = c[u + v * w], vm = c[u - v * w];
+          m01 += v * (vp - vm);
+          m10 += u * (vp + vm);
+        }
+      }
+    }
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    if (lane == 0) {
+      float s = c_scale[l];
+      float* o = kp + ((int64_t)b * cap + base + i) * FVO_KP_STRIDE;
+      o[0] = (float)x0 * s;
+      o[1] = (float)y0 * s;
+      o[2] = patch * s;
+      o[3] = fast_atan2_deg((float)m01, (float)m10);
+      o[4] = resp;
+      o[5] = (float)l;
+      o[6] = -1.f;
+      o[7] = 0.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ Gaussian blur
+__constant__ int c_gk[7] = {18, 34, 49, 55, 49, 34, 18};
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * n - 2 - i : i;
+}
+
+__global__ void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, int64_t total, int nlevels) {
+  int r = blockIdx.y;
+  int l = level_of_row(r, nlevels);
+  int y = r - c_row0[l];
+  int x = blockIdx.x * blockDim.x + threadIdx.x;
+  int w = c_w[l], h = c_h[l];
+  if (x >= w) return;
+  int b = blockIdx.z;
+  const uint8_t* im = pyr + b * total + c_off[l];
+  int xs[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) xs[k] = reflect101(x + k - 3, w);
+  int s = 0;
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const uint8_t* row = im + (int64_t)reflect101(y + j - 3, h) * w;
+    int rs = 0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) rs += c_gk[k] * row[xs[k]];
+    s += c_gk[j] * rs;
+  }
+  int q = (s + 32767 + ((s >> 16) & 1)) >> 16;  // round half to even
+  blur[b * total + c_off[l] + (int64_t)y * w + x] = (uint8_t)min(q, 255);
+}
+
+// ------------------------------------------------------------------ rBRIEF
+__global__ void k_brief(const uint8_t* __restrict__ blur, const float* __restrict__ kp, const int32_t* __restrict__ counts,
+                        uint8_t* __restrict__ desc, int64_t total, int cap) {
+  int b = blockIdx.y;
+  int n = counts[b];
+  if (n < 0) return;
+  int wpb = blockDim.x >> 6, lane = wave_lane();
+  for (int j = blockIdx.x * wpb + (threadIdx.x >> 6); j < n; j += gridDim.x * wpb) {
+    const float* k = kp + ((int64_t)b * cap + j) * FVO_KP_STRIDE;
+    int l = (int)k[5];
+    float scale = 1.f / c_scale[l];
+    float angle = k[3];
+    angle *= (float)(3.14159265358979323846 / 180.f);
+    float a = (float)cos((double)angle), bb = (float)sin((double)angle);
+    int cy = (int)rintf(k[1] * scale), cx = (int)rintf(k[0] * scale);
+    int w = c_w[l];
+    const uint8_t* c = blur + b * total + c_off[l] + (int64_t)cy * w + cx;
+    unsigned long long words[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int pi = q * 64 + lane;
+      int v[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float px = (float)c_pattern[pi * 4 + 2 * s], py = (float)c_pattern[pi * 4 + 2 * s + 1];
+        float xx = px * a - py * bb;
+        float yy = px * bb + py * a;
+        int ix = (int)rintf(xx), iy = (int)rintf(yy);
+        v[s] = c[iy * w + ix];
+      }
+      words[q] = __ballot(v[0] < v[1]);
+    }
+    if (lane < 4) {
+      unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+      reinterpret_cast<unsigned long long*>(desc + ((int64_t)b * cap + j) * FVO_DESC_BYTES)[lane] = wv;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host geometry
+static int cv_round_f(float v) { return (int)lrintf(v); }
+
+}  // namespace
+
+int orb_init(fvo_ctx* ctx) {
+  const fvo_config& c = ctx->cfg;
+  OrbGeom& g = ctx->g;
+  if (c.nlevels < 1 || c.nlevels > FVO_MAX_LEVELS) return fvo_fail(ctx, "nlevels out of range");
+  if (c.first_level != 0 || c.wta_k != 2 || c.score_type != 0 || c.patch_size != 31)
+    return fvo_fail(ctx, "only firstLevel=0, WTA_K=2, HARRIS_SCORE, patchSize=31 are supported");
+  if (c.width > 4095 || c.height > 4095) return fvo_fail(ctx, "image dimensions must be < 4096");
+  g.nlevels = c.nlevels;
+  const double sf = (double)c.scale_factor;
+  int64_t off = 0, coff = 0;
+  int row = 0;
+  for (int l = 0; l < c.nlevels; ++l) {
+    float s = (float)std::pow(sf, (double)l);
+    float inv = 1.0f / s;
+    g.scale[l] = s;
+    g.w[l] = cv_round_f((float)c.width * inv);
+    g.h[l] = cv_round_f((float)c.height * inv);
+    g.off[l] = off;
+    off += (int64_t)g.w[l] * g.h[l];
+    g.row0[l] = row;
+    row += g.h[l];
+    int rw = std::max(g.w[l] - 2 * c.edge_threshold, 0), rh = std::max(g.h[l] - 2 * c.edge_threshold, 0);
+    g.cand_off[l] = coff;
+    coff += (int64_t)((rw + 1) / 2) * ((rh + 1) / 2) + 1;
+  }
+  g.off[c.nlevels] = off;
+  g.row0[c.nlevels] = row;
+  g.cand_off[c.nlevels] = coff;
+  g.total_px = off;
+  g.total_rows = row;
+  g.cand_total = coff;
+  {
+    float factor = (float)(1.0 / sf);
+    float nd = c.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)c.nlevels));
+    int sum = 0;
+    for (int l = 0; l < c.nlevels - 1; ++l) {
+      g.nfeat[l] = cv_round_f(nd);
+      sum += g.nfeat[l];
+      nd *= factor;
+    }
+    g.nfeat[c.nlevels - 1] = std::max(c.nfeatures - sum, 0);
+  }
+  ctx->kp_cap = c.kp_capacity > 0 ? c.kp_capacity : 2 * c.nfeatures + 64;
+
+  // resize tables (levels 1..L-1), INTER_LINEAR_EXACT coefficient rule
+  std::vector<int32_t> xo, xc, yo, yc;
+  auto coeffs = [](int src, int dst, std::vector<int32_t>& ofs, std::vector<int32_t>& c1) {
+    double inv_scale = (double)dst / (double)src;
+    double scale = 1.0 / inv_scale;
+    for (int d = 0; d < dst; ++d) {
+      double fval = scale * ((double)d + 0.5) - 0.5;
+      int ival = (int)std::floor(fval);
+      if (ival >= 0 && src > 1) {
+        if (ival < src - 1) {
+          double frac = fval - (double)ival;
+          ofs.push_back(ival);
+          c1.push_back(frac < 0 ? 0 : (int)std::llrint(frac * 256.0));
+        } else {
+          ofs.push_back(-2);
+          c1.push_back(0);
+        }
+      } else {
+        ofs.push_back(-1);
+        c1.push_back(0);
+      }
+    }
+  };
+  for (int l = 1; l < c.nlevels; ++l) {
+    ctx->rt.xoff[l] = (int64_t)xo.size();
+    coeffs(g.w[l - 1], g.w[l], xo, xc);
+    ctx->rt.yoff[l] = (int64_t)yo.size();
+    coeffs(g.h[l - 1], g.h[l], yo, yc);
+  }
+  if (xo.empty()) { xo.push_back(0); xc.push_back(0); yo.push_back(0); yc.push_back(0); }
+  int rc = 0;
+  if ((rc = fvo_alloc(ctx, &ctx->rt.xofs, xo.size())) || (rc = fvo_alloc(ctx, &ctx->rt.xc1, xc.size())) ||
+      (rc = fvo_alloc(ctx, &ctx->rt.yofs, yo.size())) || (rc = fvo_alloc(ctx, &ctx->rt.yc1, yc.size())))
+    return rc;
+  FVO_HIP(ctx, hipMemcpy(ctx->rt.xofs, xo.data(), xo.size() * 4, hipMemcpyHostToDevice));
+  FVO_HIP(ctx, hipMemcpy(ctx->rt.xc1, xc.data(), xc.size() * 4, hipMemcpyHostToDevice));
+  FVO_HIP(ctx, hipMemcpy(ctx->rt.yofs, yo.data(), yo.size() * 4, hipMemcpyHostToDevice));
+  FVO_HIP(ctx, hipMemcpy(ctx->rt.yc1, yc.data(), yc.size() * 4, hipMemcpyHostToDevice));
+
+  // IC-angle row extents (orb.cpp computeKeyPoints: umax + symmetry fix-up)
+  int half = c.patch_size / 2;
+  std::vector<int> umax(half + 2 > 20 ? half + 2 : 20, 0);
+  int vmax = (int)std::floor(half * std::sqrt(2.f) / 2 + 1);
+  int vmin = (int)std::ceil(half * std::sqrt(2.f) / 2);
+  for (int v = 0; v <= vmax; ++v) umax[v] = (int)std::lrint(std::sqrt((double)half * half - v * v));
+  for (int v = half, v0 = 0; v >= vmin; --v) {
+    while (umax[v0] == umax[v0 + 1]) ++v0;
+    umax[v] = v0;
+    ++v0;
+  }
+
+  long long offs[FVO_MAX_LEVELS + 1], coffs[FVO_MAX_LEVELS + 1];
+  for (int l = 0; l <= c.nlevels; ++l) { offs[l] = g.off[l]; coffs[l] = g.cand_off[l]; }
+  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_row0), g.row0, sizeof(int) * (c.nlevels + 1)));
+  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_w), g.w, sizeof(int) * c.nlevels));
+  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_h), g.h, sizeof(int) * c.nlevels));
+  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_off), offs, sizeof(long long) * (c.nlevels + 1)));
+  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_cand_off), coffs, sizeof(long long) * (c.nlevels + 1)));
+  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_scale), g.scale, sizeof(float) * c.nlevels));
+  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_nfeat), g.nfeat, sizeof(int) * c.nlevels));
+  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax.data(), sizeof(int) * 20));
+  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), FVO_ORB_PATTERN, sizeof(FVO_ORB_PATTERN)));
+
+  const int64_t B = c.max_batch;
+  int64_t maxcand = 0;
+  for (int l = 0; l < c.nlevels; ++l) maxcand = std::max<int64_t>(maxcand, g.cand_off[l + 1] - g.cand_off[l]);
+  ctx->scratch_per = 2 * maxcand;
+  if ((rc = fvo_alloc(ctx, &ctx->pyr, B * g.total_px)) || (rc = fvo_alloc(ctx, &ctx->blur, B * g.total_px)) ||
+      (rc = fvo_alloc(ctx, &ctx->score, B * g.total_px)) || (rc = fvo_alloc(ctx, &ctx->rowcnt, B * g.total_rows)) ||
+      (rc = fvo_alloc(ctx, &ctx->rowoff, B * g.total_rows)) || (rc = fvo_alloc(ctx, &ctx->cand, B * g.cand_total)) ||
+      (rc = fvo_alloc(ctx, &ctx->hel, B * g.cand_total)) || (rc = fvo_alloc(ctx, &ctx->ncand, B * c.nlevels)) ||
+      (rc = fvo_alloc(ctx, &ctx->nsel1, B * c.nlevels)) || (rc = fvo_alloc(ctx, &ctx->nsel2, B * c.nlevels)) ||
+      (rc = fvo_alloc(ctx, &ctx->koff, B * (c.nlevels + 1))) ||
+      (rc = fvo_alloc(ctx, &ctx->scratch, B * c.nlevels * ctx->scratch_per)))
+    return rc;
+  return 0;
+}
+
+int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride, int pitch, float* kp, uint8_t* desc,
+            int32_t* counts, int cap, hipStream_t s) {
+  const fvo_config& c = ctx->cfg;
+  const OrbGeom& g = ctx->g;
+  const int L = g.nlevels;
+  const int W = c.width, H = c.height;
+  const int64_t total = g.total_px;
+  const int thr = std::min(std::max(c.fast_threshold, 0), 255);
+  hipLaunchKernelGGL(k_copy_level0, dim3((W + 255) / 256, H, batch), dim3(256), 0, s, images, image_stride, pitch,
+                     ctx->pyr, total, W, H);
+  for (int l = 1; l < L; ++l)
+    hipLaunchKernelGGL(k_resize, dim3((g.w[l] + 255) / 256, g.h[l], batch), dim3(256), 0, s, ctx->pyr, total, l,
+                       ctx->rt.xofs + ctx->rt.xoff[l], ctx->rt.xc1 + ctx->rt.xoff[l], ctx->rt.yofs + ctx->rt.yoff[l],
+                       ctx->rt.yc1 + ctx->rt.yoff[l]);
+  hipLaunchKernelGGL(k_fast_score, dim3((W + 255) / 256, g.total_rows, batch), dim3(256), 0, s, ctx->pyr, ctx->score,
+                     total, L, thr);
+  hipLaunchKernelGGL(k_nms_count, dim3(g.total_rows, batch), dim3(256), 0, s, ctx->score, ctx->rowcnt, total,
+                     g.total_rows, L, c.edge_threshold);
+  hipLaunchKernelGGL(k_row_scan, dim3(L, batch), dim3(256), 0, s, ctx->rowcnt, ctx->rowoff, ctx->ncand, g.total_rows,
+                     L);
+  hipLaunchKernelGGL(k_nms_compact, dim3(g.total_rows, batch), dim3(256), 0, s, ctx->score, ctx->rowoff, ctx->cand,
+                     total, g.cand_total, g.total_rows, L, c.edge_threshold);
+  hipLaunchKernelGGL(k_select<ElemFast>, dim3(L, batch), dim3(kSelThreads), 0, s, ctx->cand, ctx->ncand, ctx->nsel1,
+                     ctx->scratch, ctx->scratch_per, g.cand_total, L, 2);
+  hipLaunchKernelGGL(k_harris, dim3(32, L, batch), dim3(256), 0, s, ctx->pyr, ctx->cand, ctx->nsel1, ctx->hel, total,
+                     g.cand_total, L);
+  hipLaunchKernelGGL(k_select<ElemHarris>, dim3(L, batch), dim3(kSelThreads), 0, s, ctx->hel, ctx->nsel1, ctx->nsel2,
+                     ctx->scratch, ctx->scratch_per, g.cand_total, L, 1);
+  hipLaunchKernelGGL(k_offsets, dim3((batch + 63) / 64), dim3(64), 0, s, ctx->nsel2, ctx->koff, counts, batch, L, cap);
+  hipLaunchKernelGGL(k_angle, dim3(16, L, batch), dim3(256), 0, s, ctx->pyr, ctx->hel, ctx->nsel2, ctx->koff, kp,
+                     total, g.cand_total, L, cap, c.patch_size);
+  hipLaunchKernelGGL(k_blur, dim3((W + 255) / 256, g.total_rows, batch), dim3(256), 0, s, ctx->pyr, ctx->blur, total,
+                     L);
+  hipLaunchKernelGGL(k_brief, dim3(64, batch), dim3(256), 0, s, ctx->blur, kp, counts, desc, total, cap);
+  FVO_LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+// ------------------------------------------------------------------ test hook
+namespace {
+__global__ void k_pack_keys(const float* __restrict__ k, uint64_t* __restrict__ a, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = ((uint64_t)__float_as_uint(k[i]) << 32) | (uint32_t)i;
+}
+__global__ void k_unpack_idx(const uint64_t* __restrict__ a, int32_t* __restrict__ idx, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) idx[i] = (int32_t)(uint32_t)a[i];
+}
+__global__ __launch_bounds__(kSelThreads) void k_select_test(uint64_t* __restrict__ a, int n, int keep,
+                                                             int32_t* __restrict__ scratch, int32_t* __restrict__ out_n) {
+  __shared__ SelShared sh;
+  int r = select_block<ElemHarris>(sh, a, n, keep, scratch, scratch + n);
+  if (threadIdx.x == 0) *out_n = r;
+}
+}  // namespace
+
+// retainBest on n float keys (device memory); writes surviving original indices in
+// output order to idx_out and the count to *n_out.  Test hook for the selection stage.
+extern "C" int fvo_test_retain_best(fvo_ctx* ctx, const float* keys, int32_t n, int32_t keep, int32_t* idx_out,
+                                    int32_t* n_out, fvo_stream stream) {
+  hipStream_t s = (hipStream_t)stream;
+  uint64_t* a = nullptr;
+  int32_t* scr = nullptr;
+  FVO_HIP(ctx, hipMallocAsync((void**)&a, sizeof(uint64_t) * (size_t)std::max(n, 1), s));
+  FVO_HIP(ctx, hipMallocAsync((void**)&scr, sizeof(int32_t) * 2 * (size_t)std::max(n, 1), s));
+  hipLaunchKernelGGL(k_pack_keys, dim3((n + 255) / 256 + 1), dim3(256), 0, s, keys, a, n);
+  hipLaunchKernelGGL(k_select_test, dim3(1), dim3(kSelThreads), 0, s, a, n, keep, scr, n_out);
+  hipLaunchKernelGGL(k_unpack_idx, dim3((n + 255) / 256 + 1), dim3(256), 0, s, a, idx_out, n);
+  FVO_HIP(ctx, hipFreeAsync(a, s));
+  FVO_HIP(ctx, hipFreeAsync(scr, s));
+  FVO_LAUNCH_CHECK(ctx);
+  return 0;
+}

@@ -1,0 +1,147 @@
+/* fvo.h — C ABI of the MI355X stereo-VO hot path (forest-slam_amd, libfvo.so).
+ *
+ * Drop-in boundary for the OpenCV calls of si220/Forest-SLAM's ORB branch
+ * (ros_ws/src/stereo_slam.py).  Every entry point replaces one reference call:
+ *
+ *   fvo_orb_detect_compute  <- cv2.ORB_create() + orb.detectAndCompute(img, None)
+ *                              stereo_slam.py:84, :232-233, :240-241
+ *   fvo_bf_match            <- cv2.BFMatcher(cv2.NORM_HAMMING, crossCheck=True).match(d0, d1)
+ *                              stereo_slam.py:85, :234, :242 (+ the :235-238 gather)
+ *   fvo_sgbm                <- cv2.StereoSGBM_create(numDisparities=96, minDisparity=0,
+ *                              blockSize=7, P1=392, P2=1568, mode=SGBM_3WAY).compute(L, R)
+ *                              stereo_slam.py:108-117 (get_disparity_map)
+ *   fvo_backproject         <- depth = fx*B/disp, Z = depth[int(y), int(x)], X/Y, 0.1<Z<1000
+ *                              stereo_slam.py:117-121 (0/-1 -> 0.1) and :262-289
+ *   fvo_pnp_ransac          <- cv2.solvePnPRansac(P, p, K0, dist_l, reprojectionError=1.0,
+ *                              confidence=0.99, iterationsCount=1000, SOLVEPNP_ITERATIVE)
+ *                              + cv2.Rodrigues + T assembly, stereo_slam.py:292-303
+ *   fvo_ba_window           <- (new) windowed bundle adjustment, no reference counterpart
+ *
+ * Conventions
+ *  - All array pointers are DEVICE pointers owned by the caller (e.g. torch tensors'
+ *    data_ptr()).  Calls are asynchronous on `stream` (a hipStream_t, may be NULL for
+ *    the default stream); counts and statuses are written to device memory.
+ *  - Every call works on a BATCH of independent items (images / image pairs / frames);
+ *    `batch` <= fvo_config.max_batch.
+ *  - Return value: 0 on success, <0 on argument/launch error (see fvo_last_error()).
+ *    No exceptions cross this boundary.  Data-dependent failures (too few points,
+ *    capacity overflow) are reported per item in the status/count outputs.
+ *  - A context is not re-entrant: one context per (device, host thread).  All device
+ *    workspace is allocated by fvo_create(); hot calls do not allocate and can be
+ *    captured into a hipGraph.
+ */
+#ifndef FVO_H_
+#define FVO_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FVO_ABI_VERSION 1
+
+typedef struct fvo_ctx fvo_ctx;
+typedef void* fvo_stream; /* hipStream_t */
+
+/* Keypoint record written by fvo_orb_detect_compute (8 x float32 per keypoint):
+ * x, y (level-0 pixels), size, angle (deg), response (Harris), octave, class_id (-1), 0 */
+#define FVO_KP_STRIDE 8
+#define FVO_DESC_BYTES 32
+
+typedef struct fvo_config {
+  int32_t width, height; /* image size shared by every call on this context         */
+  int32_t max_batch;     /* max images (ORB) / pairs (BF, SGBM) / frames (pose) per call */
+  /* cv2.ORB_create() parameters; defaults = OpenCV defaults (stereo_slam.py:84) */
+  int32_t nfeatures;       /* 500 */
+  float scale_factor;      /* 1.2f */
+  int32_t nlevels;         /* 8 */
+  int32_t edge_threshold;  /* 31 */
+  int32_t first_level;     /* 0 (only 0 supported) */
+  int32_t wta_k;           /* 2 (only 2 supported) */
+  int32_t score_type;      /* 0 = HARRIS_SCORE (only Harris supported) */
+  int32_t patch_size;      /* 31 (only 31 supported: the rBRIEF table) */
+  int32_t fast_threshold;  /* 20 */
+  /* cv2.StereoSGBM_create() parameters used at stereo_slam.py:109-115 */
+  int32_t min_disparity;    /* 0 */
+  int32_t num_disparities;  /* 96, multiple of 16 */
+  int32_t block_size;       /* 7 */
+  int32_t P1, P2;           /* 392, 1568 */
+  int32_t disp12_max_diff;  /* 0 (-> 1 as in OpenCV) */
+  int32_t pre_filter_cap;   /* 0 (-> 15) */
+  int32_t uniqueness_ratio; /* 0 (only 0 supported) */
+  int32_t sgbm_stripes;     /* 4: OpenCV's fixed stripe count for MODE_SGBM_3WAY */
+  int32_t kp_capacity;      /* per-image keypoint capacity of the ORB outputs (0 = auto) */
+} fvo_config;
+
+/* Fill `cfg` with the reference's parameters for a width x height image. */
+void fvo_config_default(fvo_config* cfg, int32_t width, int32_t height);
+
+int fvo_create(int device, const fvo_config* cfg, fvo_ctx** out);
+void fvo_destroy(fvo_ctx* ctx);
+const char* fvo_last_error(const fvo_ctx* ctx);
+int fvo_abi_version(void);
+/* Per-image keypoint capacity (rows of the keypoint/descriptor outputs). */
+int fvo_kp_capacity(const fvo_ctx* ctx);
+/* Device workspace bytes held by the context. */
+int64_t fvo_workspace_bytes(const fvo_ctx* ctx);
+
+/* ORB detectAndCompute on `batch` grayscale u8 images.
+ * images:      batch images, image b at images + b*image_stride, rows `pitch` bytes apart.
+ * keypoints:   [batch][cap][FVO_KP_STRIDE] f32     descriptors: [batch][cap][32] u8
+ * counts:      [batch] i32 = number of keypoints, or -(needed) if it exceeds `cap`
+ *              (outputs then unspecified).  Keypoint order = OpenCV's output order. */
+int fvo_orb_detect_compute(fvo_ctx* ctx, const uint8_t* images, int32_t batch, int64_t image_stride,
+                           int32_t pitch, float* keypoints, uint8_t* descriptors, int32_t* counts,
+                           int32_t cap, fvo_stream stream);
+
+/* Cross-checked brute-force Hamming matching of `batch` (query, train) descriptor sets.
+ * query/train: [batch][cap][32] u8 with per-item counts n_query/n_train [batch] (<=0: empty).
+ * matches:     [batch][cap][3] i32 rows (queryIdx, trainIdx, distance), ascending queryIdx.
+ * n_matches:   [batch] i32. */
+int fvo_bf_match(fvo_ctx* ctx, const uint8_t* query, const int32_t* n_query, const uint8_t* train,
+                 const int32_t* n_train, int32_t batch, int32_t cap, int32_t* matches, int32_t* n_matches,
+                 fvo_stream stream);
+
+/* StereoSGBM 3-way disparity (incl. the final 3x3 median) of `batch` rectified pairs.
+ * disparity: [batch][height][width] i16, disparity*16, invalid = (min_disparity-1)*16. */
+int fvo_sgbm(fvo_ctx* ctx, const uint8_t* left, const uint8_t* right, int32_t batch, int64_t image_stride,
+             int32_t pitch, int16_t* disparity, fvo_stream stream);
+
+/* Matched-keypoint back-projection through the disparity map (stereo_slam.py:262-289).
+ * kp0/kp1:   keypoint records of the previous / current left images ([batch][cap][8]).
+ * matches:   fvo_bf_match output (query = previous, train = current).
+ * K:         host double[9] row-major camera matrix; baseline in metres.
+ * points3d:  [batch][cap][3] f64 valid points (0.1 < Z < 1000), compacted in match order.
+ * points2d:  [batch][cap][2] f32 matching current-image keypoints.  n_points: [batch]. */
+int fvo_backproject(fvo_ctx* ctx, const int16_t* disparity, const float* kp0, const float* kp1,
+                    const int32_t* matches, const int32_t* n_matches, int32_t batch, int32_t cap, const double* K,
+                    double baseline, double* points3d, float* points2d, int32_t* n_points, fvo_stream stream);
+
+/* solvePnPRansac(SOLVEPNP_ITERATIVE) + Rodrigues on `batch` independent frames.
+ * K, dist:   host double[9] / double[5] (k1 k2 p1 p2 k3).
+ * rvec/tvec: [batch][3] f64.   T: [batch][16] f64 row-major [R|t;0 0 0 1].
+ * status:    [batch] i32: 1 pose valid, 0 RANSAC failed, -1 skipped (n_points < 6,
+ *            the reference's `len(points3D) >= 6` guard, stereo_slam.py:292).
+ * inliers:   [batch][cap] u8 RANSAC inlier mask (may be NULL). */
+int fvo_pnp_ransac(fvo_ctx* ctx, const double* points3d, const float* points2d, const int32_t* n_points,
+                   int32_t batch, int32_t cap, const double* K, const double* dist, float reprojection_error,
+                   double confidence, int32_t iterations, double* rvec, double* tvec, double* T, int32_t* status,
+                   uint8_t* inliers, fvo_stream stream);
+
+/* Test hook: KeyPointsFilter::retainBest on `n` float responses (device memory) with the
+ * product's selection kernel.  idx_out [n] receives the surviving original indices in
+ * OpenCV's output order, *n_out the survivor count.  Allocates (stream-ordered). */
+int fvo_test_retain_best(fvo_ctx* ctx, const float* keys, int32_t n, int32_t keep, int32_t* idx_out, int32_t* n_out,
+                         fvo_stream stream);
+
+/* Debug hook: device pointer and byte size of an internal buffer of the most recent ORB
+ * call (0 pyramid, 1 blurred pyramid, 2 FAST score map, 3/4/5 per-level counts before /
+ * after the two retainBest passes).  For stage-by-stage parity tests only. */
+int fvo_debug_buffer(fvo_ctx* ctx, int which, void** ptr, int64_t* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FVO_H_ */
