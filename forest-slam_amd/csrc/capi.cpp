@@ -118,7 +118,7 @@ int fvo_sgbm(fvo_ctx* c, const uint8_t* left, const uint8_t* right, int32_t batc
 
 int fvo_backproject(fvo_ctx* c, const int16_t* disparity, const float* kp0, const float* kp1, const int32_t* matches,
                     const int32_t* n_matches, int32_t batch, int32_t cap, const double* K, double baseline,
-                    double* points3d, float* points2d, int32_t* n_points, fvo_stream stream) {
+                    float* points3d, float* points2d, int32_t* n_points, fvo_stream stream) {
   if (check_batch(c, batch)) return -1;
   if (batch == 0) return 0;
   if (!disparity || !kp0 || !kp1 || !matches || !n_matches || !K || !points3d || !points2d || !n_points)
@@ -128,7 +128,7 @@ int fvo_backproject(fvo_ctx* c, const int16_t* disparity, const float* kp0, cons
                          n_points, (hipStream_t)stream);
 }
 
-int fvo_pnp_ransac(fvo_ctx* c, const double* points3d, const float* points2d, const int32_t* n_points, int32_t batch,
+int fvo_pnp_ransac(fvo_ctx* c, const float* points3d, const float* points2d, const int32_t* n_points, int32_t batch,
                    int32_t cap, const double* K, const double* dist, float reprojection_error, double confidence,
                    int32_t iterations, double* rvec, double* tvec, double* T, int32_t* status, uint8_t* inliers,
                    fvo_stream stream) {

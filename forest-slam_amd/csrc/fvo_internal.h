@@ -99,9 +99,9 @@ int sgbm_run(fvo_ctx* ctx, const uint8_t* L, const uint8_t* R, int batch, int64_
              int16_t* disp, hipStream_t s);
 int pose_init(fvo_ctx* ctx);
 int backproject_run(fvo_ctx* ctx, const int16_t* disp, const float* kp0, const float* kp1, const int32_t* matches,
-                    const int32_t* nmatch, int batch, int cap, const double* K, double baseline, double* P3, float* p2,
+                    const int32_t* nmatch, int batch, int cap, const double* K, double baseline, float* P3, float* p2,
                     int32_t* npts, hipStream_t s);
-int pnp_run(fvo_ctx* ctx, const double* P3, const float* p2, const int32_t* npts, int batch, int cap, const double* K,
+int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts, int batch, int cap, const double* K,
             const double* dist, float reproj, double conf, int iters, double* rvec, double* tvec, double* T,
             int32_t* status, uint8_t* inliers, hipStream_t s);
 

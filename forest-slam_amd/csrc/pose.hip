@@ -1,7 +1,997 @@
-// placeholder replaced below
+// Pose stage for gfx950 — replaces ros_ws/src/stereo_slam.py:262-303:
+//   depth / back-projection of the matched previous-frame keypoints (:262-289), then
+//   cv2.solvePnPRansac(points3D, mkpts1_l, K0, dist_l, 1.0, 0.99, 1000, ITERATIVE) and
+//   cv2.Rodrigues -> T (:294-303).
+//
+// k_backproject  one thread per match, float32 arithmetic in NumPy 1.x order
+//                (the reference environment's value-based casting),
+//                ordered compaction of 0.1 < Z < 1000 (block scan), one block per frame.
+// k_pnp          one wavefront per frame.  RANSAC iterations are evaluated 64 at a time:
+//                lane 0 draws the subsets with OpenCV's RNG(-1) (the draws depend only on
+//                the point count), every lane solves EPnP for its subset and scores it over
+//                all points; lane 0 then replays OpenCV's sequential acceptance rule
+//                (goodCount > max(best, 4), adaptive niters) over the chunk, so the
+//                winning hypothesis and the iteration count are those of the serial loop.
+//                Refinement: DLT (or homography for planar sets) + Levenberg-Marquardt
+//                (CvLevMarq: lambda 1e-3, 20 iterations, eps FLT_EPSILON) with the
+//                per-point Jacobian rows accumulated across lanes.
+// All pose math is fp64 (as in OpenCV); compiled with -ffp-contract=off.
+#include <cfloat>
+
 #include "fvo_internal.h"
-int pose_init(fvo_ctx* ctx) { ctx->pnp_max_iters = 1000; return 0; }
-int backproject_run(fvo_ctx* ctx, const int16_t*, const float*, const float*, const int32_t*, const int32_t*, int, int,
-                    const double*, double, double*, float*, int32_t*, hipStream_t) { return fvo_fail(ctx, "todo"); }
-int pnp_run(fvo_ctx* ctx, const double*, const float*, const int32_t*, int, int, const double*, const double*, float,
-            double, int, double*, double*, double*, int32_t*, uint8_t*, hipStream_t) { return fvo_fail(ctx, "todo"); }
+
+namespace {
+
+constexpr int kChunk = 64;
+
+// ------------------------------------------------------------------ back-projection
+struct CamF {
+  double fx, fy, cx, cy, fxB;
+};
+
+__global__ void k_backproject(const int16_t* __restrict__ disp, const float* __restrict__ kp0,
+                              const float* __restrict__ kp1, const int32_t* __restrict__ matches,
+                              const int32_t* __restrict__ nmatch, int W, int H, int cap, CamF K,
+                              float* __restrict__ P3, float* __restrict__ p2, int32_t* __restrict__ npts) {
+  const int b = blockIdx.x;
+  int n = nmatch[b];
+  n = n < 0 ? 0 : (n > cap ? cap : n);
+  __shared__ int s_w[16];
+  __shared__ int s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  const float fxB = (float)K.fxB, fcx = (float)K.cx, fcy = (float)K.cy, ffx = (float)K.fx, ffy = (float)K.fy;
+  const float lo = (float)0.1, hi = 1000.f;
+  for (int base = 0; base < n; base += blockDim.x) {
+    int i = base + threadIdx.x;
+    bool keep = false;
+    float X = 0, Y = 0, Z = 0, u = 0, v = 0;
+    if (i < n) {
+      const int32_t* m = matches + ((int64_t)b * cap + i) * 3;
+      const float* a = kp0 + ((int64_t)b * cap + m[0]) * FVO_KP_STRIDE;
+      const float* c = kp1 + ((int64_t)b * cap + m[1]) * FVO_KP_STRIDE;
+      float x = a[0], y = a[1];
+      int xi = (int)x, yi = (int)y;
+      xi = min(max(xi, 0), W - 1);
+      yi = min(max(yi, 0), H - 1);
+      float d = (float)disp[((int64_t)b * H + yi) * W + xi] / 16.f;
+      if (d == 0.0f) d = lo;
+      if (d == -1.0f) d = lo;
+      Z = fxB / d;
+      X = ((x - fcx) / ffx) * Z;
+      Y = ((y - fcy) / ffy) * Z;
+      keep = (Z > lo) && (Z < hi);
+      u = c[0];
+      v = c[1];
+    }
+    unsigned long long mk = __ballot(keep);
+    int pre = __popcll(mk & ((1ull << wave_lane()) - 1ull));
+    if (wave_lane() == 0) s_w[threadIdx.x >> 6] = __popcll(mk);
+    __syncthreads();
+    int wpre = 0, tot = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+      if (k < (int)(threadIdx.x >> 6)) wpre += s_w[k];
+      tot += s_w[k];
+    }
+    if (keep) {
+      int o = s_carry + wpre + pre;
+      float* P = P3 + ((int64_t)b * cap + o) * 3;
+      P[0] = X;
+      P[1] = Y;
+      P[2] = Z;
+      p2[((int64_t)b * cap + o) * 2] = u;
+      p2[((int64_t)b * cap + o) * 2 + 1] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) npts[b] = s_carry;
+}
+
+// ------------------------------------------------------------------ small fp64 linear algebra
+// A (m x n row-major, m >= n) = U diag(W) V^T, W descending (one-sided Jacobi).
+template <int M, int N>
+__device__ void dsvd(const double* A, double* W, double* U, double* V) {
+  double u[M * N], v[N * N], w[N];
+  for (int i = 0; i < M * N; ++i) u[i] = A[i];
+  for (int i = 0; i < N * N; ++i) v[i] = (i % (N + 1) == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0;
+    for (int p = 0; p < N - 1; ++p)
+      for (int q = p + 1; q < N; ++q) {
+        double a = 0, bb = 0, g = 0;
+        for (int i = 0; i < M; ++i) {
+          double up = u[i * N + p], uq = u[i * N + q];
+          a += up * up;
+          bb += uq * uq;
+          g += up * uq;
+        }
+        if (g == 0.0 || fabs(g) <= 1e-300) continue;
+        double rel = fabs(g) / sqrt(a * bb);
+        off = fmax(off, rel);
+        if (rel < 1e-15) continue;
+        double zeta = (bb - a) / (2.0 * g);
+        double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+        for (int i = 0; i < M; ++i) {
+          double up = u[i * N + p], uq = u[i * N + q];
+          u[i * N + p] = c * up - s * uq;
+          u[i * N + q] = s * up + c * uq;
+        }
+        for (int i = 0; i < N; ++i) {
+          double vp = v[i * N + p], vq = v[i * N + q];
+          v[i * N + p] = c * vp - s * vq;
+          v[i * N + q] = s * vp + c * vq;
+        }
+      }
+    if (off < 1e-15) break;
+  }
+  int ord[N];
+  for (int j = 0; j < N; ++j) {
+    double s = 0;
+    for (int i = 0; i < M; ++i) s += u[i * N + j] * u[i * N + j];
+    w[j] = sqrt(s);
+    ord[j] = j;
+  }
+  for (int i = 1; i < N; ++i) {  // stable insertion sort, descending
+    int k = ord[i], j = i;
+    while (j > 0 && w[ord[j - 1]] < w[k]) { ord[j] = ord[j - 1]; --j; }
+    ord[j] = k;
+  }
+  for (int jj = 0; jj < N; ++jj) {
+    int j = ord[jj];
+    W[jj] = w[j];
+    double inv = w[j] > 0 ? 1.0 / w[j] : 0.0;
+    for (int i = 0; i < M; ++i) U[i * N + jj] = u[i * N + j] * inv;
+    for (int i = 0; i < N; ++i) V[i * N + jj] = v[i * N + j];
+  }
+}
+
+template <int M, int N>
+__device__ void dsolve(const double* A, const double* b, double* x) {
+  double W[N], U[M * N], V[N * N], tmp[N];
+  dsvd<M, N>(A, W, U, V);
+  double thr = DBL_EPSILON * (M > N ? M : N) * W[0];
+  for (int j = 0; j < N; ++j) {
+    tmp[j] = 0.0;
+    if (W[j] <= thr) continue;
+    double s = 0;
+    for (int i = 0; i < M; ++i) s += U[i * N + j] * b[i];
+    tmp[j] = s / W[j];
+  }
+  for (int i = 0; i < N; ++i) {
+    double s = 0;
+    for (int j = 0; j < N; ++j) s += V[i * N + j] * tmp[j];
+    x[i] = s;
+  }
+}
+
+__device__ double ddet3(const double* R) {
+  return R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) + R[2] * (R[3] * R[7] - R[4] * R[6]);
+}
+
+// ------------------------------------------------------------------ camera / Rodrigues
+struct Cam {
+  double fx, fy, cx, cy, k[5];
+};
+
+__device__ void rod_r2R(const double* r, double* R, double* J) {
+  double th = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+  if (th < DBL_EPSILON) {
+    for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    if (J) {
+      const double J0[27] = {0, 0, 0, 0, 0, 1, 0, -1, 0, 0, 0, -1, 0, 0, 0, 1, 0, 0, 0, 1, 0, -1, 0, 0, 0, 0, 0};
+      for (int i = 0; i < 27; ++i) J[i] = J0[i];
+    }
+    return;
+  }
+  double c = cos(th), s = sin(th), c1 = 1.0 - c, it = 1.0 / th;
+  double x = r[0] * it, y = r[1] * it, z = r[2] * it;
+  double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};
+  double rx[9] = {0, -z, y, z, 0, -x, -y, x, 0};
+  const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  for (int k = 0; k < 9; ++k) R[k] = c * I[k] + c1 * rrt[k] + s * rx[k];
+  if (J) {
+    double drrt[27] = {x + x, y, z, y, 0, 0, z, 0, 0, 0, x, 0, x, y + y, z, 0, z, 0, 0, 0, x, 0, 0, y, x, y, z + z};
+    const double drx[27] = {0, 0, 0, 0, 0, -1, 0, 1, 0, 0, 0, 1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 1, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 3; ++i) {
+      double ri = i == 0 ? x : i == 1 ? y : z;
+      double a0 = -s * ri, a1 = (s - 2 * c1 * it) * ri, a2 = c1 * it, a3 = (c - s * it) * ri, a4 = s * it;
+      for (int k = 0; k < 9; ++k)
+        J[i * 9 + k] = a0 * I[k] + a1 * rrt[k] + a2 * drrt[i * 9 + k] + a3 * rx[k] + a4 * drx[i * 9 + k];
+    }
+  }
+}
+
+__device__ void rod_R2r(const double* Rin, double* r) {
+  double W[3], U[9], V[9], R[9];
+  dsvd<3, 3>(Rin, W, U, V);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) R[i * 3 + j] = U[i * 3] * V[j * 3] + U[i * 3 + 1] * V[j * 3 + 1] + U[i * 3 + 2] * V[j * 3 + 2];
+  double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+  double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+  double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+  c = c > 1. ? 1. : c < -1. ? -1. : c;
+  double th = acos(c);
+  if (s < 1e-5) {
+    if (c > 0) {
+      rx = ry = rz = 0;
+    } else {
+      double t = (R[0] + 1) * 0.5;
+      rx = sqrt(fmax(t, 0.));
+      t = (R[4] + 1) * 0.5;
+      ry = sqrt(fmax(t, 0.)) * (R[1] < 0 ? -1. : 1.);
+      t = (R[8] + 1) * 0.5;
+      rz = sqrt(fmax(t, 0.)) * (R[2] < 0 ? -1. : 1.);
+      if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+      th /= sqrt(rx * rx + ry * ry + rz * rz);
+      rx *= th; ry *= th; rz *= th;
+    }
+  } else {
+    double vth = 1 / (2 * s);
+    vth *= th;
+    rx *= vth; ry *= vth; rz *= vth;
+  }
+  r[0] = rx; r[1] = ry; r[2] = rz;
+}
+
+// projectPoints (k1 k2 p1 p2 k3) for one point; J (2x6) optional.
+__device__ void dproject(const Cam& K, const double* R, const double* dRdr, const double* t, const double* M,
+                         double* uv, double* J) {
+  double X = M[0], Y = M[1], Z = M[2];
+  double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+  double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+  double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+  z = z ? 1. / z : 1;
+  x *= z;
+  y *= z;
+  const double* k = K.k;
+  double r2 = x * x + y * y, r4 = r2 * r2, r6 = r4 * r2;
+  double a1 = 2 * x * y, a2 = r2 + 2 * x * x, a3 = r2 + 2 * y * y;
+  double cdist = 1 + k[0] * r2 + k[1] * r4 + k[4] * r6;
+  double xd = x * cdist + k[2] * a1 + k[3] * a2;
+  double yd = y * cdist + k[2] * a3 + k[3] * a1;
+  uv[0] = xd * K.fx + K.cx;
+  uv[1] = yd * K.fy + K.cy;
+  if (!J) return;
+  for (int j = 0; j < 6; ++j) {
+    double dxd, dyd;
+    if (j < 3) {
+      double dx0 = X * dRdr[j * 9 + 0] + Y * dRdr[j * 9 + 1] + Z * dRdr[j * 9 + 2];
+      double dy0 = X * dRdr[j * 9 + 3] + Y * dRdr[j * 9 + 4] + Z * dRdr[j * 9 + 5];
+      double dz0 = X * dRdr[j * 9 + 6] + Y * dRdr[j * 9 + 7] + Z * dRdr[j * 9 + 8];
+      dxd = z * (dx0 - x * dz0);
+      dyd = z * (dy0 - y * dz0);
+    } else {
+      dxd = j == 3 ? z : j == 4 ? 0.0 : -x * z;
+      dyd = j == 3 ? 0.0 : j == 4 ? z : -y * z;
+    }
+    double dr2 = 2 * x * dxd + 2 * y * dyd;
+    double dcd = k[0] * dr2 + 2 * k[1] * r2 * dr2 + 3 * k[4] * r4 * dr2;
+    double da1 = 2 * (x * dyd + y * dxd);
+    J[j] = K.fx * (dxd * cdist + x * dcd + k[2] * da1 + k[3] * (dr2 + 4 * x * dxd));
+    J[6 + j] = K.fy * (dyd * cdist + y * dcd + k[2] * (dr2 + 4 * y * dyd) + k[3] * da1);
+  }
+}
+
+__device__ void dundistort(const Cam& K, double u, double v, double* xy) {
+  const double ifx = 1. / K.fx, ify = 1. / K.fy;
+  double x = (u - K.cx) * ifx, y = (v - K.cy) * ify;
+  double x0 = x, y0 = y;
+  const double* k = K.k;
+  for (int j = 0; j < 5; ++j) {
+    double r2 = x * x + y * y;
+    double icdist = 1. / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+    if (icdist < 0) {
+      x = (u - K.cx) * ifx;
+      y = (v - K.cy) * ify;
+      break;
+    }
+    double dx = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x);
+    double dy = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y;
+    x = (x0 - dx) * icdist;
+    y = (y0 - dy) * icdist;
+  }
+  xy[0] = x;
+  xy[1] = y;
+}
+
+// ------------------------------------------------------------------ EPnP (5 points)
+__device__ __forceinline__ double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ __forceinline__ double dist2(const double* a, const double* b) {
+  return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
+}
+
+template <int NP>
+struct EPnPd {
+  double fu, fv, uc, vc;
+  double pws[3 * NP], us[2 * NP], alphas[4 * NP], pcs[3 * NP];
+  double cws[4][3], ccs[4][3];
+
+  __device__ void choose_control_points() {
+    for (int j = 0; j < 3; ++j) cws[0][j] = 0;
+    for (int i = 0; i < NP; ++i)
+      for (int j = 0; j < 3; ++j) cws[0][j] += pws[3 * i + j];
+    for (int j = 0; j < 3; ++j) cws[0][j] /= NP;
+    double A[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < NP; ++i) {
+      double d[3] = {pws[3 * i] - cws[0][0], pws[3 * i + 1] - cws[0][1], pws[3 * i + 2] - cws[0][2]};
+      for (int a = 0; a < 3; ++a)
+        for (int bb = 0; bb < 3; ++bb) A[a * 3 + bb] += d[a] * d[bb];
+    }
+    double W[3], U[9], V[9];
+    dsvd<3, 3>(A, W, U, V);
+    for (int i = 1; i < 4; ++i) {
+      double k = sqrt(W[i - 1] / NP);
+      for (int j = 0; j < 3; ++j) cws[i][j] = cws[0][j] + k * U[j * 3 + (i - 1)];
+    }
+  }
+  __device__ void barycentric() {
+    double cc[9], ci[9], W[3], U[9], V[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 1; j < 4; ++j) cc[3 * i + j - 1] = cws[j][i] - cws[0][i];
+    dsvd<3, 3>(cc, W, U, V);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double s = 0;
+        for (int k = 0; k < 3; ++k) s += (W[k] > 0 ? V[i * 3 + k] / W[k] : 0.0) * U[j * 3 + k];
+        ci[i * 3 + j] = s;
+      }
+    for (int i = 0; i < NP; ++i) {
+      const double* p = &pws[3 * i];
+      double* a = &alphas[4 * i];
+      for (int j = 0; j < 3; ++j)
+        a[1 + j] = ci[3 * j] * (p[0] - cws[0][0]) + ci[3 * j + 1] * (p[1] - cws[0][1]) + ci[3 * j + 2] * (p[2] - cws[0][2]);
+      a[0] = 1.0f - a[1] - a[2] - a[3];
+    }
+  }
+  __device__ void compute_ccs(const double* betas, const double* ut) {
+    for (int i = 0; i < 4; ++i) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
+    for (int i = 0; i < 4; ++i) {
+      const double* v = ut + 12 * (11 - i);
+      for (int j = 0; j < 4; ++j)
+        for (int k = 0; k < 3; ++k) ccs[j][k] += betas[i] * v[3 * j + k];
+    }
+  }
+  __device__ void compute_pcs() {
+    for (int i = 0; i < NP; ++i) {
+      const double* a = &alphas[4 * i];
+      for (int j = 0; j < 3; ++j) pcs[3 * i + j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
+    }
+  }
+  __device__ double compute_R_and_t(const double* ut, const double* betas, double* R, double* t) {
+    compute_ccs(betas, ut);
+    compute_pcs();
+    if (pcs[2] < 0.0) {
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 3; ++j) ccs[i][j] = -ccs[i][j];
+      for (int i = 0; i < 3 * NP; ++i) pcs[i] = -pcs[i];
+    }
+    double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+    for (int i = 0; i < NP; ++i)
+      for (int j = 0; j < 3; ++j) {
+        pc0[j] += pcs[3 * i + j];
+        pw0[j] += pws[3 * i + j];
+      }
+    for (int j = 0; j < 3; ++j) {
+      pc0[j] /= NP;
+      pw0[j] /= NP;
+    }
+    double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < NP; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double dc = pcs[3 * i + j] - pc0[j];
+        abt[3 * j] += dc * (pws[3 * i] - pw0[0]);
+        abt[3 * j + 1] += dc * (pws[3 * i + 1] - pw0[1]);
+        abt[3 * j + 2] += dc * (pws[3 * i + 2] - pw0[2]);
+      }
+    double W[3], U[9], V[9];
+    dsvd<3, 3>(abt, W, U, V);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) R[i * 3 + j] = U[i * 3] * V[j * 3] + U[i * 3 + 1] * V[j * 3 + 1] + U[i * 3 + 2] * V[j * 3 + 2];
+    double det = R[0] * R[4] * R[8] + R[1] * R[5] * R[6] + R[2] * R[3] * R[7] - R[2] * R[4] * R[6] - R[1] * R[3] * R[8] -
+                 R[0] * R[5] * R[7];
+    if (det < 0) {
+      R[6] = -R[6];
+      R[7] = -R[7];
+      R[8] = -R[8];
+    }
+    for (int i = 0; i < 3; ++i) t[i] = pc0[i] - dot3(&R[3 * i], pw0);
+    double sum2 = 0.0;
+    for (int i = 0; i < NP; ++i) {
+      const double* pw = &pws[3 * i];
+      double Xc = dot3(&R[0], pw) + t[0], Yc = dot3(&R[3], pw) + t[1];
+      double iz = 1.0 / (dot3(&R[6], pw) + t[2]);
+      double ue = uc + fu * Xc * iz, ve = vc + fv * Yc * iz;
+      double u = us[2 * i], v = us[2 * i + 1];
+      sum2 += sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
+    }
+    return sum2 / NP;
+  }
+  __device__ static void qr_solve(double* A, double* b, double* X) {
+    const int nr = 6, nc = 4;
+    double A1[4], A2[4];
+    for (int k = 0; k < nc; ++k) {
+      double eta = fabs(A[k * nc + k]);
+      for (int i = k + 1; i < nr; ++i) eta = fmax(eta, fabs(A[i * nc + k]));
+      if (eta == 0) return;
+      double sum2 = 0.0, inv = 1. / eta;
+      for (int i = k; i < nr; ++i) {
+        A[i * nc + k] *= inv;
+        sum2 += A[i * nc + k] * A[i * nc + k];
+      }
+      double sigma = sqrt(sum2);
+      if (A[k * nc + k] < 0) sigma = -sigma;
+      A[k * nc + k] += sigma;
+      A1[k] = sigma * A[k * nc + k];
+      A2[k] = -eta * sigma;
+      for (int j = k + 1; j < nc; ++j) {
+        double sum = 0;
+        for (int i = k; i < nr; ++i) sum += A[i * nc + k] * A[i * nc + j];
+        double tau = sum / A1[k];
+        for (int i = k; i < nr; ++i) A[i * nc + j] -= tau * A[i * nc + k];
+      }
+    }
+    for (int j = 0; j < nc; ++j) {
+      double tau = 0;
+      for (int i = j; i < nr; ++i) tau += A[i * nc + j] * b[i];
+      tau /= A1[j];
+      for (int i = j; i < nr; ++i) b[i] -= tau * A[i * nc + j];
+    }
+    X[nc - 1] = b[nc - 1] / A2[nc - 1];
+    for (int i = nc - 2; i >= 0; --i) {
+      double sum = 0;
+      for (int j = i + 1; j < nc; ++j) sum += A[i * nc + j] * X[j];
+      X[i] = (b[i] - sum) / A2[i];
+    }
+  }
+  __device__ static void gauss_newton(const double* L, const double* rho, double* betas) {
+    for (int it = 0; it < 5; ++it) {
+      double A[24], b[6], x[4] = {0, 0, 0, 0};
+      for (int i = 0; i < 6; ++i) {
+        const double* r = L + 10 * i;
+        A[i * 4 + 0] = 2 * r[0] * betas[0] + r[1] * betas[1] + r[3] * betas[2] + r[6] * betas[3];
+        A[i * 4 + 1] = r[1] * betas[0] + 2 * r[2] * betas[1] + r[4] * betas[2] + r[7] * betas[3];
+        A[i * 4 + 2] = r[3] * betas[0] + r[4] * betas[1] + 2 * r[5] * betas[2] + r[8] * betas[3];
+        A[i * 4 + 3] = r[6] * betas[0] + r[7] * betas[1] + r[8] * betas[2] + 2 * r[9] * betas[3];
+        b[i] = rho[i] - (r[0] * betas[0] * betas[0] + r[1] * betas[0] * betas[1] + r[2] * betas[1] * betas[1] +
+                         r[3] * betas[0] * betas[2] + r[4] * betas[1] * betas[2] + r[5] * betas[2] * betas[2] +
+                         r[6] * betas[0] * betas[3] + r[7] * betas[1] * betas[3] + r[8] * betas[2] * betas[3] +
+                         r[9] * betas[3] * betas[3]);
+      }
+      qr_solve(A, b, x);
+      for (int i = 0; i < 4; ++i) betas[i] += x[i];
+    }
+  }
+  __device__ void compute_pose(double* R, double* t) {
+    choose_control_points();
+    barycentric();
+    double MtM[144];
+    for (int i = 0; i < 144; ++i) MtM[i] = 0.0;
+    for (int i = 0; i < NP; ++i) {
+      const double* as = &alphas[4 * i];
+      double u = us[2 * i], v = us[2 * i + 1];
+      double M1[12], M2[12];
+      for (int j = 0; j < 4; ++j) {
+        M1[3 * j] = as[j] * fu; M1[3 * j + 1] = 0.0; M1[3 * j + 2] = as[j] * (uc - u);
+        M2[3 * j] = 0.0; M2[3 * j + 1] = as[j] * fv; M2[3 * j + 2] = as[j] * (vc - v);
+      }
+      for (int a = 0; a < 12; ++a)
+        for (int bb = 0; bb < 12; ++bb) MtM[a * 12 + bb] += M1[a] * M1[bb] + M2[a] * M2[bb];
+    }
+    double W[12], U[144], V[144];
+    dsvd<12, 12>(MtM, W, U, V);
+    double* ut = V;  // reuse: rows = singular vectors (ut[i*12+j] = U[j*12+i])
+    for (int i = 0; i < 12; ++i)
+      for (int j = 0; j < 12; ++j) ut[i * 12 + j] = U[j * 12 + i];
+    double L[60], rho[6];
+    {
+      const double* vv[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
+      double dv[4][6][3];
+      for (int i = 0; i < 4; ++i) {
+        int a = 0, bb = 1;
+        for (int j = 0; j < 6; ++j) {
+          for (int k = 0; k < 3; ++k) dv[i][j][k] = vv[i][3 * a + k] - vv[i][3 * bb + k];
+          if (++bb > 3) { ++a; bb = a + 1; }
+        }
+      }
+      for (int i = 0; i < 6; ++i) {
+        double* r = L + 10 * i;
+        r[0] = dot3(dv[0][i], dv[0][i]);
+        r[1] = 2.0f * dot3(dv[0][i], dv[1][i]);
+        r[2] = dot3(dv[1][i], dv[1][i]);
+        r[3] = 2.0f * dot3(dv[0][i], dv[2][i]);
+        r[4] = 2.0f * dot3(dv[1][i], dv[2][i]);
+        r[5] = dot3(dv[2][i], dv[2][i]);
+        r[6] = 2.0f * dot3(dv[0][i], dv[3][i]);
+        r[7] = 2.0f * dot3(dv[1][i], dv[3][i]);
+        r[8] = 2.0f * dot3(dv[2][i], dv[3][i]);
+        r[9] = dot3(dv[3][i], dv[3][i]);
+      }
+      rho[0] = dist2(cws[0], cws[1]); rho[1] = dist2(cws[0], cws[2]); rho[2] = dist2(cws[0], cws[3]);
+      rho[3] = dist2(cws[1], cws[2]); rho[4] = dist2(cws[1], cws[3]); rho[5] = dist2(cws[2], cws[3]);
+    }
+    double best_err = 0, Rb[9], tb[3];
+    for (int N = 1; N <= 3; ++N) {
+      double betas[4];
+      if (N == 1) {
+        double A[24], b4[4];
+        const int c[4] = {0, 1, 3, 6};
+        for (int i = 0; i < 6; ++i)
+          for (int j = 0; j < 4; ++j) A[i * 4 + j] = L[i * 10 + c[j]];
+        dsolve<6, 4>(A, rho, b4);
+        double s = b4[0] < 0 ? -1.0 : 1.0;
+        betas[0] = sqrt(s * b4[0]);
+        betas[1] = s * b4[1] / betas[0];
+        betas[2] = s * b4[2] / betas[0];
+        betas[3] = s * b4[3] / betas[0];
+      } else if (N == 2) {
+        double A[18], b3[3];
+        for (int i = 0; i < 6; ++i)
+          for (int j = 0; j < 3; ++j) A[i * 3 + j] = L[i * 10 + j];
+        dsolve<6, 3>(A, rho, b3);
+        if (b3[0] < 0) {
+          betas[0] = sqrt(-b3[0]);
+          betas[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
+        } else {
+          betas[0] = sqrt(b3[0]);
+          betas[1] = (b3[2] > 0) ? sqrt(b3[2]) : 0.0;
+        }
+        if (b3[1] < 0) betas[0] = -betas[0];
+        betas[2] = 0.0;
+        betas[3] = 0.0;
+      } else {
+        double A[30], b5[5];
+        for (int i = 0; i < 6; ++i)
+          for (int j = 0; j < 5; ++j) A[i * 5 + j] = L[i * 10 + j];
+        dsolve<6, 5>(A, rho, b5);
+        if (b5[0] < 0) {
+          betas[0] = sqrt(-b5[0]);
+          betas[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
+        } else {
+          betas[0] = sqrt(b5[0]);
+          betas[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0;
+        }
+        if (b5[1] < 0) betas[0] = -betas[0];
+        betas[2] = b5[3] / betas[0];
+        betas[3] = 0.0;
+      }
+      gauss_newton(L, rho, betas);
+      double Rn[9], tn[3];
+      double e = compute_R_and_t(ut, betas, Rn, tn);
+      if (N == 1 || e < best_err) {
+        best_err = e;
+        for (int i = 0; i < 9; ++i) Rb[i] = Rn[i];
+        for (int i = 0; i < 3; ++i) tb[i] = tn[i];
+      }
+    }
+    for (int i = 0; i < 9; ++i) R[i] = Rb[i];
+    for (int i = 0; i < 3; ++i) t[i] = tb[i];
+  }
+};
+
+struct RNG {
+  uint64_t state;
+  __device__ unsigned next() {
+    state = (uint64_t)(unsigned)state * 4164903690u + (unsigned)(state >> 32);
+    return (unsigned)state;
+  }
+  __device__ int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a) + a); }
+};
+
+__device__ int update_num_iters(double p, double ep, int m, int maxIters) {
+  p = fmax(p, 0.);
+  p = fmin(p, 1.);
+  ep = fmax(ep, 0.);
+  ep = fmin(ep, 1.);
+  double num = fmax(1. - p, DBL_MIN);
+  double denom = 1. - pow(1. - ep, (double)m);
+  if (denom < DBL_MIN) return 0;
+  num = log(num);
+  denom = log(denom);
+  return denom >= 0 || -num >= maxIters * (-denom) ? maxIters : (int)rint(num / denom);
+}
+
+__device__ __forceinline__ double wsum_d(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ------------------------------------------------------------------ RANSAC + refine
+struct PnpShared {
+  int sub[kChunk][5];
+  int good[kChunk];
+  double model[kChunk][6];
+  double best[6];
+  double param[6];
+  int maxGood, niters, done, next_iter;
+  uint64_t rng;
+  int ninl;
+  int flag;
+};
+
+__device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const float* p2, const int* inl, int n,
+                          double* mn) {
+  // ---- init (cvFindExtrinsicCameraParams2, useExtrinsicGuess = false)
+  const int lane = wave_lane();
+  double acc[28];
+  for (int k = 0; k < 28; ++k) acc[k] = 0;
+  for (int i = lane; i < n; i += 64) {
+    int j = inl[i];
+    dundistort(K, (double)p2[2 * j], (double)p2[2 * j + 1], &mn[2 * i]);
+    acc[0] += (double)P3[3 * j];
+    acc[1] += (double)P3[3 * j + 1];
+    acc[2] += (double)P3[3 * j + 2];
+  }
+  for (int k = 0; k < 3; ++k) acc[k] = wsum_d(acc[k]);
+  double Mc[3] = {acc[0] / n, acc[1] / n, acc[2] / n};
+  double MM[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = lane; i < n; i += 64) {
+    int j = inl[i];
+    double d[3] = {(double)P3[3 * j] - Mc[0], (double)P3[3 * j + 1] - Mc[1], (double)P3[3 * j + 2] - Mc[2]};
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) MM[a * 3 + b] += d[a] * d[b];
+  }
+  for (int k = 0; k < 9; ++k) MM[k] = wsum_d(MM[k]);
+  double W3[3], U3[9], V3[9];
+  dsvd<3, 3>(MM, W3, U3, V3);
+  const bool planar = W3[2] / W3[1] < 1e-3;
+  if (!planar && n < 6) {
+    if (lane == 0) sh.flag = 0;  // DLT would throw: keep the RANSAC model
+    __syncthreads();
+    return;
+  }
+  double LLp[78];
+  for (int k = 0; k < 78; ++k) LLp[k] = 0;
+  double Rt[9], T[3];
+  if (!planar) {
+    for (int i = lane; i < n; i += 64) {
+      int j = inl[i];
+      double x = -mn[2 * i], y = -mn[2 * i + 1];
+      double P[3] = {(double)P3[3 * j], (double)P3[3 * j + 1], (double)P3[3 * j + 2]};
+      double r0[12] = {P[0], P[1], P[2], 1., 0, 0, 0, 0, x * P[0], x * P[1], x * P[2], x};
+      double r1[12] = {0, 0, 0, 0, P[0], P[1], P[2], 1., y * P[0], y * P[1], y * P[2], y};
+      int k = 0;
+      for (int a = 0; a < 12; ++a)
+        for (int b = a; b < 12; ++b) LLp[k++] += r0[a] * r0[b] + r1[a] * r1[b];
+    }
+  } else {
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Rt[i * 3 + j] = V3[j * 3 + i];
+    if (Rt[2] * Rt[2] + Rt[5] * Rt[5] < 1e-10)
+      for (int i = 0; i < 9; ++i) Rt[i] = (i % 4 == 0);
+    if (ddet3(Rt) < 0)
+      for (int i = 0; i < 9; ++i) Rt[i] = -Rt[i];
+    for (int i = 0; i < 3; ++i) T[i] = -(Rt[i * 3] * Mc[0] + Rt[i * 3 + 1] * Mc[1] + Rt[i * 3 + 2] * Mc[2]);
+    // homography DLT (A^T A, 9x9 upper triangle = 45 entries)
+    for (int i = lane; i < n; i += 64) {
+      int j = inl[i];
+      double s0 = P3[3 * j], s1 = P3[3 * j + 1], s2 = P3[3 * j + 2];
+      double X = Rt[0] * s0 + Rt[1] * s1 + Rt[2] * s2 + T[0];
+      double Y = Rt[3] * s0 + Rt[4] * s1 + Rt[5] * s2 + T[1];
+      double u = mn[2 * i], v = mn[2 * i + 1];
+      double r0[9] = {X, Y, 1, 0, 0, 0, -u * X, -u * Y, -u};
+      double r1[9] = {0, 0, 0, X, Y, 1, -v * X, -v * Y, -v};
+      int k = 0;
+      for (int a = 0; a < 9; ++a)
+        for (int b = a; b < 9; ++b) LLp[k++] += r0[a] * r0[b] + r1[a] * r1[b];
+    }
+  }
+  for (int k = 0; k < 78; ++k) LLp[k] = wsum_d(LLp[k]);
+  double param[6] = {0, 0, 0, 0, 0, 0};
+  if (lane == 0) {
+    double R[9];
+    if (!planar) {
+      double LL[144], LW[12], LU[144], LV[144];
+      int k = 0;
+      for (int a = 0; a < 12; ++a)
+        for (int b = a; b < 12; ++b) { LL[a * 12 + b] = LLp[k]; LL[b * 12 + a] = LLp[k]; ++k; }
+      dsvd<12, 12>(LL, LW, LU, LV);
+      double RRt[12];
+      for (int i = 0; i < 12; ++i) RRt[i] = LV[i * 12 + 11];
+      double RR[9] = {RRt[0], RRt[1], RRt[2], RRt[4], RRt[5], RRt[6], RRt[8], RRt[9], RRt[10]};
+      double tt[3] = {RRt[3], RRt[7], RRt[11]};
+      if (ddet3(RR) < 0) {
+        for (int i = 0; i < 9; ++i) RR[i] = -RR[i];
+        for (int i = 0; i < 3; ++i) tt[i] = -tt[i];
+      }
+      double sc = 0;
+      for (int i = 0; i < 9; ++i) sc += RR[i] * RR[i];
+      sc = sqrt(sc);
+      double Wr[3], Ur[9], Vr[9];
+      dsvd<3, 3>(RR, Wr, Ur, Vr);
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[i * 3 + j] = Ur[i * 3] * Vr[j * 3] + Ur[i * 3 + 1] * Vr[j * 3 + 1] + Ur[i * 3 + 2] * Vr[j * 3 + 2];
+      double nR = 0;
+      for (int i = 0; i < 9; ++i) nR += R[i] * R[i];
+      nR = sqrt(nR);
+      for (int i = 0; i < 3; ++i) param[3 + i] = tt[i] * nR / sc;
+      rod_R2r(R, param);
+    } else {
+      double AtA[81], W9[9], U9[81], V9[81], H[9], t[3];
+      int k = 0;
+      for (int a = 0; a < 9; ++a)
+        for (int b = a; b < 9; ++b) { AtA[a * 9 + b] = LLp[k]; AtA[b * 9 + a] = LLp[k]; ++k; }
+      dsvd<9, 9>(AtA, W9, U9, V9);
+      for (int i = 0; i < 9; ++i) H[i] = V9[i * 9 + 8];
+      if (fabs(H[8]) >= 1e-300) {
+        for (int i = 0; i < 9; ++i) H[i] /= H[8];
+        double h1 = sqrt(H[0] * H[0] + H[3] * H[3] + H[6] * H[6]);
+        double h2 = sqrt(H[1] * H[1] + H[4] * H[4] + H[7] * H[7]);
+        for (int i = 0; i < 3; ++i) {
+          H[i * 3] /= fmax(h1, DBL_EPSILON);
+          H[i * 3 + 1] /= fmax(h2, DBL_EPSILON);
+          t[i] = H[i * 3 + 2] * 2. / fmax(h1 + h2, DBL_EPSILON);
+        }
+        H[2] = H[3] * H[7] - H[6] * H[4];
+        H[5] = H[6] * H[1] - H[0] * H[7];
+        H[8] = H[0] * H[4] - H[3] * H[1];
+        double r[3];
+        rod_R2r(H, r);
+        rod_r2R(r, H, nullptr);
+        for (int i = 0; i < 3; ++i) t[i] += H[i * 3] * T[0] + H[i * 3 + 1] * T[1] + H[i * 3 + 2] * T[2];
+        for (int i = 0; i < 3; ++i)
+          for (int j = 0; j < 3; ++j) R[i * 3 + j] = H[i * 3] * Rt[j] + H[i * 3 + 1] * Rt[3 + j] + H[i * 3 + 2] * Rt[6 + j];
+        param[3] = t[0]; param[4] = t[1]; param[5] = t[2];
+      } else {
+        for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0);
+      }
+      rod_R2r(R, param);
+    }
+    for (int i = 0; i < 6; ++i) sh.param[i] = param[i];
+  }
+  __syncthreads();
+  // ---- Levenberg-Marquardt (CvLevMarq semantics)
+  auto eval = [&](bool withJ, double* JtJ, double* JtErr) -> double {
+    double p[6];
+    for (int i = 0; i < 6; ++i) p[i] = sh.param[i];
+    double R[9], dR[27];
+    rod_r2R(p, R, dR);
+    double a[28];
+    for (int k = 0; k < 28; ++k) a[k] = 0;
+    for (int i = lane; i < n; i += 64) {
+      int j = inl[i];
+      double M[3] = {(double)P3[3 * j], (double)P3[3 * j + 1], (double)P3[3 * j + 2]}, uv[2], J[12];
+      dproject(K, R, dR, p + 3, M, uv, withJ ? J : nullptr);
+      double e0 = uv[0] - (double)p2[2 * j], e1 = uv[1] - (double)p2[2 * j + 1];
+      a[27] += e0 * e0 + e1 * e1;
+      if (withJ) {
+        int k = 0;
+        for (int r = 0; r < 6; ++r)
+          for (int c = r; c < 6; ++c) a[k++] += J[r] * J[c] + J[6 + r] * J[6 + c];
+        for (int r = 0; r < 6; ++r) a[21 + r] += J[r] * e0 + J[6 + r] * e1;
+      }
+    }
+    for (int k = withJ ? 0 : 27; k < 28; ++k) a[k] = wsum_d(a[k]);
+    if (withJ) {
+      int k = 0;
+      for (int r = 0; r < 6; ++r)
+        for (int c = r; c < 6; ++c) { JtJ[r * 6 + c] = a[k]; JtJ[c * 6 + r] = a[k]; ++k; }
+      for (int r = 0; r < 6; ++r) JtErr[r] = a[21 + r];
+    }
+    return sqrt(a[27]);
+  };
+  double JtJ[36], JtErr[6], prev[6];
+  double lambdaLg10 = -3, prevErrNorm = DBL_MAX;
+  auto step = [&]() {
+    if (lane == 0) {
+      double lambda = exp(lambdaLg10 * log(10.));
+      double A[36], x[6];
+      for (int i = 0; i < 36; ++i) A[i] = JtJ[i];
+      for (int i = 0; i < 6; ++i) A[i * 6 + i] *= 1. + lambda;
+      dsolve<6, 6>(A, JtErr, x);
+      for (int i = 0; i < 6; ++i) sh.param[i] = prev[i] - x[i];
+    }
+    __syncthreads();
+  };
+  int iters = 0;
+  for (;;) {
+    double e0 = eval(true, JtJ, JtErr);
+    for (int i = 0; i < 6; ++i) prev[i] = sh.param[i];
+    __syncthreads();
+    step();
+    if (iters == 0) prevErrNorm = e0;
+    double errNorm;
+    for (;;) {
+      errNorm = eval(false, nullptr, nullptr);
+      if (errNorm > prevErrNorm && ++lambdaLg10 <= 16) {
+        step();
+        continue;
+      }
+      break;
+    }
+    lambdaLg10 = fmax(lambdaLg10 - 1, -16.0);
+    double dn = 0, pn = 0;
+    for (int i = 0; i < 6; ++i) {
+      dn += (sh.param[i] - prev[i]) * (sh.param[i] - prev[i]);
+      pn += prev[i] * prev[i];
+    }
+    double rel = sqrt(dn) / (sqrt(pn) + DBL_EPSILON);
+    if (++iters >= 20 || rel < FLT_EPSILON) break;
+    prevErrNorm = errNorm;
+  }
+  if (lane == 0) sh.flag = 1;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(64) void k_pnp(const float* __restrict__ P3all, const float* __restrict__ p2all,
+                                            const int32_t* __restrict__ npts, int cap, Cam K, float thr2, double conf,
+                                            int maxIters, double* __restrict__ rvec, double* __restrict__ tvec,
+                                            double* __restrict__ T, int32_t* __restrict__ status,
+                                            uint8_t* __restrict__ inliers, int32_t* __restrict__ inl_idx,
+                                            double* __restrict__ mn_buf) {
+  __shared__ PnpShared sh;
+  const int b = blockIdx.x, lane = threadIdx.x;
+  int n = npts[b];
+  n = n < 0 ? 0 : (n > cap ? cap : n);
+  const float* P3 = P3all + (int64_t)b * cap * 3;
+  const float* p2 = p2all + (int64_t)b * cap * 2;
+  double* Tout = T + (int64_t)b * 16;
+  if (n < 6) {
+    if (lane < 16) Tout[lane] = (lane % 5 == 0) ? 1.0 : 0.0;
+    if (lane < 3) { rvec[b * 3 + lane] = 0; tvec[b * 3 + lane] = 0; }
+    if (inliers)
+      for (int i = lane; i < cap; i += 64) inliers[(int64_t)b * cap + i] = 0;
+    if (lane == 0) status[b] = -1;
+    return;
+  }
+  const int mp = 5;
+  if (lane == 0) {
+    sh.maxGood = 0;
+    sh.niters = maxIters;
+    sh.done = 0;
+    sh.next_iter = 0;
+    sh.rng = ~0ull;
+  }
+  __syncthreads();
+  while (!sh.done) {
+    const int it0 = sh.next_iter;
+    if (lane == 0) {
+      RNG rng{sh.rng};
+      for (int k = 0; k < kChunk; ++k) {
+        for (int i = 0; i < mp; ++i) {
+          int j;
+          for (;;) {
+            j = rng.uniform(0, n);
+            bool dup = false;
+            for (int q = 0; q < i; ++q) dup |= sh.sub[k][q] == j;
+            if (!dup) break;
+          }
+          sh.sub[k][i] = j;
+        }
+      }
+      sh.rng = rng.state;
+    }
+    __syncthreads();
+    // hypothesis for iteration it0 + lane
+    {
+      EPnPd<5> e;
+      e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
+      for (int i = 0; i < mp; ++i) {
+        int j = sh.sub[lane][i];
+        for (int c = 0; c < 3; ++c) e.pws[3 * i + c] = (double)P3[3 * j + c];
+        double xy[2];
+        dundistort(K, (double)p2[2 * j], (double)p2[2 * j + 1], xy);
+        float fx = (float)xy[0], fy = (float)xy[1];
+        e.us[2 * i] = fx * K.fx + K.cx;
+        e.us[2 * i + 1] = fy * K.fy + K.cy;
+      }
+      double R[9], t[3], r[3], dR[27];
+      e.compute_pose(R, t);
+      rod_R2r(R, r);
+      for (int i = 0; i < 3; ++i) { sh.model[lane][i] = r[i]; sh.model[lane][3 + i] = t[i]; }
+      rod_r2R(r, R, dR);
+      int good = 0;
+      for (int i = 0; i < n; ++i) {
+        double M[3] = {(double)P3[3 * i], (double)P3[3 * i + 1], (double)P3[3 * i + 2]}, uv[2];
+        dproject(K, R, dR, t, M, uv, nullptr);
+        float du = p2[2 * i] - (float)uv[0], dv = p2[2 * i + 1] - (float)uv[1];
+        float err = du * du + dv * dv;
+        good += err <= thr2;
+      }
+      sh.good[lane] = good;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      int k = 0;
+      for (; k < kChunk; ++k) {
+        int iter = it0 + k;
+        if (iter >= sh.niters) break;
+        int g = sh.good[k];
+        if (g > max(sh.maxGood, mp - 1)) {
+          for (int i = 0; i < 6; ++i) sh.best[i] = sh.model[k][i];
+          sh.maxGood = g;
+          sh.niters = update_num_iters(conf, (double)(n - g) / n, mp, sh.niters);
+        }
+      }
+      sh.next_iter = it0 + kChunk;
+      if (sh.next_iter >= sh.niters || k < kChunk) sh.done = 1;
+    }
+    __syncthreads();
+  }
+  if (sh.maxGood <= 0) {
+    if (lane < 16) Tout[lane] = (lane % 5 == 0) ? 1.0 : 0.0;
+    if (lane < 3) { rvec[b * 3 + lane] = 0; tvec[b * 3 + lane] = 0; }
+    if (inliers)
+      for (int i = lane; i < cap; i += 64) inliers[(int64_t)b * cap + i] = 0;
+    if (lane == 0) status[b] = 0;
+    return;
+  }
+  // inlier mask of the best model + ordered compaction of inlier indices
+  int* inl = inl_idx + (int64_t)b * cap;
+  {
+    double r[3] = {sh.best[0], sh.best[1], sh.best[2]}, t[3] = {sh.best[3], sh.best[4], sh.best[5]};
+    double R[9], dR[27];
+    rod_r2R(r, R, dR);
+    int carry = 0;
+    for (int base = 0; base < n; base += 64) {
+      int i = base + lane;
+      bool f = false;
+      if (i < n) {
+        double M[3] = {(double)P3[3 * i], (double)P3[3 * i + 1], (double)P3[3 * i + 2]}, uv[2];
+        dproject(K, R, dR, t, M, uv, nullptr);
+        float du = p2[2 * i] - (float)uv[0], dv = p2[2 * i + 1] - (float)uv[1];
+        f = du * du + dv * dv <= thr2;
+        if (inliers) inliers[(int64_t)b * cap + i] = (uint8_t)f;
+      }
+      unsigned long long m = __ballot(f);
+      if (f) inl[carry + __popcll(m & ((1ull << lane) - 1ull))] = i;
+      carry += __popcll(m);
+    }
+    if (inliers)
+      for (int i = n + lane; i < cap; i += 64) inliers[(int64_t)b * cap + i] = 0;
+    if (lane == 0) sh.ninl = carry;
+  }
+  __syncthreads();
+  lm_refine(sh, K, P3, p2, inl, sh.ninl, mn_buf + (int64_t)b * cap * 2);
+  double out[6];
+  for (int i = 0; i < 6; ++i) out[i] = sh.flag ? sh.param[i] : sh.best[i];
+  if (lane == 0) {
+    double R[9];
+    rod_r2R(out, R, nullptr);
+    for (int i = 0; i < 3; ++i) {
+      rvec[b * 3 + i] = out[i];
+      tvec[b * 3 + i] = out[3 + i];
+      Tout[i * 4 + 0] = R[i * 3];
+      Tout[i * 4 + 1] = R[i * 3 + 1];
+      Tout[i * 4 + 2] = R[i * 3 + 2];
+      Tout[i * 4 + 3] = out[3 + i];
+    }
+    Tout[12] = 0; Tout[13] = 0; Tout[14] = 0; Tout[15] = 1;
+    status[b] = 1;
+  }
+}
+
+}  // namespace
+
+int pose_init(fvo_ctx* ctx) {
+  ctx->pnp_max_iters = 1000;
+  const int64_t n = (int64_t)ctx->cfg.max_batch * ctx->kp_cap;
+  int rc;
+  if ((rc = fvo_alloc(ctx, &ctx->pnp_sub, n)) || (rc = fvo_alloc(ctx, &ctx->pnp_hyp, 2 * n))) return rc;
+  return 0;
+}
+
+int backproject_run(fvo_ctx* ctx, const int16_t* disp, const float* kp0, const float* kp1, const int32_t* matches,
+                    const int32_t* nmatch, int batch, int cap, const double* K, double baseline, float* P3, float* p2,
+                    int32_t* npts, hipStream_t s) {
+  CamF c{K[0], K[4], K[2], K[5], K[0] * baseline};
+  hipLaunchKernelGGL(k_backproject, dim3(batch), dim3(256), 0, s, disp, kp0, kp1, matches, nmatch, ctx->cfg.width,
+                     ctx->cfg.height, cap, c, P3, p2, npts);
+  FVO_LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts, int batch, int cap, const double* K,
+            const double* dist, float reproj, double conf, int iters, double* rvec, double* tvec, double* T,
+            int32_t* status, uint8_t* inliers, hipStream_t s) {
+  if (cap > ctx->kp_cap) return fvo_fail(ctx, "pnp: cap exceeds the context keypoint capacity");
+  Cam c{K[0], K[4], K[2], K[5], {dist[0], dist[1], dist[2], dist[3], dist[4]}};
+  float thr2 = (float)((double)reproj * reproj);
+  hipLaunchKernelGGL(k_pnp, dim3(batch), dim3(64), 0, s, P3, p2, npts, cap, c, thr2, conf, iters, rvec, tvec, T, status,
+                     inliers, ctx->pnp_sub, ctx->pnp_hyp);
+  FVO_LAUNCH_CHECK(ctx);
+  return 0;
+}

@@ -112,11 +112,13 @@ int fvo_sgbm(fvo_ctx* ctx, const uint8_t* left, const uint8_t* right, int32_t ba
  * kp0/kp1:   keypoint records of the previous / current left images ([batch][cap][8]).
  * matches:   fvo_bf_match output (query = previous, train = current).
  * K:         host double[9] row-major camera matrix; baseline in metres.
- * points3d:  [batch][cap][3] f64 valid points (0.1 < Z < 1000), compacted in match order.
+ * points3d:  [batch][cap][3] f32 valid points (0.1 < Z < 1000), compacted in match order.  f32
+ *            because the reference's NumPy 1.x (Python 3.8) evaluates float64-scalar x
+ *            float32-array expressions in float32 (value-based casting), DESIGN.md §Parity.
  * points2d:  [batch][cap][2] f32 matching current-image keypoints.  n_points: [batch]. */
 int fvo_backproject(fvo_ctx* ctx, const int16_t* disparity, const float* kp0, const float* kp1,
                     const int32_t* matches, const int32_t* n_matches, int32_t batch, int32_t cap, const double* K,
-                    double baseline, double* points3d, float* points2d, int32_t* n_points, fvo_stream stream);
+                    double baseline, float* points3d, float* points2d, int32_t* n_points, fvo_stream stream);
 
 /* solvePnPRansac(SOLVEPNP_ITERATIVE) + Rodrigues on `batch` independent frames.
  * K, dist:   host double[9] / double[5] (k1 k2 p1 p2 k3).
@@ -124,7 +126,7 @@ int fvo_backproject(fvo_ctx* ctx, const int16_t* disparity, const float* kp0, co
  * status:    [batch] i32: 1 pose valid, 0 RANSAC failed, -1 skipped (n_points < 6,
  *            the reference's `len(points3D) >= 6` guard, stereo_slam.py:292).
  * inliers:   [batch][cap] u8 RANSAC inlier mask (may be NULL). */
-int fvo_pnp_ransac(fvo_ctx* ctx, const double* points3d, const float* points2d, const int32_t* n_points,
+int fvo_pnp_ransac(fvo_ctx* ctx, const float* points3d, const float* points2d, const int32_t* n_points,
                    int32_t batch, int32_t cap, const double* K, const double* dist, float reprojection_error,
                    double confidence, int32_t iterations, double* rvec, double* tvec, double* T, int32_t* status,
                    uint8_t* inliers, fvo_stream stream);

@@ -164,30 +164,41 @@ def sgbm_row_cost(L, R, y, num_disp=96):
 
 
 def disparity_map(disp16: np.ndarray) -> np.ndarray:
-    """stereo_slam.py:117-121: /16 in float32, 0.0 and -1.0 -> 0.1."""
-    d = disp16.astype(np.float32) / 16
-    d[d == 0.0] = 0.1
-    d[d == -1.0] = 0.1
-    return d
+    """stereo_slam.py:117-121: /16 in float32, 0.0 and -1.0 -> 0.1 (float32)."""
+    return disparity_map_np1(disp16)
 
 
 # ----------------------------------------------------------------------------- pose
 def backproject(disp_f32: np.ndarray, mk0: np.ndarray, mk1: np.ndarray, K: np.ndarray, baseline: float):
-    """stereo_slam.py:265-289 in float64, exactly as numpy evaluates it."""
+    """stereo_slam.py:265-289 with the reference environment's NumPy 1.x promotion rules
+    (Ubuntu 20.04 / Python 3.8: NumPy <= 1.24, value-based casting): a float64 *scalar*
+    combined with a float32 *array* computes in float32.  So depth, X, Y, Z and points3D
+    are float32; the float64 scalars are rounded to float32 first.  This container runs
+    NumPy 2, hence the explicit casts."""
+    f32 = np.float32
     cx, cy, fx, fy = K[0, 2], K[1, 2], K[0, 0], K[1, 1]
-    depth = fx * baseline / disp_f32
-    X = mk0[:, 0]
-    Y = mk0[:, 1]
+    depth = f32(fx * baseline) / disp_f32.astype(f32)
+    X = mk0[:, 0].astype(f32)
+    Y = mk0[:, 1].astype(f32)
     Z = depth[Y.astype(int), X.astype(int)]
-    X = ((X - cx) / fx) * Z
-    Y = ((Y - cy) / fy) * Z
-    P = np.column_stack((X, Y, Z))
-    valid = (Z > 0.1) & (Z < 1000)
+    X = ((X - f32(cx)) / f32(fx)) * Z
+    Y = ((Y - f32(cy)) / f32(fy)) * Z
+    P = np.column_stack((X, Y, Z)).astype(f32)
+    valid = (Z > f32(0.1)) & (Z < f32(1000))
     return P[valid], mk1[valid], valid
+
+
+def disparity_map_np1(disp16: np.ndarray) -> np.ndarray:
+    """stereo_slam.py:117-121 (float32 throughout under NumPy 1.x)."""
+    d = disp16.astype(np.float32) / np.float32(16)
+    d[d == np.float32(0.0)] = np.float32(0.1)
+    d[d == np.float32(-1.0)] = np.float32(0.1)
+    return d
 
 
 def solve_pnp_ransac(P3: np.ndarray, p2: np.ndarray, K: np.ndarray, dist: np.ndarray, reproj: float = 1.0,
                      confidence: float = 0.99, iters: int = 1000):
+    """Returns (ok, rvec, tvec, inlier_idx, ransac_iters, ransac_inliers)."""
     P3 = np.ascontiguousarray(P3, dtype=np.float64)
     p2 = np.ascontiguousarray(p2, dtype=np.float32)
     K = np.ascontiguousarray(K, dtype=np.float64)

@@ -150,3 +150,71 @@ def test_sgbm_small_geometry(oracle_mod):
     torch.cuda.synchronize()
     want = oracle_mod.sgbm(L.numpy(), R.numpy(), num_disp=64)
     assert np.array_equal(d[0].cpu().numpy(), want)
+
+
+def _pnp_case(seed, n, outlier_frac, noise, K, dist, oracle_mod):
+    rng = np.random.default_rng(seed)
+    P = np.c_[rng.uniform(-6, 6, n), rng.uniform(-2, 2, n), rng.uniform(2, 40, n)].astype(np.float32)
+    rv = rng.normal(0, 0.02, 3)
+    tv = rng.normal(0, 0.1, 3)
+    uv = oracle_mod.project_points(P.astype(np.float64), rv, tv, K, dist) + rng.normal(0, noise, (n, 2))
+    out = rng.random(n) < outlier_frac
+    uv[out] += rng.uniform(-40, 40, (out.sum(), 2))
+    return P, uv.astype(np.float32), rv, tv
+
+
+def test_pnp_ransac_matches_oracle(oracle_mod):
+    from forest_slam_amd import _lib, synth
+    K, dist = synth.K0, synth.DIST_L
+    cases = [(s, n, f, nz) for s, (n, f, nz) in enumerate([(300, 0.3, 0.3), (80, 0.5, 0.2), (1000, 0.1, 0.5),
+                                                           (40, 0.0, 0.0), (12, 0.2, 0.1), (6, 0.0, 0.2),
+                                                           (500, 0.7, 0.3), (5, 0.0, 0.0)])]
+    B = len(cases)
+    ctx = _lib.Context(960, 600, max_batch=B)
+    cap = ctx.kp_cap
+    P3 = np.zeros((B, cap, 3), np.float32)
+    p2 = np.zeros((B, cap, 2), np.float32)
+    npts = np.zeros(B, np.int32)
+    data = []
+    for i, (s, n, f, nz) in enumerate(cases):
+        P, uv, rv, tv = _pnp_case(s, n, f, nz, K, dist, oracle_mod)
+        P3[i, :n], p2[i, :n], npts[i] = P, uv, n
+        data.append((P, uv, rv, tv))
+    rvec, tvec, T, st, inl = ctx.pnp_ransac(torch.from_numpy(P3).cuda(), torch.from_numpy(p2).cuda(),
+                                            torch.from_numpy(npts).cuda(), K, dist)
+    torch.cuda.synchronize()
+    rvec, tvec, st, inl = rvec.cpu().numpy(), tvec.cpu().numpy(), st.cpu().numpy(), inl.cpu().numpy()
+    for i, (P, uv, rv, tv) in enumerate(data):
+        n = len(P)
+        if n < 6:
+            assert st[i] == -1
+            continue
+        ok, r_ref, t_ref, inl_ref, _, _ = oracle_mod.solve_pnp_ransac(P.astype(np.float64), uv, K, dist)
+        assert st[i] == int(ok)
+        assert np.array_equal(np.nonzero(inl[i, :n])[0], inl_ref), i
+        scale = max(np.abs(r_ref).max(), np.abs(t_ref).max(), 1e-3)
+        assert np.abs(rvec[i] - r_ref).max() <= 1e-4 * scale + 1e-9, (i, rvec[i], r_ref)
+        assert np.abs(tvec[i] - t_ref).max() <= 1e-4 * scale + 1e-9, (i, tvec[i], t_ref)
+
+
+def test_frontend_matches_oracle_pipeline(oracle_mod, frames):
+    """End-to-end stereo_slam.py iteration (:232-306) on 2 frame pairs: matches bit-exact,
+    3D points bit-exact (float32), relative pose within 1e-4."""
+    from forest_slam_amd import synth, vo
+    fe = vo.StereoFrontEnd(960, 600, synth.K0, synth.DIST_L, synth.BASELINE, batch=2, nfeatures=500)
+    Ls = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
+    Rs = torch.from_numpy(np.stack([f[1] for f in frames])).cuda()
+    fe.prime(Ls[0], Rs[0])
+    T, st = fe.step(Ls[1:3], Rs[1:3])
+    torch.cuda.synchronize()
+    T, st = T.cpu().numpy(), st.cpu().numpy()
+    for i in range(2):
+        ref = oracle_mod.frame_pose(frames[i][0], frames[i][1], frames[i + 1][0], synth.K0, synth.DIST_L,
+                                    synth.BASELINE, 500)
+        nm = int(fe.nmatch[i].item())
+        assert np.array_equal(fe.matches[i, :nm].cpu().numpy(), ref["matches"])
+        assert np.array_equal(fe.disp[i].cpu().numpy(), ref["disp16"])
+        n = int(fe.npts[i].item())
+        assert np.array_equal(fe.P3[i, :n].cpu().numpy(), ref["P3"])
+        assert ref["T"] is not None and st[i] == 1
+        assert np.abs(T[i] - ref["T"]).max() <= 1e-4 * max(1.0, np.abs(ref["T"]).max())
