@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Benchmark: stereo frames/s of the MI355X VO hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+Workload (BASELINE.json configs[1]): 960x600 synthetic forest stereo along the 1018_00
+ground-truth path, ORB nfeatures=1000, cross-checked BF-Hamming matching (left and the
+reference's unused right matches), StereoSGBM-3way (96 disparities), back-projection,
+PnP-RANSAC(+LM) — stereo_slam.py:232-306 per frame.  A step = one batch of B consecutive
+frames of the rank's own sequence (seed = rank), inputs resident in HBM before timing.
+Multi-GPU: one sequence per GPU, no data-path collective (weak scaling); the only
+collectives are the timing barrier and the max-over-ranks reduction.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement for the roofline definition.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def algorithmic_bytes_per_frame(W: int, H: int, N: int) -> int:
+    """2WH (L,R u8 in) + 2WH (int16 disparity) + 2N*48 (kp+desc, 2 images)
+    + 2*(2N*32 + 4N) (two matchings) + 22N (back-projection) = 4WH + 254N."""
+    return 4 * W * H + 254 * N
+
+
+def cpu_baseline(n_frames: int, nfeatures: int, W: int, H: int) -> dict:
+    """Scalar C++ restatement of the reference CPU path (oracle/, 1 thread) timed on a
+    bounded sample: per frame the reference's full per-iteration work — 4 ORB extractions
+    (prev/cur x L/R), 2 BF cross-check matchings, SGBM-3way, back-projection, PnP."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test/baseline infrastructure only
+    from forest_slam_amd import synth
+    seq = synth.StereoSequence(seed=0, n_frames=n_frames + 1, W=W, H=H, device="cpu")
+    imgs = [tuple(x.numpy() for x in seq.frame(i)) for i in range(n_frames + 1)]
+    t0 = time.perf_counter()
+    for i in range(n_frames):
+        (pL, pR), (cL, cR) = imgs[i], imgs[i + 1]
+        oracle.frame_pose(pL, pR, cL, seq.K, synth.DIST_L, synth.BASELINE, nfeatures)
+        _, dR0 = oracle.orb_detect_compute(pR, nfeatures)
+        _, dR1 = oracle.orb_detect_compute(cR, nfeatures)
+        oracle.bf_match(dR0, dR1)
+    dt = time.perf_counter() - t0
+    return {"value": n_frames / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n_frames} consecutive {W}x{H} synthetic stereo frames, nfeatures={nfeatures}: "
+                      "4 ORB + 2 BF-xcheck + SGBM-3way + back-projection + PnP-RANSAC per frame, "
+                      f"oracle/ scalar C++ on 1 host thread, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
+    ap.add_argument("--nfeatures", type=int, default=1000)
+    ap.add_argument("--width", type=int, default=960)
+    ap.add_argument("--height", type=int, default=600)
+    ap.add_argument("--ate-frames", type=int, default=120, help="frames of the ATE run (0 = skip)")
+    ap.add_argument("--cpu-frames", type=int, default=4, help="CPU baseline sample (0 = skip)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import forest_slam_amd.build as fbuild
+    from forest_slam_amd import eval as ev
+    from forest_slam_amd import synth, vo
+
+    if not os.path.exists(fbuild.OUT):
+        raise SystemExit("libfvo.so missing: run __graft_entry__.build() first")
+
+    W, H, B = args.width, args.height, args.batch
+    seq = synth.StereoSequence(seed=rank, n_frames=B + 1, W=W, H=H, device=dev)
+    L_all, R_all = seq.frames(range(B + 1))
+    torch.cuda.synchronize()
+    fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=B, nfeatures=args.nfeatures, device=dev)
+    fe.prime(L_all[0], R_all[0])
+    Lb, Rb = L_all[1:].contiguous(), R_all[1:].contiguous()
+
+    def step():
+        fe.step(Lb, Rb)
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+
+    # per-kernel breakdown (separate pass, every launch bracketed by events)
+    fe.ctx.timing_enable(None)
+    nprof = 2
+    for _ in range(nprof):
+        step()
+    stages = fe.ctx.timing_read()
+    fe.ctx.timing_enable([])
+    dom = max(stages, key=lambda k: stages[k][0])
+    stage_ms = {k: round(v[0] / nprof, 4) for k, v in sorted(stages.items(), key=lambda kv: -kv[1][0])}
+
+    # timed region: only the dominant kernel bracketed (2 events per launch)
+    fe.ctx.timing_enable([dom])
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    dom_t = fe.ctx.timing_read()
+    fe.ctx.timing_enable([])
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames = world * B * args.steps
+    value = frames / elapsed
+    dom_ms, dom_launches = dom_t.get(dom, (0.0, 0))
+    avg_launch_s = dom_ms / max(dom_launches, 1) / 1e3
+    frames_per_launch = B  # every kernel of the step processes the whole batch in one launch
+    bpf = algorithmic_bytes_per_frame(W, H, args.nfeatures)
+    achieved = bpf * frames_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+
+    ate = None
+    if rank == 0 and args.ate_frames > 1:
+        aseq = synth.StereoSequence(seed=100, n_frames=args.ate_frames, W=W, H=H, device=dev)
+        La, Ra = aseq.frames(range(aseq.n))
+        afe = vo.StereoFrontEnd(W, H, aseq.K, synth.DIST_L, synth.BASELINE, batch=min(B, 32),
+                                nfeatures=args.nfeatures, device=dev)
+        rows, _, st = vo.run_sequence(afe, La, Ra, aseq.t)
+        gt = ev.tum_rows(aseq.t, aseq.T_wc)
+        # the estimate is the camera trajectory in the first camera's frame; Sim(3)-align
+        r = ev.ate(gt, rows)
+        ate = {"rmse_m": round(r["rmse"], 4), "frames": int(aseq.n), "poses": r["n"],
+               "pnp_failures": int((st == 0).sum()), "skipped": int((st == -1).sum())}
+        del afe
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_frames > 0:
+        cpu = cpu_baseline(args.cpu_frames, args.nfeatures, W, H)
+
+    if rank == 0:
+        out = {
+            "metric": "stereo frames/sec (extract+match+local-BA) at 600p, 1/8 MI355X; ATE RMSE",
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "mixed: u8/i16 integer (FAST, BRIEF, Hamming, SGM), f32 (ORB angle/Harris, back-projection), "
+                     "f64 (PnP)",
+            "data": "synthetic: ray-cast forest stereo along the 1018_00 GT path (seed = rank), "
+                    "BotanicGarden bag not available",
+            "config": {"workload": "stereo VO front end, configs[1]: 960x600, ORB nfeatures=1000, "
+                                   "BF-Hamming xcheck (L+R), SGBM-3way 96 disp, back-projection, PnP-RANSAC",
+                       "frames_per_step_per_gpu": B, "width": W, "height": H, "nfeatures": args.nfeatures,
+                       "local_ba": "not in this round's step (DESIGN.md)", "parallelism": f"seq-per-gpu x{world}"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                         "algorithmic_bytes_per_frame": bpf, "frames_per_launch": frames_per_launch,
+                         "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
+            "cpu_baseline": cpu,
+            "ate": ate,
+            "stages_ms_per_step": stage_ms,
+            "workspace_gb": round(fe.ctx.workspace_bytes / 1e9, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

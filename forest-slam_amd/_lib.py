@@ -47,7 +47,16 @@ SIGNATURES = {
                                       _P, _P, _P, _P]),
     "fvo_test_retain_best": (ctypes.c_int, [_P, _P, _I, _I, _P, _P, _P]),
     "fvo_debug_buffer": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
+    "fvo_kernel_count": (ctypes.c_int, []),
+    "fvo_kernel_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "fvo_timing_enable": (ctypes.c_int, [_P, ctypes.c_uint64]),
+    "fvo_timing_read": (ctypes.c_int, [_P, _P, _P]),
 }
+
+
+def kernel_names() -> list[str]:
+    L = load()
+    return [L.fvo_kernel_name(i).decode() for i in range(L.fvo_kernel_count())]
 
 
 def load(path: str = LIB_PATH):
@@ -133,6 +142,27 @@ class Context:
     @property
     def workspace_bytes(self) -> int:
         return int(self.L.fvo_workspace_bytes(self.h))
+
+    def timing_enable(self, names=None):
+        """Bracket launches of the named kernels (all if None, none if []) with HIP events."""
+        all_names = kernel_names()
+        if names is None:
+            mask = (1 << len(all_names)) - 1
+        else:
+            mask = 0
+            for n in names:
+                mask |= 1 << all_names.index(n)
+        self._check(self.L.fvo_timing_enable(self.h, mask))
+
+    def timing_read(self) -> dict:
+        """{kernel: (total_ms, launches)} for the launches recorded since the last read."""
+        import numpy as np
+        nk = self.L.fvo_kernel_count()
+        ms = np.zeros(nk, np.float64)
+        cnt = np.zeros(nk, np.int32)
+        self._check(self.L.fvo_timing_read(self.h, ms.ctypes.data_as(ctypes.c_void_p),
+                                           cnt.ctypes.data_as(ctypes.c_void_p)))
+        return {n: (float(ms[i]), int(cnt[i])) for i, n in enumerate(kernel_names()) if cnt[i] > 0}
 
     # ------------------------------------------------------------------ stages
     def orb(self, images: torch.Tensor, out=None):

@@ -125,10 +125,10 @@ int bf_run(fvo_ctx* ctx, const uint8_t* q, const int32_t* nq, const uint8_t* t, 
            int32_t* matches, int32_t* nmatch, hipStream_t s) {
   if ((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(t)) & 15)
     return fvo_fail(ctx, "descriptor buffers must be 16-byte aligned");
-  hipLaunchKernelGGL(k_bf_argmin, dim3((cap + kRowsPerBlock - 1) / kRowsPerBlock, batch, 2), dim3(kRowsPerBlock), 0,
-                     s, q, nq, t, nt, cap, ctx->bf_sidx, ctx->bf_sdist, ctx->bf_tidx);
-  hipLaunchKernelGGL(k_bf_finish, dim3(batch), dim3(256), 0, s, nq, nt, cap, ctx->bf_sidx, ctx->bf_sdist, ctx->bf_tidx,
-                     matches, nmatch);
+  FVO_TIMED(ctx, KN_BF_ARGMIN, s, hipLaunchKernelGGL(k_bf_argmin, dim3((cap + kRowsPerBlock - 1) / kRowsPerBlock, batch, 2), dim3(kRowsPerBlock), 0,
+                     s, q, nq, t, nt, cap, ctx->bf_sidx, ctx->bf_sdist, ctx->bf_tidx));
+  FVO_TIMED(ctx, KN_BF_FINISH, s, hipLaunchKernelGGL(k_bf_finish, dim3(batch), dim3(256), 0, s, nq, nt, cap, ctx->bf_sidx, ctx->bf_sdist, ctx->bf_tidx,
+                     matches, nmatch));
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }

@@ -10,6 +10,17 @@ int fvo_fail(fvo_ctx* ctx, const std::string& msg) {
   return -1;
 }
 
+hipEvent_t fvo_event(fvo_ctx* ctx) {
+  if (!ctx->tpool.empty()) {
+    hipEvent_t e = ctx->tpool.back();
+    ctx->tpool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
 extern "C" {
 
 int fvo_abi_version(void) { return FVO_ABI_VERSION; }
@@ -73,6 +84,8 @@ int fvo_create(int device, const fvo_config* cfg, fvo_ctx** out) {
 void fvo_destroy(fvo_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  for (auto& r : c->trecs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+  for (auto e : c->tpool) (void)hipEventDestroy(e);
   release(c);
   delete c;
 }
@@ -141,6 +154,39 @@ int fvo_pnp_ransac(fvo_ctx* c, const float* points3d, const float* points2d, con
   if (!(confidence > 0 && confidence < 1)) return fvo_fail(c, "confidence must be in (0,1)");
   return pnp_run(c, points3d, points2d, n_points, batch, cap, K, dist, reprojection_error, confidence, iterations,
                  rvec, tvec, T, status, inliers, (hipStream_t)stream);
+}
+
+int fvo_kernel_count(void) { return KN_COUNT; }
+
+const char* fvo_kernel_name(int id) {
+  static const char* names[KN_COUNT] = {
+      "orb_copy_level0", "orb_resize", "orb_fast_score", "orb_nms_count", "orb_row_scan", "orb_nms_compact",
+      "orb_select_fast", "orb_harris", "orb_select_harris", "orb_offsets", "orb_angle", "orb_blur", "orb_brief",
+      "bf_argmin", "bf_finish", "sgbm_hsum", "sgbm_vsum", "sgbm_vert", "sgbm_horiz", "sgbm_median", "backproject",
+      "pnp_ransac"};
+  return (id >= 0 && id < KN_COUNT) ? names[id] : "";
+}
+
+int fvo_timing_enable(fvo_ctx* c, uint64_t mask) {
+  if (!c) return -1;
+  c->tmask = mask;
+  return 0;
+}
+
+int fvo_timing_read(fvo_ctx* c, double* ms, int32_t* launches) {
+  if (!c || !ms || !launches) return -1;
+  for (int i = 0; i < KN_COUNT; ++i) { ms[i] = 0.0; launches[i] = 0; }
+  for (auto& r : c->trecs) {
+    FVO_HIP(c, hipEventSynchronize(r.b));
+    float t = 0.f;
+    FVO_HIP(c, hipEventElapsedTime(&t, r.a, r.b));
+    ms[r.id] += t;
+    launches[r.id] += 1;
+    c->tpool.push_back(r.a);
+    c->tpool.push_back(r.b);
+  }
+  c->trecs.clear();
+  return 0;
 }
 
 // Debug/test hook: device pointer + size of an internal workspace buffer of the last call.

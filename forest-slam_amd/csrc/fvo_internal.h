@@ -35,8 +35,23 @@ struct ResizeTab {
   int64_t xoff[FVO_MAX_LEVELS], yoff[FVO_MAX_LEVELS];
 };
 
+// Kernel ids for the optional per-launch event timing (fvo_timing_enable / _read).
+enum FvoKernel {
+  KN_ORB_COPY, KN_ORB_RESIZE, KN_ORB_FAST, KN_ORB_NMS_COUNT, KN_ORB_ROW_SCAN, KN_ORB_COMPACT, KN_ORB_SELECT1,
+  KN_ORB_HARRIS, KN_ORB_SELECT2, KN_ORB_OFFSETS, KN_ORB_ANGLE, KN_ORB_BLUR, KN_ORB_BRIEF, KN_BF_ARGMIN,
+  KN_BF_FINISH, KN_SG_HSUM, KN_SG_VSUM, KN_SG_VERT, KN_SG_HORIZ, KN_SG_MEDIAN, KN_BACKPROJECT, KN_PNP, KN_COUNT
+};
+
+struct TimingRec {
+  int id;
+  hipEvent_t a, b;
+};
+
 struct fvo_ctx {
   int device = 0;
+  uint64_t tmask = 0;                 // kernels whose launches are bracketed by events
+  std::vector<TimingRec> trecs;
+  std::vector<hipEvent_t> tpool;
   fvo_config cfg{};
   OrbGeom g{};
   std::string err;
@@ -86,6 +101,24 @@ int fvo_fail(fvo_ctx* ctx, const std::string& msg);
     if (e_ != hipSuccess) return fvo_fail(ctx, std::string(#expr) + ": " + hipGetErrorString(e_)); \
   } while (0)
 #define FVO_LAUNCH_CHECK(ctx) FVO_HIP(ctx, hipGetLastError())
+
+hipEvent_t fvo_event(fvo_ctx* ctx);
+// Launch `...` on stream `s`; when kernel `id` is in ctx->tmask, bracket it with events.
+#define FVO_TIMED(ctx, id, s, ...)                               \
+  do {                                                           \
+    const bool t_ = ((ctx)->tmask >> (id)) & 1ull;               \
+    hipEvent_t a_ = nullptr, b_ = nullptr;                       \
+    if (t_) {                                                    \
+      a_ = fvo_event(ctx);                                       \
+      (void)hipEventRecord(a_, s);                               \
+    }                                                            \
+    __VA_ARGS__;                                                 \
+    if (t_) {                                                    \
+      b_ = fvo_event(ctx);                                       \
+      (void)hipEventRecord(b_, s);                               \
+      (ctx)->trecs.push_back(TimingRec{(int)(id), a_, b_});      \
+    }                                                            \
+  } while (0)
 
 // Per-module init/launchers (defined in the .hip files).
 int orb_init(fvo_ctx* ctx);

@@ -794,32 +794,32 @@ int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride
   const int W = c.width, H = c.height;
   const int64_t total = g.total_px;
   const int thr = std::min(std::max(c.fast_threshold, 0), 255);
-  hipLaunchKernelGGL(k_copy_level0, dim3((W + 255) / 256, H, batch), dim3(256), 0, s, images, image_stride, pitch,
-                     ctx->pyr, total, W, H);
+  FVO_TIMED(ctx, KN_ORB_COPY, s, hipLaunchKernelGGL(k_copy_level0, dim3((W + 255) / 256, H, batch), dim3(256), 0, s, images, image_stride, pitch,
+                     ctx->pyr, total, W, H));
   for (int l = 1; l < L; ++l)
-    hipLaunchKernelGGL(k_resize, dim3((g.w[l] + 255) / 256, g.h[l], batch), dim3(256), 0, s, ctx->pyr, total, l,
+    FVO_TIMED(ctx, KN_ORB_RESIZE, s, hipLaunchKernelGGL(k_resize, dim3((g.w[l] + 255) / 256, g.h[l], batch), dim3(256), 0, s, ctx->pyr, total, l,
                        ctx->rt.xofs + ctx->rt.xoff[l], ctx->rt.xc1 + ctx->rt.xoff[l], ctx->rt.yofs + ctx->rt.yoff[l],
-                       ctx->rt.yc1 + ctx->rt.yoff[l]);
-  hipLaunchKernelGGL(k_fast_score, dim3((W + 255) / 256, g.total_rows, batch), dim3(256), 0, s, ctx->pyr, ctx->score,
-                     total, L, thr);
-  hipLaunchKernelGGL(k_nms_count, dim3(g.total_rows, batch), dim3(256), 0, s, ctx->score, ctx->rowcnt, total,
-                     g.total_rows, L, c.edge_threshold);
-  hipLaunchKernelGGL(k_row_scan, dim3(L, batch), dim3(256), 0, s, ctx->rowcnt, ctx->rowoff, ctx->ncand, g.total_rows,
-                     L);
-  hipLaunchKernelGGL(k_nms_compact, dim3(g.total_rows, batch), dim3(256), 0, s, ctx->score, ctx->rowoff, ctx->cand,
-                     total, g.cand_total, g.total_rows, L, c.edge_threshold);
-  hipLaunchKernelGGL(k_select<ElemFast>, dim3(L, batch), dim3(kSelThreads), 0, s, ctx->cand, ctx->ncand, ctx->nsel1,
-                     ctx->scratch, ctx->scratch_per, g.cand_total, L, 2);
-  hipLaunchKernelGGL(k_harris, dim3(32, L, batch), dim3(256), 0, s, ctx->pyr, ctx->cand, ctx->nsel1, ctx->hel, total,
-                     g.cand_total, L);
-  hipLaunchKernelGGL(k_select<ElemHarris>, dim3(L, batch), dim3(kSelThreads), 0, s, ctx->hel, ctx->nsel1, ctx->nsel2,
-                     ctx->scratch, ctx->scratch_per, g.cand_total, L, 1);
-  hipLaunchKernelGGL(k_offsets, dim3((batch + 63) / 64), dim3(64), 0, s, ctx->nsel2, ctx->koff, counts, batch, L, cap);
-  hipLaunchKernelGGL(k_angle, dim3(16, L, batch), dim3(256), 0, s, ctx->pyr, ctx->hel, ctx->nsel2, ctx->koff, kp,
-                     total, g.cand_total, L, cap, c.patch_size);
-  hipLaunchKernelGGL(k_blur, dim3((W + 255) / 256, g.total_rows, batch), dim3(256), 0, s, ctx->pyr, ctx->blur, total,
-                     L);
-  hipLaunchKernelGGL(k_brief, dim3(64, batch), dim3(256), 0, s, ctx->blur, kp, counts, desc, total, cap);
+                       ctx->rt.yc1 + ctx->rt.yoff[l]));
+  FVO_TIMED(ctx, KN_ORB_FAST, s, hipLaunchKernelGGL(k_fast_score, dim3((W + 255) / 256, g.total_rows, batch), dim3(256), 0, s, ctx->pyr, ctx->score,
+                     total, L, thr));
+  FVO_TIMED(ctx, KN_ORB_NMS_COUNT, s, hipLaunchKernelGGL(k_nms_count, dim3(g.total_rows, batch), dim3(256), 0, s, ctx->score, ctx->rowcnt, total,
+                     g.total_rows, L, c.edge_threshold));
+  FVO_TIMED(ctx, KN_ORB_ROW_SCAN, s, hipLaunchKernelGGL(k_row_scan, dim3(L, batch), dim3(256), 0, s, ctx->rowcnt, ctx->rowoff, ctx->ncand, g.total_rows,
+                     L));
+  FVO_TIMED(ctx, KN_ORB_COMPACT, s, hipLaunchKernelGGL(k_nms_compact, dim3(g.total_rows, batch), dim3(256), 0, s, ctx->score, ctx->rowoff, ctx->cand,
+                     total, g.cand_total, g.total_rows, L, c.edge_threshold));
+  FVO_TIMED(ctx, KN_ORB_SELECT1, s, hipLaunchKernelGGL(k_select<ElemFast>, dim3(L, batch), dim3(kSelThreads), 0, s, ctx->cand, ctx->ncand, ctx->nsel1,
+                     ctx->scratch, ctx->scratch_per, g.cand_total, L, 2));
+  FVO_TIMED(ctx, KN_ORB_HARRIS, s, hipLaunchKernelGGL(k_harris, dim3(32, L, batch), dim3(256), 0, s, ctx->pyr, ctx->cand, ctx->nsel1, ctx->hel, total,
+                     g.cand_total, L));
+  FVO_TIMED(ctx, KN_ORB_SELECT2, s, hipLaunchKernelGGL(k_select<ElemHarris>, dim3(L, batch), dim3(kSelThreads), 0, s, ctx->hel, ctx->nsel1, ctx->nsel2,
+                     ctx->scratch, ctx->scratch_per, g.cand_total, L, 1));
+  FVO_TIMED(ctx, KN_ORB_OFFSETS, s, hipLaunchKernelGGL(k_offsets, dim3((batch + 63) / 64), dim3(64), 0, s, ctx->nsel2, ctx->koff, counts, batch, L, cap));
+  FVO_TIMED(ctx, KN_ORB_ANGLE, s, hipLaunchKernelGGL(k_angle, dim3(16, L, batch), dim3(256), 0, s, ctx->pyr, ctx->hel, ctx->nsel2, ctx->koff, kp,
+                     total, g.cand_total, L, cap, c.patch_size));
+  FVO_TIMED(ctx, KN_ORB_BLUR, s, hipLaunchKernelGGL(k_blur, dim3((W + 255) / 256, g.total_rows, batch), dim3(256), 0, s, ctx->pyr, ctx->blur, total,
+                     L));
+  FVO_TIMED(ctx, KN_ORB_BRIEF, s, hipLaunchKernelGGL(k_brief, dim3(64, batch), dim3(256), 0, s, ctx->blur, kp, counts, desc, total, cap));
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }

@@ -978,8 +978,8 @@ int backproject_run(fvo_ctx* ctx, const int16_t* disp, const float* kp0, const f
                     const int32_t* nmatch, int batch, int cap, const double* K, double baseline, float* P3, float* p2,
                     int32_t* npts, hipStream_t s) {
   CamF c{K[0], K[4], K[2], K[5], K[0] * baseline};
-  hipLaunchKernelGGL(k_backproject, dim3(batch), dim3(256), 0, s, disp, kp0, kp1, matches, nmatch, ctx->cfg.width,
-                     ctx->cfg.height, cap, c, P3, p2, npts);
+  FVO_TIMED(ctx, KN_BACKPROJECT, s, hipLaunchKernelGGL(k_backproject, dim3(batch), dim3(256), 0, s, disp, kp0, kp1, matches, nmatch, ctx->cfg.width,
+                     ctx->cfg.height, cap, c, P3, p2, npts));
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }
@@ -990,8 +990,8 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
   if (cap > ctx->kp_cap) return fvo_fail(ctx, "pnp: cap exceeds the context keypoint capacity");
   Cam c{K[0], K[4], K[2], K[5], {dist[0], dist[1], dist[2], dist[3], dist[4]}};
   float thr2 = (float)((double)reproj * reproj);
-  hipLaunchKernelGGL(k_pnp, dim3(batch), dim3(64), 0, s, P3, p2, npts, cap, c, thr2, conf, iters, rvec, tvec, T, status,
-                     inliers, ctx->pnp_sub, ctx->pnp_hyp);
+  FVO_TIMED(ctx, KN_PNP, s, hipLaunchKernelGGL(k_pnp, dim3(batch), dim3(64), 0, s, P3, p2, npts, cap, c, thr2, conf, iters, rvec, tvec, T, status,
+                     inliers, ctx->pnp_sub, ctx->pnp_hyp));
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }

@@ -422,29 +422,29 @@ int sgbm_run(fvo_ctx* ctx, const uint8_t* L, const uint8_t* R, int batch, int64_
   uint16_t* cost = ctx->sg_cost;
   uint16_t* cost_extra = ctx->sg_cost + (int64_t)batch * p.H * plane;
   size_t shm = (size_t)12 * p.W + (size_t)(kChunk + 6) * p.D;
-  hipLaunchKernelGGL(k_sg_hsum, dim3((p.width1 + kChunk - 1) / kChunk, p.H, batch), dim3(256), shm, s, L, R,
-                     image_stride, pitch, p, hsum);
-  hipLaunchKernelGGL(k_sg_vsum, dim3((unsigned)((plane + 255) / 256), batch), dim3(256), 0, s, hsum, cost, cost_extra,
-                     p);
+  FVO_TIMED(ctx, KN_SG_HSUM, s, hipLaunchKernelGGL(k_sg_hsum, dim3((p.width1 + kChunk - 1) / kChunk, p.H, batch), dim3(256), shm, s, L, R,
+                     image_stride, pitch, p, hsum));
+  FVO_TIMED(ctx, KN_SG_VSUM, s, hipLaunchKernelGGL(k_sg_vsum, dim3((unsigned)((plane + 255) / 256), batch), dim3(256), 0, s, hsum, cost, cost_extra,
+                     p));
   dim3 gv((p.width1 + 63) / 64, p.nstripes, batch), gh((p.H + 63) / 64, batch);
   switch (p.D) {
     case 64:
-      hipLaunchKernelGGL(k_sg_vert<64>, gv, dim3(64), 0, s, cost, cost_extra, ctx->sg_V, p);
-      hipLaunchKernelGGL(k_sg_horiz<64>, gh, dim3(64), 0, s, cost, ctx->sg_V, ctx->sg_L, ctx->sg_raw, ctx->sg_d2,
-                         ctx->sg_d2c, p);
+      FVO_TIMED(ctx, KN_SG_VERT, s, hipLaunchKernelGGL(k_sg_vert<64>, gv, dim3(64), 0, s, cost, cost_extra, ctx->sg_V, p));
+      FVO_TIMED(ctx, KN_SG_HORIZ, s, hipLaunchKernelGGL(k_sg_horiz<64>, gh, dim3(64), 0, s, cost, ctx->sg_V, ctx->sg_L, ctx->sg_raw, ctx->sg_d2,
+                         ctx->sg_d2c, p));
       break;
     case 96:
-      hipLaunchKernelGGL(k_sg_vert<96>, gv, dim3(64), 0, s, cost, cost_extra, ctx->sg_V, p);
-      hipLaunchKernelGGL(k_sg_horiz<96>, gh, dim3(64), 0, s, cost, ctx->sg_V, ctx->sg_L, ctx->sg_raw, ctx->sg_d2,
-                         ctx->sg_d2c, p);
+      FVO_TIMED(ctx, KN_SG_VERT, s, hipLaunchKernelGGL(k_sg_vert<96>, gv, dim3(64), 0, s, cost, cost_extra, ctx->sg_V, p));
+      FVO_TIMED(ctx, KN_SG_HORIZ, s, hipLaunchKernelGGL(k_sg_horiz<96>, gh, dim3(64), 0, s, cost, ctx->sg_V, ctx->sg_L, ctx->sg_raw, ctx->sg_d2,
+                         ctx->sg_d2c, p));
       break;
     default:
-      hipLaunchKernelGGL(k_sg_vert<128>, gv, dim3(64), 0, s, cost, cost_extra, ctx->sg_V, p);
-      hipLaunchKernelGGL(k_sg_horiz<128>, gh, dim3(64), 0, s, cost, ctx->sg_V, ctx->sg_L, ctx->sg_raw, ctx->sg_d2,
-                         ctx->sg_d2c, p);
+      FVO_TIMED(ctx, KN_SG_VERT, s, hipLaunchKernelGGL(k_sg_vert<128>, gv, dim3(64), 0, s, cost, cost_extra, ctx->sg_V, p));
+      FVO_TIMED(ctx, KN_SG_HORIZ, s, hipLaunchKernelGGL(k_sg_horiz<128>, gh, dim3(64), 0, s, cost, ctx->sg_V, ctx->sg_L, ctx->sg_raw, ctx->sg_d2,
+                         ctx->sg_d2c, p));
       break;
   }
-  hipLaunchKernelGGL(k_sg_median, dim3((p.W + 255) / 256, p.H, batch), dim3(256), 0, s, ctx->sg_raw, disp, p.W, p.H);
+  FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.W + 255) / 256, p.H, batch), dim3(256), 0, s, ctx->sg_raw, disp, p.W, p.H));
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }

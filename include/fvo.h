@@ -137,6 +137,16 @@ int fvo_pnp_ransac(fvo_ctx* ctx, const float* points3d, const float* points2d, c
 int fvo_test_retain_best(fvo_ctx* ctx, const float* keys, int32_t n, int32_t keep, int32_t* idx_out, int32_t* n_out,
                          fvo_stream stream);
 
+/* Per-kernel timing with HIP events recorded on the launch stream (measurement hooks for
+ * bench.py).  mask: bit i brackets every launch of kernel i (0..fvo_kernel_count()-1,
+ * names from fvo_kernel_name()).  fvo_timing_read synchronises on the recorded events,
+ * writes the summed milliseconds and launch counts per kernel (arrays of
+ * fvo_kernel_count() entries) and clears the record. */
+int fvo_kernel_count(void);
+const char* fvo_kernel_name(int id);
+int fvo_timing_enable(fvo_ctx* ctx, uint64_t mask);
+int fvo_timing_read(fvo_ctx* ctx, double* ms, int32_t* launches);
+
 /* Debug hook: device pointer and byte size of an internal buffer of the most recent ORB
  * call (0 pyramid, 1 blurred pyramid, 2 FAST score map, 3/4/5 per-level counts before /
  * after the two retainBest passes).  For stage-by-stage parity tests only. */
