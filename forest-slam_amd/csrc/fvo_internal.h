@@ -86,10 +86,12 @@ struct fvo_ctx {
   int32_t* sg_d2c = nullptr;    // [B][H][W] packed cost/x for disp2
   int sg_extra_rows = 0;
   // pose workspace
-  double* pnp_hyp = nullptr;    // [B][iters][6]
-  int32_t* pnp_good = nullptr;  // [B][iters]
-  int32_t* pnp_sub = nullptr;   // [B][iters][5]
-  int32_t* pnp_niters = nullptr; // [B]
+  double* pnp_hyp = nullptr;      // [B][cap][2] normalised inlier points (refinement)
+  int32_t* pnp_sub = nullptr;     // [B][cap] inlier indices
+  int16_t* pnp_subsets = nullptr; // [B][max_iters][5] RANSAC subsets
+  double* pnp_models = nullptr;   // [B][max_iters][6] hypotheses (rvec, tvec)
+  int32_t* pnp_good = nullptr;    // [B][max_iters] inlier counts
+  void* pnp_state = nullptr;      // [B] PnpState
   int32_t pnp_max_iters = 0;
 };
 

@@ -816,110 +816,143 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
   __syncthreads();
 }
 
-__global__ __launch_bounds__(64) void k_pnp(const float* __restrict__ P3all, const float* __restrict__ p2all,
-                                            const int32_t* __restrict__ npts, int cap, Cam K, float thr2, double conf,
-                                            int maxIters, double* __restrict__ rvec, double* __restrict__ tvec,
-                                            double* __restrict__ T, int32_t* __restrict__ status,
-                                            uint8_t* __restrict__ inliers, int32_t* __restrict__ inl_idx,
-                                            double* __restrict__ mn_buf) {
-  __shared__ PnpShared sh;
-  const int b = blockIdx.x, lane = threadIdx.x;
+struct PnpState {
+  int maxGood, niters, best_it, n;
+};
+
+// Subsets of every potential RANSAC iteration, drawn exactly as getSubset() with
+// RNG(-1): 5 distinct indices from rng.uniform(0, n) with rejection of repeats.  The
+// draws depend only on n, so they can be generated before any hypothesis is scored.
+__global__ void k_pnp_subsets(const int32_t* __restrict__ npts, int batch, int cap, int maxIters,
+                              int16_t* __restrict__ sub, PnpState* __restrict__ state) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
   int n = npts[b];
   n = n < 0 ? 0 : (n > cap ? cap : n);
+  PnpState st;
+  st.maxGood = 0;
+  st.niters = maxIters;
+  st.best_it = -1;
+  st.n = n;
+  state[b] = st;
+  if (n < 6) return;
+  RNG rng{~0ull};
+  int16_t* o = sub + (int64_t)b * maxIters * 5;
+  for (int it = 0; it < maxIters; ++it) {
+    int idx[5];
+    for (int i = 0; i < 5; ++i) {
+      int j;
+      for (;;) {
+        j = rng.uniform(0, n);
+        bool dup = false;
+        for (int q = 0; q < i; ++q) dup |= idx[q] == j;
+        if (!dup) break;
+      }
+      idx[i] = j;
+      o[it * 5 + i] = (int16_t)j;
+    }
+  }
+}
+
+// One lane per RANSAC iteration: EPnP on its subset (undistorted, float32-rounded
+// normalised points, as solvePnP(SOLVEPNP_EPNP) sees them) and the inlier count of the
+// hypothesis over all points (projectPoints in fp64, error in float32).  Blocks whose
+// first iteration is past the frame's current iteration bound exit immediately.
+__global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ P3all, const float* __restrict__ p2all,
+                                                int cap, Cam K, float thr2, int maxIters, int it_lo,
+                                                const int16_t* __restrict__ sub, const PnpState* __restrict__ state,
+                                                double* __restrict__ model, int32_t* __restrict__ good) {
+  extern __shared__ __attribute__((aligned(16))) float spts[];  // [n][5] x,y,z,u,v
+  const int b = blockIdx.y;
+  const int it = it_lo + blockIdx.x * 64 + threadIdx.x;
+  const PnpState st = state[b];
+  const int n = st.n;
+  if (n < 6 || it_lo + (int)blockIdx.x * 64 >= min(st.niters, maxIters)) return;
+  const float* P3 = P3all + (int64_t)b * cap * 3;
+  const float* p2 = p2all + (int64_t)b * cap * 2;
+  for (int i = threadIdx.x; i < n; i += 64) {
+    spts[i * 5 + 0] = P3[3 * i];
+    spts[i * 5 + 1] = P3[3 * i + 1];
+    spts[i * 5 + 2] = P3[3 * i + 2];
+    spts[i * 5 + 3] = p2[2 * i];
+    spts[i * 5 + 4] = p2[2 * i + 1];
+  }
+  __syncthreads();
+  if (it >= maxIters) return;
+  const int16_t* sb = sub + ((int64_t)b * maxIters + it) * 5;
+  EPnPd<5> e;
+  e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
+  for (int i = 0; i < 5; ++i) {
+    int j = sb[i];
+    for (int c = 0; c < 3; ++c) e.pws[3 * i + c] = (double)spts[j * 5 + c];
+    double xy[2];
+    dundistort(K, (double)spts[j * 5 + 3], (double)spts[j * 5 + 4], xy);
+    float fx = (float)xy[0], fy = (float)xy[1];
+    e.us[2 * i] = fx * K.fx + K.cx;
+    e.us[2 * i + 1] = fy * K.fy + K.cy;
+  }
+  double R[9], t[3], r[3], dR[27];
+  e.compute_pose(R, t);
+  rod_R2r(R, r);
+  double* mo = model + ((int64_t)b * maxIters + it) * 6;
+  for (int i = 0; i < 3; ++i) { mo[i] = r[i]; mo[3 + i] = t[i]; }
+  rod_r2R(r, R, dR);
+  int g = 0;
+  for (int i = 0; i < n; ++i) {
+    const float* q = spts + i * 5;
+    double M[3] = {(double)q[0], (double)q[1], (double)q[2]}, uv[2];
+    dproject(K, R, dR, t, M, uv, nullptr);
+    float du = q[3] - (float)uv[0], dv = q[4] - (float)uv[1];
+    g += (du * du + dv * dv) <= thr2;
+  }
+  good[(int64_t)b * maxIters + it] = g;
+}
+
+// RANSACPointSetRegistrator::run's acceptance loop replayed in iteration order over
+// [it_lo, it_hi): accept iff goodCount > max(maxGoodCount, 4); niters is updated with
+// RANSACUpdateNumIters(confidence, (n - good)/n, 5, niters) and bounds the loop.
+__global__ void k_pnp_replay(int batch, int maxIters, int it_lo, int it_hi, double conf,
+                             const int32_t* __restrict__ good, PnpState* __restrict__ state) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  PnpState st = state[b];
+  if (st.n < 6) return;
+  for (int it = it_lo; it < it_hi && it < st.niters; ++it) {
+    int g = good[(int64_t)b * maxIters + it];
+    if (g > max(st.maxGood, 4)) {
+      st.best_it = it;
+      st.maxGood = g;
+      st.niters = update_num_iters(conf, (double)(st.n - g) / st.n, 5, st.niters);
+    }
+  }
+  state[b] = st;
+}
+
+__global__ __launch_bounds__(64) void k_pnp_refine(const float* __restrict__ P3all, const float* __restrict__ p2all,
+                                                   int cap, Cam K, float thr2, int maxIters,
+                                                   const PnpState* __restrict__ state,
+                                                   const double* __restrict__ model, double* __restrict__ rvec,
+                                                   double* __restrict__ tvec, double* __restrict__ T,
+                                                   int32_t* __restrict__ status, uint8_t* __restrict__ inliers,
+                                                   int32_t* __restrict__ inl_idx, double* __restrict__ mn_buf) {
+  __shared__ PnpShared sh;
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const PnpState st = state[b];
+  const int n = st.n;
   const float* P3 = P3all + (int64_t)b * cap * 3;
   const float* p2 = p2all + (int64_t)b * cap * 2;
   double* Tout = T + (int64_t)b * 16;
-  if (n < 6) {
+  if (n < 6 || st.maxGood <= 0) {
     if (lane < 16) Tout[lane] = (lane % 5 == 0) ? 1.0 : 0.0;
     if (lane < 3) { rvec[b * 3 + lane] = 0; tvec[b * 3 + lane] = 0; }
     if (inliers)
       for (int i = lane; i < cap; i += 64) inliers[(int64_t)b * cap + i] = 0;
-    if (lane == 0) status[b] = -1;
+    if (lane == 0) status[b] = n < 6 ? -1 : 0;
     return;
   }
-  const int mp = 5;
-  if (lane == 0) {
-    sh.maxGood = 0;
-    sh.niters = maxIters;
-    sh.done = 0;
-    sh.next_iter = 0;
-    sh.rng = ~0ull;
-  }
+  const double* mo = model + ((int64_t)b * maxIters + st.best_it) * 6;
+  if (lane < 6) sh.best[lane] = mo[lane];
   __syncthreads();
-  while (!sh.done) {
-    const int it0 = sh.next_iter;
-    if (lane == 0) {
-      RNG rng{sh.rng};
-      for (int k = 0; k < kChunk; ++k) {
-        for (int i = 0; i < mp; ++i) {
-          int j;
-          for (;;) {
-            j = rng.uniform(0, n);
-            bool dup = false;
-            for (int q = 0; q < i; ++q) dup |= sh.sub[k][q] == j;
-            if (!dup) break;
-          }
-          sh.sub[k][i] = j;
-        }
-      }
-      sh.rng = rng.state;
-    }
-    __syncthreads();
-    // hypothesis for iteration it0 + lane
-    {
-      EPnPd<5> e;
-      e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
-      for (int i = 0; i < mp; ++i) {
-        int j = sh.sub[lane][i];
-        for (int c = 0; c < 3; ++c) e.pws[3 * i + c] = (double)P3[3 * j + c];
-        double xy[2];
-        dundistort(K, (double)p2[2 * j], (double)p2[2 * j + 1], xy);
-        float fx = (float)xy[0], fy = (float)xy[1];
-        e.us[2 * i] = fx * K.fx + K.cx;
-        e.us[2 * i + 1] = fy * K.fy + K.cy;
-      }
-      double R[9], t[3], r[3], dR[27];
-      e.compute_pose(R, t);
-      rod_R2r(R, r);
-      for (int i = 0; i < 3; ++i) { sh.model[lane][i] = r[i]; sh.model[lane][3 + i] = t[i]; }
-      rod_r2R(r, R, dR);
-      int good = 0;
-      for (int i = 0; i < n; ++i) {
-        double M[3] = {(double)P3[3 * i], (double)P3[3 * i + 1], (double)P3[3 * i + 2]}, uv[2];
-        dproject(K, R, dR, t, M, uv, nullptr);
-        float du = p2[2 * i] - (float)uv[0], dv = p2[2 * i + 1] - (float)uv[1];
-        float err = du * du + dv * dv;
-        good += err <= thr2;
-      }
-      sh.good[lane] = good;
-    }
-    __syncthreads();
-    if (lane == 0) {
-      int k = 0;
-      for (; k < kChunk; ++k) {
-        int iter = it0 + k;
-        if (iter >= sh.niters) break;
-        int g = sh.good[k];
-        if (g > max(sh.maxGood, mp - 1)) {
-          for (int i = 0; i < 6; ++i) sh.best[i] = sh.model[k][i];
-          sh.maxGood = g;
-          sh.niters = update_num_iters(conf, (double)(n - g) / n, mp, sh.niters);
-        }
-      }
-      sh.next_iter = it0 + kChunk;
-      if (sh.next_iter >= sh.niters || k < kChunk) sh.done = 1;
-    }
-    __syncthreads();
-  }
-  if (sh.maxGood <= 0) {
-    if (lane < 16) Tout[lane] = (lane % 5 == 0) ? 1.0 : 0.0;
-    if (lane < 3) { rvec[b * 3 + lane] = 0; tvec[b * 3 + lane] = 0; }
-    if (inliers)
-      for (int i = lane; i < cap; i += 64) inliers[(int64_t)b * cap + i] = 0;
-    if (lane == 0) status[b] = 0;
-    return;
-  }
-  // inlier mask of the best model + ordered compaction of inlier indices
   int* inl = inl_idx + (int64_t)b * cap;
   {
     double r[3] = {sh.best[0], sh.best[1], sh.best[2]}, t[3] = {sh.best[3], sh.best[4], sh.best[5]};
@@ -968,9 +1001,12 @@ __global__ __launch_bounds__(64) void k_pnp(const float* __restrict__ P3all, con
 
 int pose_init(fvo_ctx* ctx) {
   ctx->pnp_max_iters = 1000;
-  const int64_t n = (int64_t)ctx->cfg.max_batch * ctx->kp_cap;
+  const int64_t B = ctx->cfg.max_batch, n = B * ctx->kp_cap, it = B * ctx->pnp_max_iters;
   int rc;
-  if ((rc = fvo_alloc(ctx, &ctx->pnp_sub, n)) || (rc = fvo_alloc(ctx, &ctx->pnp_hyp, 2 * n))) return rc;
+  if ((rc = fvo_alloc(ctx, &ctx->pnp_sub, n)) || (rc = fvo_alloc(ctx, &ctx->pnp_hyp, 2 * n)) ||
+      (rc = fvo_alloc(ctx, &ctx->pnp_subsets, it * 5)) || (rc = fvo_alloc(ctx, &ctx->pnp_models, it * 6)) ||
+      (rc = fvo_alloc(ctx, &ctx->pnp_good, it)) || (rc = fvo_alloc(ctx, (PnpState**)&ctx->pnp_state, B)))
+    return rc;
   return 0;
 }
 
@@ -978,8 +1014,9 @@ int backproject_run(fvo_ctx* ctx, const int16_t* disp, const float* kp0, const f
                     const int32_t* nmatch, int batch, int cap, const double* K, double baseline, float* P3, float* p2,
                     int32_t* npts, hipStream_t s) {
   CamF c{K[0], K[4], K[2], K[5], K[0] * baseline};
-  FVO_TIMED(ctx, KN_BACKPROJECT, s, hipLaunchKernelGGL(k_backproject, dim3(batch), dim3(256), 0, s, disp, kp0, kp1, matches, nmatch, ctx->cfg.width,
-                     ctx->cfg.height, cap, c, P3, p2, npts));
+  FVO_TIMED(ctx, KN_BACKPROJECT, s, hipLaunchKernelGGL(k_backproject, dim3(batch), dim3(256), 0, s, disp, kp0, kp1,
+                                                       matches, nmatch, ctx->cfg.width, ctx->cfg.height, cap, c, P3,
+                                                       p2, npts));
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }
@@ -989,9 +1026,29 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
             int32_t* status, uint8_t* inliers, hipStream_t s) {
   if (cap > ctx->kp_cap) return fvo_fail(ctx, "pnp: cap exceeds the context keypoint capacity");
   Cam c{K[0], K[4], K[2], K[5], {dist[0], dist[1], dist[2], dist[3], dist[4]}};
-  float thr2 = (float)((double)reproj * reproj);
-  FVO_TIMED(ctx, KN_PNP, s, hipLaunchKernelGGL(k_pnp, dim3(batch), dim3(64), 0, s, P3, p2, npts, cap, c, thr2, conf, iters, rvec, tvec, T, status,
-                     inliers, ctx->pnp_sub, ctx->pnp_hyp));
+  const float thr2 = (float)((double)reproj * reproj);
+  const int maxIters = iters;
+  PnpState* st = (PnpState*)ctx->pnp_state;
+  const size_t shm = (size_t)cap * 5 * sizeof(float);
+  if (shm > 64 * 1024)
+    FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_pnp_hyp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  const int first = std::min(maxIters, 128);
+  FVO_TIMED(ctx, KN_PNP, s, {
+    hipLaunchKernelGGL(k_pnp_subsets, dim3((batch + 63) / 64), dim3(64), 0, s, npts, batch, cap, maxIters,
+                       ctx->pnp_subsets, st);
+    hipLaunchKernelGGL(k_pnp_hyp, dim3((first + 63) / 64, batch), dim3(64), shm, s, P3, p2, cap, c, thr2, maxIters, 0,
+                       ctx->pnp_subsets, st, ctx->pnp_models, ctx->pnp_good);
+    hipLaunchKernelGGL(k_pnp_replay, dim3((batch + 63) / 64), dim3(64), 0, s, batch, maxIters, 0, first, conf,
+                       ctx->pnp_good, st);
+    if (maxIters > first) {
+      hipLaunchKernelGGL(k_pnp_hyp, dim3((maxIters - first + 63) / 64, batch), dim3(64), shm, s, P3, p2, cap, c, thr2,
+                         maxIters, first, ctx->pnp_subsets, st, ctx->pnp_models, ctx->pnp_good);
+      hipLaunchKernelGGL(k_pnp_replay, dim3((batch + 63) / 64), dim3(64), 0, s, batch, maxIters, first, maxIters, conf,
+                         ctx->pnp_good, st);
+    }
+    hipLaunchKernelGGL(k_pnp_refine, dim3(batch), dim3(64), 0, s, P3, p2, cap, c, thr2, maxIters, st,
+                       ctx->pnp_models, rvec, tvec, T, status, inliers, ctx->pnp_sub, ctx->pnp_hyp);
+  });
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }
