@@ -162,7 +162,7 @@ const char* fvo_kernel_name(int id) {
   static const char* names[KN_COUNT] = {
       "orb_copy_level0", "orb_resize", "orb_fast_score", "orb_nms_count", "orb_row_scan", "orb_nms_compact",
       "orb_select_fast", "orb_harris", "orb_select_harris", "orb_offsets", "orb_angle", "orb_blur", "orb_brief",
-      "bf_argmin", "bf_finish", "sgbm_hsum", "sgbm_vsum", "sgbm_vert", "sgbm_horiz", "sgbm_median", "backproject",
+      "bf_argmin", "bf_finish", "sgbm_hsum", "sgbm_vert", "sgbm_horiz", "sgbm_median", "backproject",
       "pnp_ransac"};
   return (id >= 0 && id < KN_COUNT) ? names[id] : "";
 }

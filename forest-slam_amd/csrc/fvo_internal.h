@@ -39,7 +39,7 @@ struct ResizeTab {
 enum FvoKernel {
   KN_ORB_COPY, KN_ORB_RESIZE, KN_ORB_FAST, KN_ORB_NMS_COUNT, KN_ORB_ROW_SCAN, KN_ORB_COMPACT, KN_ORB_SELECT1,
   KN_ORB_HARRIS, KN_ORB_SELECT2, KN_ORB_OFFSETS, KN_ORB_ANGLE, KN_ORB_BLUR, KN_ORB_BRIEF, KN_BF_ARGMIN,
-  KN_BF_FINISH, KN_SG_HSUM, KN_SG_VSUM, KN_SG_VERT, KN_SG_HORIZ, KN_SG_MEDIAN, KN_BACKPROJECT, KN_PNP, KN_COUNT
+  KN_BF_FINISH, KN_SG_HSUM, KN_SG_VERT, KN_SG_HORIZ, KN_SG_MEDIAN, KN_BACKPROJECT, KN_PNP, KN_COUNT
 };
 
 struct TimingRec {
@@ -78,13 +78,12 @@ struct fvo_ctx {
   int32_t* bf_sdist = nullptr;
   int32_t* bf_tidx = nullptr;
   // SGBM workspace
-  uint16_t* sg_cost = nullptr;  // [B][H + extra][width1][D]
-  uint16_t* sg_L = nullptr;     // [B][H][width1][D] left->right pass
-  uint16_t* sg_V = nullptr;     // [B][H][width1][D] top-down pass (output rows)
-  int16_t* sg_raw = nullptr;    // [B][H][W] pre-median disparity
-  int16_t* sg_d2 = nullptr;     // [B][H][W] right-view disparity (pseudo LR check)
-  int32_t* sg_d2c = nullptr;    // [B][H][W] packed cost/x for disp2
-  int sg_extra_rows = 0;
+  uint16_t* sg_cost = nullptr;  // hsum [B][H][width1][D], then the left->right pass L [B][width1][D/8][H]x8
+  uint16_t* sg_L = nullptr;     // cost C [B][width1][D/8][H]x8
+  uint16_t* sg_V = nullptr;     // top-down pass V [B][width1][D/8][H]x8
+  int16_t* sg_raw = nullptr;    // [B][W][H] pre-median disparity (transposed)
+  int16_t* sg_d2 = nullptr;     // [B][W][H] right-view disparity (pseudo LR check)
+  int16_t* sg_d2c = nullptr;    // [B][W][H] right-view best cost
   // pose workspace
   double* pnp_hyp = nullptr;      // [B][cap][2] normalised inlier points (refinement)
   int32_t* pnp_sub = nullptr;     // [B][cap] inlier indices

@@ -2,18 +2,22 @@
 // get_disparity_map (ros_ws/src/stereo_slam.py:108-117): numDisparities 96, minDisparity 0,
 // blockSize 7, P1 392, P2 1568, 3-way aggregation, 4 fixed stripes, then medianBlur(3).
 //
-// Layout in HBM (per pair b): every volume is [row][x1][d] u16 with x1 = x - max(maxD,0)
-// in [0, width1) and d in [0, D): a row slice is width1*D*2 bytes (166 KB at 600p).
-//   k_sg_hsum    BT pixel cost (x-Sobel clipped + intensity>>2) staged per row chunk in
-//                LDS, 7-tap horizontal box sum (clamped) -> hsum volume
-//   k_sg_vsum    7-tap vertical running sum (rows clamped to [0,H-1]) -> cost volume C,
-//                plus the 3 stripe-start rows whose window clamps at the stripe's first row
-//   k_sg_vert    top->down SGM path, one lane per column x1, all D in packed u16x2 VGPRs,
-//                restarted at each stripe's first processed row (OpenCV's overlap rule)
-//   k_sg_horiz   left->right path (stored), right->left path fused with S = L+R+V, WTA,
-//                parabolic sub-pixel step and the pseudo left-right check; one lane per row
-//   k_sg_median  3x3 median (replicated border) -> int16 disparity*16
-// Integer arithmetic only; results are bit-identical to oracle/sgbm_ref.cpp.
+// Volumes per pair, all [row][x1][d] u16 (x1 = x - max(maxD,0) in [0,width1), d in [0,D)):
+//   hsum (k_sg_hsum -> k_sg_vert), C and V (k_sg_vert -> k_sg_horiz), LV = L + V (the
+//   left->right pass, written over hsum).  raw / d2 / d2c are [x][row] int16.
+// Kernels
+//   k_sg_hsum<D>   thread per (d, 64-column segment): BT pixel cost of both channels in one
+//                  u16x2 word from LDS-staged row planes, 7-wide sliding window along x1
+//   k_sg_vert<D>   quad of lanes per column (D/4 disparities per lane): 7-row vertical box
+//                  sum as a running sum (clamped to the stripe's first row and to H-1, the
+//                  overlap rule of OpenCV's 4 stripes) fused with the top->down path
+//   k_sg_horiz<D>  quad of lanes per row: left->right path (stores LV), right->left path
+//                  fused with S = LV + R, first-minimum WTA, integer parabolic sub-pixel,
+//                  right-view disparity and the pseudo left-right check
+//   k_sg_median    3x3 median (replicated border) -> int16 disparity*16
+// Path states are packed u16x2 VGPRs (v_pk_add/sub/min_u16, v_alignbit for d-1 / d+1);
+// neighbours across the quad come from DPP quad permutes.  Integer arithmetic only;
+// bit-identical to oracle/sgbm_ref.cpp.
 #include "fvo_internal.h"
 
 namespace {
@@ -29,330 +33,339 @@ struct SgParams {
   int W, H, D, minD, minX1, width1, P1, P2, ftzero, disp12, ss, ov, nstripes;
 };
 
-// ------------------------------------------------------------------ pixel cost + hsum
-constexpr int kChunk = 256;  // x1 outputs per block
+// SGM recurrence for one packed pair k of a lane's disparity run, in place.  `old_km1`
+// carries the previous value of pair k-1 (already overwritten); lo0 / hiN are the words
+// that border the run (sentinels, or the neighbour lane's old values).
+template <int NPL>
+__device__ __forceinline__ uint32_t sgm_pair(uint32_t* st, int k, uint32_t& old_km1, uint32_t c, u16x2 P1,
+                                             u16x2 mp2, u16x2 mpv, uint32_t lo0, uint32_t hiN) {
+  uint32_t cur = st[k];
+  uint32_t lo = k > 0 ? old_km1 : lo0;
+  uint32_t hi = k < NPL - 1 ? st[k + 1] : hiN;
+  u16x2 dm = as_v(__builtin_amdgcn_alignbit(cur, lo, 16));  // (prev[2k-1], prev[2k])
+  u16x2 dp = as_v(__builtin_amdgcn_alignbit(hi, cur, 16));  // (prev[2k+1], prev[2k+2])
+  u16x2 m = vmin(vmin(dm + P1, dp + P1), vmin(as_v(cur), mp2));
+  uint32_t nv = as_u(as_v(c) + m - mpv);
+  old_km1 = cur;
+  st[k] = nv;
+  return nv;
+}
 
-__global__ __launch_bounds__(256) void k_sg_hsum(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
-                                                 int64_t stride, int pitch, SgParams p,
-                                                 uint16_t* __restrict__ hsum) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int W = p.W, D = p.D;
-  // per-pixel planes for the whole row: a0,a1 (left), b0,b1 (right) + BT min/max of each
-  uint8_t* la = smem;               // [2][W]
-  uint8_t* lmn = la + 2 * W;        // [2][W]
-  uint8_t* lmx = lmn + 2 * W;       // [2][W]
-  uint8_t* rb = lmx + 2 * W;        // [2][W]
-  uint8_t* rmn = rb + 2 * W;        // [2][W]
-  uint8_t* rmx = rmn + 2 * W;       // [2][W]
-  uint8_t* pd = rmx + 2 * W;        // [kChunk + 6][D]
+constexpr uint32_t kSent = 0x7FFFu;  // "no neighbour" entry: P1 + 0x7FFF never wins the min
+
+// ------------------------------------------------------------------ quad helpers
+// A quad of lanes owns one row; lane q of the quad holds disparities [q*D/4, (q+1)*D/4).
+// Neighbour entries across the quad come from DPP quad permutes; minima by two xor steps.
+constexpr int kQPrev = 0x90;  // quad_perm [0,0,1,2]: value of lane q-1
+constexpr int kQNext = 0xF9;  // quad_perm [1,2,3,3]: value of lane q+1
+constexpr int kQX1 = 0xB1;    // quad_perm [1,0,3,2]
+constexpr int kQX2 = 0x4E;    // quad_perm [2,3,0,1]
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+
+template <int NV4>
+__device__ __forceinline__ void load_run(const uint16_t* base, uint32_t* out) {
+  const uint4* p4 = reinterpret_cast<const uint4*>(base);
+#pragma unroll
+  for (int i = 0; i < NV4; ++i) {
+    uint4 q = p4[i];
+    out[4 * i] = q.x; out[4 * i + 1] = q.y; out[4 * i + 2] = q.z; out[4 * i + 3] = q.w;
+  }
+}
+
+// One step of a horizontal path over a lane's run; returns the quad-wide minimum.
+template <int PQ>
+__device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
+                                          uint32_t P2) {
+  const uint32_t prevLast = qperm<kQPrev>(st[PQ - 1]);
+  const uint32_t nextFirst = qperm<kQNext>(st[0]);
+  const uint32_t lo0 = q == 0 ? (kSent << 16) : prevLast;
+  const uint32_t hiN = q == 3 ? kSent : nextFirst;
+  const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
+  u16x2 mn = splat(0xFFFF);
+  uint32_t oldk = 0;
+#pragma unroll
+  for (int k = 0; k < PQ; ++k) mn = vmin(mn, as_v(sgm_pair<PQ>(st, k, oldk, c[k], P1, mp2, mpv, lo0, hiN)));
+  uint32_t m = as_u(mn);
+  m = min(m & 0xFFFFu, m >> 16);
+  m = min(m, qperm<kQX1>(m));
+  m = min(m, qperm<kQX2>(m));
+  return m;
+}
+
+
+// ------------------------------------------------------------------ pixel cost + hsum
+// Block = one row segment of 2*kSeg columns x all D disparities; thread (seg, d) slides a
+// 7-wide window along its kSeg columns, so each pixel cost is computed once per window.
+// The BT terms of both channels (x-Sobel, intensity) ride in one u16x2 word:
+// c = min(max(u - v1, v0 - u)^+, max(v - u1, u0 - v)^+) with saturating packed subtracts.
+constexpr int kSeg = 64;
+
+template <int D>
+__global__ __launch_bounds__(2 * D) void k_sg_hsum(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
+                                                   int64_t stride, int pitch, SgParams p,
+                                                   uint16_t* __restrict__ hsum) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sw[];
+  const int W = p.W;
+  // [0] Lu [1] Lmin [2] Lmax [3] Ru [4] Rmin [5] Rmax, each [W] u16x2 (Sobel, intensity)
   const int y = blockIdx.y, b = blockIdx.z;
-  const int x1s = blockIdx.x * kChunk;
-  const int x1e = min(x1s + kChunk, p.width1);
   const uint8_t* L = Limg + b * stride;
   const uint8_t* R = Rimg + b * stride;
-  const uint8_t* r1 = L + (int64_t)y * pitch;
-  const uint8_t* r2 = R + (int64_t)y * pitch;
-  const uint8_t* n1 = L + (int64_t)(y > 0 ? y - 1 : y) * pitch;
-  const uint8_t* s1 = L + (int64_t)(y < p.H - 1 ? y + 1 : y) * pitch;
-  const uint8_t* n2 = R + (int64_t)(y > 0 ? y - 1 : y) * pitch;
-  const uint8_t* s2 = R + (int64_t)(y < p.H - 1 ? y + 1 : y) * pitch;
+  const int ym = y > 0 ? y - 1 : y, yp = y < p.H - 1 ? y + 1 : y;
   const int ft = p.ftzero;
   auto clip = [ft](int v) { return min(max(v, -ft), ft) + ft; };
-  for (int x = threadIdx.x; x < W; x += blockDim.x) {
-    int a0 = clip(0), a1v = clip(0), b0 = clip(0), b1v = clip(0);
-    if (x >= 1 && x < W - 1) {
-      a0 = clip((r1[x + 1] - r1[x - 1]) * 2 + n1[x + 1] - n1[x - 1] + s1[x + 1] - s1[x - 1]);
-      b0 = clip((r2[x + 1] - r2[x - 1]) * 2 + n2[x + 1] - n2[x - 1] + s2[x + 1] - s2[x - 1]);
-      a1v = r1[x];
-      b1v = r2[x];
-    }
-    la[x] = (uint8_t)a0;
-    la[W + x] = (uint8_t)a1v;
-    rb[x] = (uint8_t)b0;
-    rb[W + x] = (uint8_t)b1v;
-  }
-  __syncthreads();
+  auto chan = [&](const uint8_t* img, int x) -> uint32_t {  // (Sobel, intensity) of column x
+    if (x < 1 || x >= W - 1) return (uint32_t)clip(0) * 0x10001u;  // both channels read ftzero
+    const uint8_t* r0 = img + (int64_t)ym * pitch;
+    const uint8_t* r1 = img + (int64_t)y * pitch;
+    const uint8_t* r2 = img + (int64_t)yp * pitch;
+    int s = (r1[x + 1] - r1[x - 1]) * 2 + r0[x + 1] - r0[x - 1] + r2[x + 1] - r2[x - 1];
+    return (uint32_t)clip(s) | ((uint32_t)r1[x] << 16);
+  };
   for (int x = threadIdx.x; x < W; x += blockDim.x) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const uint8_t* A = la + c * W;
-      const uint8_t* Bv = rb + c * W;
-      int u = A[x], ul = x > 0 ? (u + A[x - 1]) / 2 : u, ur = x < W - 1 ? (u + A[x + 1]) / 2 : u;
-      lmn[c * W + x] = (uint8_t)min(min(ul, ur), u);
-      lmx[c * W + x] = (uint8_t)max(max(ul, ur), u);
-      int v = Bv[x], vl = x > 0 ? (v + Bv[x - 1]) / 2 : v, vr = x < W - 1 ? (v + Bv[x + 1]) / 2 : v;
-      rmn[c * W + x] = (uint8_t)min(min(vl, vr), v);
-      rmx[c * W + x] = (uint8_t)max(max(vl, vr), v);
+    for (int side = 0; side < 2; ++side) {
+      const uint8_t* img = side ? R : L;
+      u16x2 u = as_v(chan(img, x));
+      u16x2 ul = x > 0 ? as_v(chan(img, x - 1)) : u, ur = x < W - 1 ? as_v(chan(img, x + 1)) : u;
+      u16x2 hl = (u + ul) >> 1, hr = (u + ur) >> 1;  // (a + b) / 2 of non-negatives
+      if (x == 0) hl = u;
+      if (x == W - 1) hr = u;
+      sw[(3 * side) * W + x] = as_u(u);
+      sw[(3 * side + 1) * W + x] = as_u(vmin(vmin(hl, hr), u));
+      sw[(3 * side + 2) * W + x] = as_u(__builtin_elementwise_max(__builtin_elementwise_max(hl, hr), u));
     }
   }
   __syncthreads();
-  // pixel cost for x1 in [x1s-3, x1e+3) (clamped to [0,width1-1]) into pd
-  const int nloc = (x1e - x1s) + 6;
-  for (int i = threadIdx.x; i < nloc * D; i += blockDim.x) {
-    int xl = i / D, d = i - xl * D;
-    int x1 = min(max(x1s - 3 + xl, 0), p.width1 - 1);
-    int x = x1 + p.minX1;
-    int xr = x - (d + p.minD);
-    int cost = 0;
+  const int d = threadIdx.x % D, seg = threadIdx.x / D;
+  const int x1b = blockIdx.x * (2 * kSeg) + seg * kSeg;
+  if (x1b >= p.width1) return;
+  const uint32_t *Lu = sw, *L0 = sw + W, *L1 = sw + 2 * W, *Ru = sw + 3 * W, *R0 = sw + 4 * W, *R1 = sw + 5 * W;
+  const int dofs = p.minX1 - d - p.minD;  // xr = x1 + dofs >= 0
+  auto pc = [&](int x1) -> int {
+    x1 = min(max(x1, 0), p.width1 - 1);
+    const int x = x1 + p.minX1, xr = x1 + dofs;
+    u16x2 u = as_v(Lu[x]), u0 = as_v(L0[x]), u1 = as_v(L1[x]);
+    u16x2 v = as_v(Ru[xr]), v0 = as_v(R0[xr]), v1 = as_v(R1[xr]);
+    u16x2 c0 = __builtin_elementwise_max(__builtin_elementwise_sub_sat(u, v1), __builtin_elementwise_sub_sat(v0, u));
+    u16x2 c1 = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, u1), __builtin_elementwise_sub_sat(u0, v));
+    uint32_t m = as_u(vmin(c0, c1));
+    return (int)(m & 0xFFFFu) + (int)(m >> 18);
+  };
+  int ring[7];
+  int s = 0;
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      int u = la[c * W + x], u0 = lmn[c * W + x], u1 = lmx[c * W + x];
-      int v = rb[c * W + xr], v0 = rmn[c * W + xr], v1 = rmx[c * W + xr];
-      int c0 = max(0, u - v1);
-      c0 = max(c0, v0 - u);
-      int c1 = max(0, v - u1);
-      c1 = max(c1, u0 - v);
-      cost += min(c0, c1) >> (c == 0 ? 0 : 2);
+  for (int k = 0; k < 7; ++k) { ring[k] = pc(x1b - 3 + k); s += ring[k]; }
+  uint16_t* out = hsum + ((int64_t)b * p.H + y) * p.width1 * D + d;
+#pragma unroll
+  for (int i = 0; i < kSeg; ++i) {
+    if (i > 0) {
+      int nv = pc(x1b + i + 3);
+      s += nv - ring[(i - 1) % 7];
+      ring[(i - 1) % 7] = nv;
     }
-    pd[i] = (uint8_t)cost;
-  }
-  __syncthreads();
-  uint16_t* out = hsum + ((int64_t)b * p.H + y) * p.width1 * D;
-  for (int i = threadIdx.x; i < (x1e - x1s) * D; i += blockDim.x) {
-    int xl = i / D, d = i - xl * D;
-    int s = 0;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) s += pd[(xl + k) * D + d];
-    out[(int64_t)(x1s + xl) * D + d] = (uint16_t)s;
+    if (x1b + i < p.width1) out[(int64_t)(x1b + i) * D] = (uint16_t)s;
   }
 }
 
-// ------------------------------------------------------------------ vertical box sum
-__global__ void k_sg_vsum(const uint16_t* __restrict__ hsum, uint16_t* __restrict__ cost,
-                          uint16_t* __restrict__ cost_extra, SgParams p) {
-  const int64_t plane = (int64_t)p.width1 * p.D;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = blockIdx.y;
-  if (i >= plane) return;
-  const uint16_t* hs = hsum + (int64_t)b * p.H * plane + i;
-  uint16_t* co = cost + (int64_t)b * p.H * plane + i;
-  const int H = p.H;
-  auto hrow = [&](int r) -> int { return hs[(int64_t)min(max(r, 0), H - 1) * plane]; };
-  int acc = 0;
-  for (int r = -3; r <= 3; ++r) acc += hrow(r);
-  co[0] = (uint16_t)acc;
-  for (int y = 1; y < H; ++y) {
-    acc += hrow(y + 3) - hrow(y - 4);
-    co[(int64_t)y * plane] = (uint16_t)acc;
-  }
-  // stripe-start rows: window rows clamp at the stripe's first processed row
-  uint16_t* ce = cost_extra + (int64_t)b * (p.nstripes - 1) * 3 * plane + i;
-  for (int s = 1; s < p.nstripes; ++s) {
-    int start = max(min(s * p.ss - p.ov, H), 0);
-    for (int k = 0; k < 3; ++k) {
-      int y = start + k;
-      int a = 0;
-      for (int r = y - 3; r <= y + 3; ++r) a += hs[(int64_t)min(max(r, start), H - 1) * plane];
-      ce[(int64_t)((s - 1) * 3 + k) * plane] = (uint16_t)a;
-    }
-  }
-}
-
-// ------------------------------------------------------------------ top->down path
+// ------------------------------------------------------------------ vertical sum + top->down
+// Quad per column x1 (lane q holds disparities [q*D/4, (q+1)*D/4)), 16 columns per wave,
+// one block per (16 columns, stripe, pair).  The 7-row vertical box sum is a running sum
+// over the hsum rows, with rows clamped to the stripe's first processed row and to H-1
+// (OpenCV's stripe overlap rule); the top->down path restarts at each stripe's first row.
 template <int D>
-__global__ __launch_bounds__(64) void k_sg_vert(const uint16_t* __restrict__ cost, const uint16_t* __restrict__ cost_extra,
-                                                uint16_t* __restrict__ V, SgParams p) {
-  constexpr int NP = D / 2;
-  const int x1 = blockIdx.x * 64 + threadIdx.x;
+__global__ __launch_bounds__(64) void k_sg_vert(const uint16_t* __restrict__ hsum, uint16_t* __restrict__ Cvol,
+                                                uint16_t* __restrict__ Vvol, SgParams p) {
+  constexpr int DQ = D / 4, PQ = DQ / 2, NV4 = DQ / 8;
+  const int q = threadIdx.x & 3;
+  const int x1 = blockIdx.x * 16 + (threadIdx.x >> 2);
   const int s = blockIdx.y, b = blockIdx.z;
-  if (x1 >= p.width1) return;
+  if (x1 >= p.width1) return;  // whole quads leave together
   const int64_t plane = (int64_t)p.width1 * D;
   const int H = p.H;
   const int start = max(min(s * p.ss - p.ov, H), 0);
   const int end = min((s + 1) * p.ss, H);
   const int first_out = min(s * p.ss, H);
-  uint32_t st[NP];
+  if (start >= end) return;
+  const int64_t colofs = (int64_t)b * H * plane + (int64_t)x1 * D + q * DQ;
+  auto row = [&](int r) { return hsum + colofs + (int64_t)r * plane; };
+  uint32_t crun[PQ], st[PQ], a[PQ], o[PQ], an[PQ], on[PQ];
+  load_run<NV4>(row(start), crun);
 #pragma unroll
-  for (int k = 0; k < NP; ++k) st[k] = 0;
+  for (int k = 0; k < PQ; ++k) {
+    u16x2 v = as_v(crun[k]);
+    crun[k] = as_u(v + v + v + v);  // rows start-3..start clamp to start
+  }
+  for (int r = start + 1; r <= start + 3; ++r) {
+    load_run<NV4>(row(min(r, H - 1)), a);
+#pragma unroll
+    for (int k = 0; k < PQ; ++k) crun[k] = as_u(as_v(crun[k]) + as_v(a[k]));
+  }
+#pragma unroll
+  for (int k = 0; k < PQ; ++k) st[k] = 0;
+  if (start + 1 < end) {
+    load_run<NV4>(row(min(start + 4, H - 1)), an);
+    load_run<NV4>(row(start), on);
+  }
   uint32_t minPrev = 0;
   const u16x2 P1 = splat(p.P1);
-  const uint32_t SENT = 0x7FFFu;
   for (int y = start; y < end; ++y) {
-    const uint16_t* crow;
-    if (s > 0 && y < start + 3)
-      crow = cost_extra + ((int64_t)b * (p.nstripes - 1) * 3 + (s - 1) * 3 + (y - start)) * plane;
-    else
-      crow = cost + ((int64_t)b * H + y) * plane;
-    const uint4* cp = reinterpret_cast<const uint4*>(crow + (int64_t)x1 * D);
-    uint32_t c[NP];
+    if (y > start) {  // window [y-3, y+3] clamped to [start, H-1]
 #pragma unroll
-    for (int k = 0; k < NP / 4; ++k) {
-      uint4 q = cp[k];
-      c[4 * k] = q.x; c[4 * k + 1] = q.y; c[4 * k + 2] = q.z; c[4 * k + 3] = q.w;
+      for (int k = 0; k < PQ; ++k) { a[k] = an[k]; o[k] = on[k]; }
+      if (y + 1 < end) {
+        load_run<NV4>(row(min(y + 4, H - 1)), an);
+        load_run<NV4>(row(max(y - 3, start)), on);
+      }
+#pragma unroll
+      for (int k = 0; k < PQ; ++k) crun[k] = as_u(as_v(crun[k]) - as_v(o[k]) + as_v(a[k]));
     }
-    const u16x2 mp2 = splat(minPrev + p.P2);
-    const u16x2 mpv = splat(minPrev);
-    uint32_t nst[NP];
-    u16x2 mn = splat(0xFFFF);
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      uint32_t lo = k > 0 ? st[k - 1] : (SENT << 16);
-      uint32_t hi = k < NP - 1 ? st[k + 1] : SENT;
-      u16x2 cur = as_v(st[k]);
-      u16x2 dm = as_v(__builtin_amdgcn_alignbit(st[k], lo, 16));  // (prev[2k-1], prev[2k])
-      u16x2 dp = as_v(__builtin_amdgcn_alignbit(hi, st[k], 16));  // (prev[2k+1], prev[2k+2])
-      u16x2 m = vmin(vmin(dm + P1, dp + P1), vmin(cur, mp2));
-      u16x2 nv = as_v(c[k]) + m - mpv;
-      nst[k] = as_u(nv);
-      mn = vmin(mn, nv);
-    }
-#pragma unroll
-    for (int k = 0; k < NP; ++k) st[k] = nst[k];
-    uint32_t mu = as_u(mn);
-    minPrev = min(mu & 0xFFFFu, mu >> 16);
+    minPrev = hstep<PQ>(st, crun, q, P1, minPrev, p.P2);
     if (y >= first_out) {
-      uint4* vp = reinterpret_cast<uint4*>(V + ((int64_t)b * H + y) * plane + (int64_t)x1 * D);
+      uint4* cp = reinterpret_cast<uint4*>(Cvol + colofs + (int64_t)y * plane);
+      uint4* vp = reinterpret_cast<uint4*>(Vvol + colofs + (int64_t)y * plane);
 #pragma unroll
-      for (int k = 0; k < NP / 4; ++k) vp[k] = make_uint4(st[4 * k], st[4 * k + 1], st[4 * k + 2], st[4 * k + 3]);
+      for (int i = 0; i < NV4; ++i) {
+        cp[i] = make_uint4(crun[4 * i], crun[4 * i + 1], crun[4 * i + 2], crun[4 * i + 3]);
+        vp[i] = make_uint4(st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3]);
+      }
     }
   }
 }
 
 // ------------------------------------------------------------------ horizontal paths + WTA
+// raw / d2 / d2c are stored transposed, [x][row], so the rows of a wave are contiguous.
 template <int D>
-__global__ __launch_bounds__(64) void k_sg_horiz(const uint16_t* __restrict__ cost, const uint16_t* __restrict__ V,
-                                                 uint16_t* __restrict__ Lv, int16_t* __restrict__ raw,
-                                                 int16_t* __restrict__ d2, int32_t* __restrict__ d2c, SgParams p) {
-  constexpr int NP = D / 2;
-  __shared__ uint32_t sS[64][NP + 1];
-  const int lane = threadIdx.x;
-  const int y = blockIdx.x * 64 + lane;
+__global__ __launch_bounds__(64) void k_sg_horiz(const uint16_t* __restrict__ Cvol, const uint16_t* __restrict__ Vvol,
+                                                 uint16_t* __restrict__ LVvol, int16_t* __restrict__ rawT,
+                                                 int16_t* __restrict__ d2T, int16_t* __restrict__ d2cT, SgParams p) {
+  constexpr int DQ = D / 4, PQ = DQ / 2, NV4 = DQ / 8;
+  const int q = threadIdx.x & 3;
+  const int y = blockIdx.x * 16 + (threadIdx.x >> 2);
   const int b = blockIdx.y;
   const int H = p.H, W = p.W;
-  if (y >= H) return;
-  const int64_t plane = (int64_t)p.width1 * D;
-  const uint16_t* crow = cost + ((int64_t)b * H + y) * plane;
-  uint16_t* lrow = Lv + ((int64_t)b * H + y) * plane;
-  const uint16_t* vrow = V + ((int64_t)b * H + y) * plane;
+  if (y >= H) return;  // whole quads leave together
+  const int64_t rowofs = ((int64_t)b * H + y) * p.width1 * D + q * DQ;
   const u16x2 P1 = splat(p.P1);
-  const uint32_t SENT = 0x7FFFu;
-  // ---- left -> right
-  uint32_t st[NP];
-#pragma unroll
-  for (int k = 0; k < NP; ++k) st[k] = 0;
-  uint32_t minPrev = 0;
-  for (int x1 = 0; x1 < p.width1; ++x1) {
-    const uint4* cp = reinterpret_cast<const uint4*>(crow + (int64_t)x1 * D);
-    uint32_t c[NP];
-#pragma unroll
-    for (int k = 0; k < NP / 4; ++k) {
-      uint4 q = cp[k];
-      c[4 * k] = q.x; c[4 * k + 1] = q.y; c[4 * k + 2] = q.z; c[4 * k + 3] = q.w;
-    }
-    const u16x2 mp2 = splat(minPrev + p.P2), mpv = splat(minPrev);
-    uint32_t nst[NP];
-    u16x2 mn = splat(0xFFFF);
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      uint32_t lo = k > 0 ? st[k - 1] : (SENT << 16);
-      uint32_t hi = k < NP - 1 ? st[k + 1] : SENT;
-      u16x2 dm = as_v(__builtin_amdgcn_alignbit(st[k], lo, 16));
-      u16x2 dp = as_v(__builtin_amdgcn_alignbit(hi, st[k], 16));
-      u16x2 m = vmin(vmin(dm + P1, dp + P1), vmin(as_v(st[k]), mp2));
-      u16x2 nv = as_v(c[k]) + m - mpv;
-      nst[k] = as_u(nv);
-      mn = vmin(mn, nv);
-    }
-#pragma unroll
-    for (int k = 0; k < NP; ++k) st[k] = nst[k];
-    uint32_t mu = as_u(mn);
-    minPrev = min(mu & 0xFFFFu, mu >> 16);
-    uint4* lp = reinterpret_cast<uint4*>(lrow + (int64_t)x1 * D);
-#pragma unroll
-    for (int k = 0; k < NP / 4; ++k) lp[k] = make_uint4(st[4 * k], st[4 * k + 1], st[4 * k + 2], st[4 * k + 3]);
-  }
-  // ---- right -> left, sum, WTA, sub-pixel, right-view disparity
   const int INVALID = (p.minD - 1) * 16;
-  int16_t* drow = raw + ((int64_t)b * H + y) * W;
-  int16_t* d2row = d2 + ((int64_t)b * H + y) * W;
-  int32_t* d2crow = d2c + ((int64_t)b * H + y) * W;
-  for (int x = 0; x < W; ++x) {
-    drow[x] = (int16_t)INVALID;
-    d2row[x] = (int16_t)INVALID;
-    d2crow[x] = 0x7FFF;
+  const int64_t colT = (int64_t)b * W * H + y;  // + x*H
+  for (int x = q; x < W; x += 4) {
+    rawT[colT + (int64_t)x * H] = (int16_t)INVALID;
+    d2T[colT + (int64_t)x * H] = (int16_t)INVALID;
+    d2cT[colT + (int64_t)x * H] = (int16_t)0x7FFF;
   }
+  // ---- left -> right: LV = L + V
+  uint32_t st[PQ], c[PQ], v[PQ], cn[PQ], vn[PQ];
 #pragma unroll
-  for (int k = 0; k < NP; ++k) st[k] = 0;
+  for (int k = 0; k < PQ; ++k) st[k] = 0;
+  uint32_t minPrev = 0;
+  load_run<NV4>(Cvol + rowofs, cn);
+  load_run<NV4>(Vvol + rowofs, vn);
+  for (int x1 = 0; x1 < p.width1; ++x1) {
+#pragma unroll
+    for (int k = 0; k < PQ; ++k) { c[k] = cn[k]; v[k] = vn[k]; }
+    if (x1 + 1 < p.width1) {
+      load_run<NV4>(Cvol + rowofs + (int64_t)(x1 + 1) * D, cn);
+      load_run<NV4>(Vvol + rowofs + (int64_t)(x1 + 1) * D, vn);
+    }
+    minPrev = hstep<PQ>(st, c, q, P1, minPrev, p.P2);
+    uint4* lp = reinterpret_cast<uint4*>(LVvol + rowofs + (int64_t)x1 * D);
+#pragma unroll
+    for (int i = 0; i < NV4; ++i)
+      lp[i] = make_uint4(as_u(as_v(st[4 * i]) + as_v(v[4 * i])), as_u(as_v(st[4 * i + 1]) + as_v(v[4 * i + 1])),
+                         as_u(as_v(st[4 * i + 2]) + as_v(v[4 * i + 2])), as_u(as_v(st[4 * i + 3]) + as_v(v[4 * i + 3])));
+  }
+  __syncthreads();  // init stores above vs. the quad leader's read-modify-writes below
+  // ---- right -> left, S = LV + R, first-minimum WTA, sub-pixel, right-view disparity
+#pragma unroll
+  for (int k = 0; k < PQ; ++k) st[k] = 0;
   minPrev = 0;
+  load_run<NV4>(Cvol + rowofs + (int64_t)(p.width1 - 1) * D, cn);
+  load_run<NV4>(LVvol + rowofs + (int64_t)(p.width1 - 1) * D, vn);
   for (int x1 = p.width1 - 1; x1 >= 0; --x1) {
-    const uint4* cp = reinterpret_cast<const uint4*>(crow + (int64_t)x1 * D);
-    const uint4* lp = reinterpret_cast<const uint4*>(lrow + (int64_t)x1 * D);
-    const uint4* vp = reinterpret_cast<const uint4*>(vrow + (int64_t)x1 * D);
-    uint32_t c[NP], lv[NP], vv[NP];
 #pragma unroll
-    for (int k = 0; k < NP / 4; ++k) {
-      uint4 q = cp[k], l4 = lp[k], v4 = vp[k];
-      c[4 * k] = q.x; c[4 * k + 1] = q.y; c[4 * k + 2] = q.z; c[4 * k + 3] = q.w;
-      lv[4 * k] = l4.x; lv[4 * k + 1] = l4.y; lv[4 * k + 2] = l4.z; lv[4 * k + 3] = l4.w;
-      vv[4 * k] = v4.x; vv[4 * k + 1] = v4.y; vv[4 * k + 2] = v4.z; vv[4 * k + 3] = v4.w;
+    for (int k = 0; k < PQ; ++k) { c[k] = cn[k]; v[k] = vn[k]; }
+    if (x1 > 0) {
+      load_run<NV4>(Cvol + rowofs + (int64_t)(x1 - 1) * D, cn);
+      load_run<NV4>(LVvol + rowofs + (int64_t)(x1 - 1) * D, vn);
     }
-    const u16x2 mp2 = splat(minPrev + p.P2), mpv = splat(minPrev);
-    uint32_t nst[NP];
-    u16x2 mn = splat(0xFFFF), smn = splat(0xFFFF);
+    minPrev = hstep<PQ>(st, c, q, P1, minPrev, p.P2);
+    // local first-minimum over this lane's run, with its S neighbours
+    int best = 0x7FFFFFFF, bd = 0, sm1 = 0, sp1 = 0, prevv = 0;
+    bool cap = false;
+    uint32_t sFirst = 0, sLast = 0;
 #pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      uint32_t lo = k > 0 ? st[k - 1] : (SENT << 16);
-      uint32_t hi = k < NP - 1 ? st[k + 1] : SENT;
-      u16x2 dm = as_v(__builtin_amdgcn_alignbit(st[k], lo, 16));
-      u16x2 dp = as_v(__builtin_amdgcn_alignbit(hi, st[k], 16));
-      u16x2 m = vmin(vmin(dm + P1, dp + P1), vmin(as_v(st[k]), mp2));
-      u16x2 nv = as_v(c[k]) + m - mpv;
-      nst[k] = as_u(nv);
-      mn = vmin(mn, nv);
-      u16x2 S = as_v(lv[k]) + nv + as_v(vv[k]);
-      sS[lane][k] = as_u(S);
-      smn = vmin(smn, S);
-    }
+    for (int k = 0; k < PQ; ++k) {
+      uint32_t S = as_u(as_v(v[k]) + as_v(st[k]));
+      if (k == 0) sFirst = S & 0xFFFFu;
+      if (k == PQ - 1) sLast = S >> 16;
 #pragma unroll
-    for (int k = 0; k < NP; ++k) st[k] = nst[k];
-    uint32_t mu = as_u(mn);
-    minPrev = min(mu & 0xFFFFu, mu >> 16);
-    uint32_t su = as_u(smn);
-    const int minCost = (int)min(su & 0xFFFFu, su >> 16);
-    int best = D - 1;
-    for (int k = NP - 1; k >= 0; --k) {
-      uint32_t w = sS[lane][k];
-      if ((int)(w >> 16) == minCost) best = 2 * k + 1;
-      if ((int)(w & 0xFFFFu) == minCost) best = 2 * k;
+      for (int h = 0; h < 2; ++h) {
+        int sv = h ? (int)(S >> 16) : (int)(S & 0xFFFFu);
+        if (cap) { sp1 = sv; cap = false; }
+        if (sv < best) { best = sv; bd = 2 * k + h; sm1 = prevv; cap = true; }
+        prevv = sv;
+      }
     }
-    auto Sd = [&](int d) -> int {
-      uint32_t w = sS[lane][d >> 1];
-      return (int)((d & 1) ? (w >> 16) : (w & 0xFFFFu));
-    };
-    const int d = best;
-    const int x2 = x1 + p.minX1 - d - p.minD;
-    if (x2 >= 0 && x2 < W && d2crow[x2] > minCost) {
-      d2crow[x2] = minCost;
-      d2row[x2] = (int16_t)(d + p.minD);
+    const int fromPrev = (int)qperm<kQPrev>(sLast), fromNext = (int)qperm<kQNext>(sFirst);
+    if (bd == 0) sm1 = fromPrev;
+    if (bd == DQ - 1) sp1 = fromNext;
+    bd += q * DQ;
+    // quad reduction: smaller cost wins, ties go to the smaller disparity
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      int ob, od, om, op;
+      if (r == 0) {
+        ob = (int)qperm<kQX1>(best); od = (int)qperm<kQX1>(bd); om = (int)qperm<kQX1>(sm1); op = (int)qperm<kQX1>(sp1);
+      } else {
+        ob = (int)qperm<kQX2>(best); od = (int)qperm<kQX2>(bd); om = (int)qperm<kQX2>(sm1); op = (int)qperm<kQX2>(sp1);
+      }
+      if (ob < best || (ob == best && od < bd)) { best = ob; bd = od; sm1 = om; sp1 = op; }
     }
-    int dd;
-    if (0 < d && d < D - 1) {
-      int sm = Sd(d - 1), sp = Sd(d + 1), s0 = Sd(d);
-      int denom2 = max(sm + sp - 2 * s0, 1);
-      dd = d * 16 + ((sm - sp) * 16 + denom2) / (denom2 * 2);
-    } else {
-      dd = d * 16;
+    if (q == 0) {
+      const int d = bd;
+      const int x2 = x1 + p.minX1 - d - p.minD;
+      if (x2 >= 0 && x2 < W) {
+        int64_t i2 = colT + (int64_t)x2 * H;
+        if ((int)d2cT[i2] > best) {
+          d2cT[i2] = (int16_t)best;
+          d2T[i2] = (int16_t)(d + p.minD);
+        }
+      }
+      int dd;
+      if (0 < d && d < D - 1) {
+        int denom2 = max(sm1 + sp1 - 2 * best, 1);
+        dd = d * 16 + ((sm1 - sp1) * 16 + denom2) / (denom2 * 2);
+      } else {
+        dd = d * 16;
+      }
+      rawT[colT + (int64_t)(x1 + p.minX1) * H] = (int16_t)(dd + p.minD * 16);
     }
-    drow[x1 + p.minX1] = (int16_t)(dd + p.minD * 16);
   }
-  // ---- pseudo left-right consistency check
-  for (int x = p.minX1; x < p.minX1 + p.width1; ++x) {
-    int d1 = drow[x];
+  __syncthreads();
+  // ---- pseudo left-right consistency check, columns split over the quad
+  for (int x = p.minX1 + q; x < p.minX1 + p.width1; x += 4) {
+    int64_t ix = colT + (int64_t)x * H;
+    int d1 = rawT[ix];
     if (d1 == INVALID) continue;
     int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
     int _x = x - _d, x_ = x - d_;
-    if (0 <= x_ && x_ < W && d2row[x_] >= p.minD && abs(d2row[x_] - d_) > p.disp12 && 0 <= _x && _x < W &&
-        d2row[_x] >= p.minD && abs(d2row[_x] - _d) > p.disp12)
-      drow[x] = (int16_t)INVALID;
+    if (0 <= x_ && x_ < W && 0 <= _x && _x < W) {
+      int a = d2T[colT + (int64_t)x_ * H], cc = d2T[colT + (int64_t)_x * H];
+      if (a >= p.minD && abs(a - d_) > p.disp12 && cc >= p.minD && abs(cc - _d) > p.disp12) rawT[ix] = (int16_t)INVALID;
+    }
   }
 }
 
 // ------------------------------------------------------------------ median 3x3
-__global__ void k_sg_median(const int16_t* __restrict__ raw, int16_t* __restrict__ out, int W, int H) {
-  int x = blockIdx.x * blockDim.x + threadIdx.x;
-  int y = blockIdx.y, b = blockIdx.z;
-  if (x >= W) return;
-  const int16_t* s = raw + (int64_t)b * H * W;
+__global__ void k_sg_median(const int16_t* __restrict__ rawT, int16_t* __restrict__ out, int W, int H) {
+  int y = blockIdx.x * blockDim.x + threadIdx.x;  // rows contiguous in the transposed input
+  int x = blockIdx.y, b = blockIdx.z;
+  if (y >= H) return;
+  const int16_t* s = rawT + (int64_t)b * W * H;
   int v[9];
   int k = 0;
 #pragma unroll
@@ -360,7 +373,7 @@ __global__ void k_sg_median(const int16_t* __restrict__ raw, int16_t* __restrict
 #pragma unroll
     for (int dx = -1; dx <= 1; ++dx) {
       int yy = min(max(y + dy, 0), H - 1), xx = min(max(x + dx, 0), W - 1);
-      v[k++] = s[(int64_t)yy * W + xx];
+      v[k++] = s[(int64_t)xx * H + yy];
     }
   // Paeth's 19-compare median-of-9 network
 #define SG_S(a, b) { int t_ = min(v[a], v[b]); v[b] = max(v[a], v[b]); v[a] = t_; }
@@ -391,6 +404,25 @@ SgParams make_params(const fvo_config& c) {
   return p;
 }
 
+template <int D>
+void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_t* R, int batch, int64_t stride,
+                 int pitch, int16_t* disp, hipStream_t s) {
+  uint16_t* hsum = ctx->sg_cost;
+  uint16_t* C = ctx->sg_L;
+  uint16_t* V = ctx->sg_V;
+  uint16_t* LV = ctx->sg_cost;  // hsum is consumed by k_sg_vert before LV is written
+  const size_t shm = (size_t)24 * p.W;  // six u16x2 planes of the row
+  FVO_TIMED(ctx, KN_SG_HSUM, s,
+            hipLaunchKernelGGL(k_sg_hsum<D>, dim3((p.width1 + 2 * kSeg - 1) / (2 * kSeg), p.H, batch), dim3(2 * D),
+                               shm, s, L, R, stride, pitch, p, hsum));
+  FVO_TIMED(ctx, KN_SG_VERT, s, hipLaunchKernelGGL(k_sg_vert<D>, dim3((p.width1 + 15) / 16, p.nstripes, batch),
+                                                   dim3(64), 0, s, hsum, C, V, p));
+  FVO_TIMED(ctx, KN_SG_HORIZ, s, hipLaunchKernelGGL(k_sg_horiz<D>, dim3((p.H + 15) / 16, batch), dim3(64), 0, s, C, V,
+                                                    LV, ctx->sg_raw, ctx->sg_d2, ctx->sg_d2c, p));
+  FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.H + 255) / 256, p.W, batch), dim3(256), 0, s,
+                                                     ctx->sg_raw, disp, p.W, p.H));
+}
+
 }  // namespace
 
 int sgbm_init(fvo_ctx* ctx) {
@@ -403,48 +435,23 @@ int sgbm_init(fvo_ctx* ctx) {
   SgParams p = make_params(c);
   if (p.width1 <= 0) return fvo_fail(ctx, "SGBM: image narrower than numDisparities");
   const int64_t B = c.max_batch, plane = (int64_t)p.width1 * p.D;
-  ctx->sg_extra_rows = (p.nstripes - 1) * 3;
   int rc;
-  if ((rc = fvo_alloc(ctx, &ctx->sg_cost, B * (p.H + ctx->sg_extra_rows) * plane)) ||
-      (rc = fvo_alloc(ctx, &ctx->sg_L, B * p.H * plane)) || (rc = fvo_alloc(ctx, &ctx->sg_V, B * p.H * plane)) ||
-      (rc = fvo_alloc(ctx, &ctx->sg_raw, B * p.H * p.W)) || (rc = fvo_alloc(ctx, &ctx->sg_d2, B * p.H * p.W)) ||
-      (rc = fvo_alloc(ctx, &ctx->sg_d2c, B * p.H * p.W)))
+  // sg_cost: hsum, then reused for L; sg_L: C; sg_V: V  (each B * H * plane u16)
+  if ((rc = fvo_alloc(ctx, &ctx->sg_cost, B * p.H * plane)) || (rc = fvo_alloc(ctx, &ctx->sg_L, B * p.H * plane)) ||
+      (rc = fvo_alloc(ctx, &ctx->sg_V, B * p.H * plane)) || (rc = fvo_alloc(ctx, &ctx->sg_raw, B * p.H * p.W)) ||
+      (rc = fvo_alloc(ctx, &ctx->sg_d2, B * p.H * p.W)) || (rc = fvo_alloc(ctx, &ctx->sg_d2c, B * p.H * p.W)))
     return rc;
   return 0;
 }
 
 int sgbm_run(fvo_ctx* ctx, const uint8_t* L, const uint8_t* R, int batch, int64_t image_stride, int pitch,
              int16_t* disp, hipStream_t s) {
-  const fvo_config& c = ctx->cfg;
-  SgParams p = make_params(c);
-  const int64_t plane = (int64_t)p.width1 * p.D;
-  uint16_t* hsum = ctx->sg_L;  // the L volume doubles as hsum scratch (consumed before L is written)
-  uint16_t* cost = ctx->sg_cost;
-  uint16_t* cost_extra = ctx->sg_cost + (int64_t)batch * p.H * plane;
-  size_t shm = (size_t)12 * p.W + (size_t)(kChunk + 6) * p.D;
-  FVO_TIMED(ctx, KN_SG_HSUM, s, hipLaunchKernelGGL(k_sg_hsum, dim3((p.width1 + kChunk - 1) / kChunk, p.H, batch), dim3(256), shm, s, L, R,
-                     image_stride, pitch, p, hsum));
-  FVO_TIMED(ctx, KN_SG_VSUM, s, hipLaunchKernelGGL(k_sg_vsum, dim3((unsigned)((plane + 255) / 256), batch), dim3(256), 0, s, hsum, cost, cost_extra,
-                     p));
-  dim3 gv((p.width1 + 63) / 64, p.nstripes, batch), gh((p.H + 63) / 64, batch);
+  SgParams p = make_params(ctx->cfg);
   switch (p.D) {
-    case 64:
-      FVO_TIMED(ctx, KN_SG_VERT, s, hipLaunchKernelGGL(k_sg_vert<64>, gv, dim3(64), 0, s, cost, cost_extra, ctx->sg_V, p));
-      FVO_TIMED(ctx, KN_SG_HORIZ, s, hipLaunchKernelGGL(k_sg_horiz<64>, gh, dim3(64), 0, s, cost, ctx->sg_V, ctx->sg_L, ctx->sg_raw, ctx->sg_d2,
-                         ctx->sg_d2c, p));
-      break;
-    case 96:
-      FVO_TIMED(ctx, KN_SG_VERT, s, hipLaunchKernelGGL(k_sg_vert<96>, gv, dim3(64), 0, s, cost, cost_extra, ctx->sg_V, p));
-      FVO_TIMED(ctx, KN_SG_HORIZ, s, hipLaunchKernelGGL(k_sg_horiz<96>, gh, dim3(64), 0, s, cost, ctx->sg_V, ctx->sg_L, ctx->sg_raw, ctx->sg_d2,
-                         ctx->sg_d2c, p));
-      break;
-    default:
-      FVO_TIMED(ctx, KN_SG_VERT, s, hipLaunchKernelGGL(k_sg_vert<128>, gv, dim3(64), 0, s, cost, cost_extra, ctx->sg_V, p));
-      FVO_TIMED(ctx, KN_SG_HORIZ, s, hipLaunchKernelGGL(k_sg_horiz<128>, gh, dim3(64), 0, s, cost, ctx->sg_V, ctx->sg_L, ctx->sg_raw, ctx->sg_d2,
-                         ctx->sg_d2c, p));
-      break;
+    case 64: launch_sgbm<64>(ctx, p, L, R, batch, image_stride, pitch, disp, s); break;
+    case 96: launch_sgbm<96>(ctx, p, L, R, batch, image_stride, pitch, disp, s); break;
+    default: launch_sgbm<128>(ctx, p, L, R, batch, image_stride, pitch, disp, s); break;
   }
-  FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.W + 255) / 256, p.H, batch), dim3(256), 0, s, ctx->sg_raw, disp, p.W, p.H));
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }
