@@ -38,26 +38,65 @@ def algorithmic_bytes_per_frame(W: int, H: int, N: int) -> int:
 
 
 def cpu_baseline(n_frames: int, nfeatures: int, W: int, H: int) -> dict:
-    """Scalar C++ restatement of the reference CPU path (oracle/, 1 thread) timed on a
-    bounded sample: per frame the reference's full per-iteration work — 4 ORB extractions
-    (prev/cur x L/R), 2 BF cross-check matchings, SGBM-3way, back-projection, PnP."""
+    """Scalar C++ restatement of the reference CPU path (oracle/) timed on a bounded sample:
+    per frame the reference's full per-iteration work — 4 ORB extractions (prev/cur x L/R),
+    2 BF cross-check matchings, SGBM-3way, back-projection, PnP.  Timed on 1 host thread
+    and with frames spread over `cores` threads (the C calls release the GIL), as
+    SURVEY.md §8(d) asks; `value` is the multi-core rate."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test/baseline infrastructure only
+    from concurrent.futures import ThreadPoolExecutor
     from forest_slam_amd import synth
-    seq = synth.StereoSequence(seed=0, n_frames=n_frames + 1, W=W, H=H, device="cpu")
-    imgs = [tuple(x.numpy() for x in seq.frame(i)) for i in range(n_frames + 1)]
-    t0 = time.perf_counter()
-    for i in range(n_frames):
+    cores = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
+    n_mt = max(n_frames, cores * 2)
+    rdev = "cuda" if torch.cuda.is_available() else "cpu"  # rendering only; the timed work is host C++
+    seq = synth.StereoSequence(seed=0, n_frames=n_mt + 1, W=W, H=H, device=rdev)
+    imgs = [tuple(x.cpu().numpy() for x in seq.frame(i)) for i in range(n_mt + 1)]
+
+    def one(i):
         (pL, pR), (cL, cR) = imgs[i], imgs[i + 1]
         oracle.frame_pose(pL, pR, cL, seq.K, synth.DIST_L, synth.BASELINE, nfeatures)
         _, dR0 = oracle.orb_detect_compute(pR, nfeatures)
         _, dR1 = oracle.orb_detect_compute(cR, nfeatures)
         oracle.bf_match(dR0, dR1)
-    dt = time.perf_counter() - t0
-    return {"value": n_frames / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n_frames} consecutive {W}x{H} synthetic stereo frames, nfeatures={nfeatures}: "
-                      "4 ORB + 2 BF-xcheck + SGBM-3way + back-projection + PnP-RANSAC per frame, "
-                      f"oracle/ scalar C++ on 1 host thread, {dt:.1f} s"}
+
+    t0 = time.perf_counter()
+    for i in range(n_frames):
+        one(i)
+    dt1 = time.perf_counter() - t0
+    with ThreadPoolExecutor(max_workers=cores) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(one, range(n_mt)))
+        dtm = time.perf_counter() - t0
+    return {"value": n_mt / dtm, "unit": "frames/s", "cores": cores, "kind": "port",
+            "value_1core": n_frames / dt1,
+            "sample": f"{W}x{H} synthetic stereo frames, nfeatures={nfeatures}: 4 ORB + 2 BF-xcheck + "
+                      f"SGBM-3way + back-projection + PnP-RANSAC per frame, oracle/ scalar C++; {n_mt} frames "
+                      f"over {cores} threads in {dtm:.1f} s; {n_frames} frames on 1 thread in {dt1:.1f} s"}
+
+
+# stage name (fvo_kernel_name) -> kernel symbol prefix in rocprofv3 summaries
+KERNEL_SYMBOL = {"sgbm_horiz": "k_sg_horiz", "sgbm_vert": "k_sg_vert", "sgbm_hsum": "k_sg_hsum",
+                 "sgbm_median": "k_sg_median", "orb_fast_score": "k_fast_score", "orb_blur": "k_blur",
+                 "pnp_ransac": "k_pnp_hyp", "bf_argmin": "k_bf_argmin"}
+
+
+def pmc_traffic(stage: str):
+    """HBM bytes per launch of the stage's kernel from the newest committed PMC summary
+    (profiles/<round>/pmc_per_kernel.csv, written by profiles/collect.sh from separate
+    FETCH_SIZE / WRITE_SIZE passes of this same bench command; gfx950 corrections applied
+    there).  None when no summary covers the kernel."""
+    import csv
+    import glob
+    sym = KERNEL_SYMBOL.get(stage)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_per_kernel.csv")))
+    if not sym or not files:
+        return None, None
+    with open(files[-1]) as f:
+        for row in csv.DictReader(f):
+            if row["kernel"].startswith(sym):
+                return float(row["hbm_bytes_per_dispatch_corrected"]), os.path.relpath(files[-1], ROOT)
+    return None, None
 
 
 def main():
@@ -143,6 +182,8 @@ def main():
     frames_per_launch = B  # every kernel of the step processes the whole batch in one launch
     bpf = algorithmic_bytes_per_frame(W, H, args.nfeatures)
     achieved = bpf * frames_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(dom)
+    traffic_rate = traffic / avg_launch_s / 1e9 if (traffic and avg_launch_s > 0) else None
 
     ate = None
     if rank == 0 and args.ate_frames > 1:
@@ -183,7 +224,10 @@ def main():
                        "frames_per_step_per_gpu": B, "width": W, "height": H, "nfeatures": args.nfeatures,
                        "local_ba": "not in this round's step (DESIGN.md)", "parallelism": f"seq-per-gpu x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic_rate_gbs": round(traffic_rate, 1) if traffic_rate else None,
+                         "traffic_frac": round(traffic_rate / HBM_PEAK_GBS, 4) if traffic_rate else None,
                          "algorithmic_bytes_per_frame": bpf, "frames_per_launch": frames_per_launch,
                          "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
             "cpu_baseline": cpu,

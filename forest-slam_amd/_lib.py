@@ -24,8 +24,11 @@ class FvoConfig(ctypes.Structure):
         ("scale_factor", ctypes.c_float)] + [(n, ctypes.c_int32) for n in (
             "nlevels", "edge_threshold", "first_level", "wta_k", "score_type", "patch_size", "fast_threshold",
             "min_disparity", "num_disparities", "block_size", "P1", "P2", "disp12_max_diff", "pre_filter_cap",
-            "uniqueness_ratio", "sgbm_stripes", "kp_capacity")]
+            "uniqueness_ratio", "sgbm_stripes", "kp_capacity", "stages")]
 
+
+ABI_VERSION = 2  # FVO_ABI_VERSION of include/fvo.h
+STAGE_ORB, STAGE_BF, STAGE_SGBM, STAGE_POSE = 1, 2, 4, 8
 
 # name -> (restype, argtypes); mirrors include/fvo.h
 _P = ctypes.c_void_p
@@ -71,7 +74,7 @@ def load(path: str = LIB_PATH):
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.fvo_abi_version() != 1:
+        if L.fvo_abi_version() != ABI_VERSION:
             raise RuntimeError("libfvo.so ABI version mismatch")
         _lib = L
     return _lib

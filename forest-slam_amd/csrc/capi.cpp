@@ -49,6 +49,7 @@ void fvo_config_default(fvo_config* c, int32_t width, int32_t height) {
   c->uniqueness_ratio = 0;
   c->sgbm_stripes = 4;
   c->kp_capacity = 0;
+  c->stages = FVO_STAGE_ALL;
 }
 
 static void release(fvo_ctx* c) {
@@ -74,9 +75,23 @@ int fvo_create(int device, const fvo_config* cfg, fvo_ctx** out) {
     return rc;
   };
   if (hipSetDevice(device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(-1); }
-  if (cfg->width < 64 || cfg->height < 64 || cfg->max_batch < 1) { c->err = "bad image size or max_batch"; return bail(-1); }
-  int rc;
-  if ((rc = orb_init(c)) || (rc = bf_init(c)) || (rc = sgbm_init(c)) || (rc = pose_init(c))) return bail(rc);
+  if (c->cfg.stages == 0) c->cfg.stages = FVO_STAGE_ALL;
+  const int st = c->cfg.stages;
+  if (st & ~FVO_STAGE_ALL) { c->err = "unknown bits in stages"; return bail(-1); }
+  if (cfg->max_batch < 1) { c->err = "max_batch must be >= 1"; return bail(-1); }
+  if ((st & (FVO_STAGE_ORB | FVO_STAGE_SGBM)) && (cfg->width < 64 || cfg->height < 64)) {
+    c->err = "image size must be at least 64x64";
+    return bail(-1);
+  }
+  if (!(st & FVO_STAGE_ORB) && (st & (FVO_STAGE_BF | FVO_STAGE_POSE)) && cfg->kp_capacity < 1) {
+    c->err = "kp_capacity must be set when the ORB stage is not enabled";
+    return bail(-1);
+  }
+  c->kp_cap = cfg->kp_capacity > 0 ? cfg->kp_capacity : 2 * cfg->nfeatures + 64;
+  int rc = 0;
+  if (((st & FVO_STAGE_ORB) && (rc = orb_init(c))) || ((st & FVO_STAGE_BF) && (rc = bf_init(c))) ||
+      ((st & FVO_STAGE_SGBM) && (rc = sgbm_init(c))) || ((st & FVO_STAGE_POSE) && (rc = pose_init(c))))
+    return bail(rc);
   *out = c;
   return 0;
 }
@@ -94,15 +109,16 @@ const char* fvo_last_error(const fvo_ctx* c) { return c ? c->err.c_str() : "null
 int fvo_kp_capacity(const fvo_ctx* c) { return c ? c->kp_cap : 0; }
 int64_t fvo_workspace_bytes(const fvo_ctx* c) { return c ? c->ws_bytes : 0; }
 
-static int check_batch(fvo_ctx* c, int32_t batch) {
+static int check_batch(fvo_ctx* c, int32_t batch, int stage) {
   if (!c) return -1;
+  if (!(c->cfg.stages & stage)) return fvo_fail(c, "stage not enabled in this context (fvo_config.stages)");
   if (batch < 0 || batch > c->cfg.max_batch) return fvo_fail(c, "batch exceeds max_batch");
   return 0;
 }
 
 int fvo_orb_detect_compute(fvo_ctx* c, const uint8_t* images, int32_t batch, int64_t image_stride, int32_t pitch,
                            float* keypoints, uint8_t* descriptors, int32_t* counts, int32_t cap, fvo_stream stream) {
-  if (check_batch(c, batch)) return -1;
+  if (check_batch(c, batch, FVO_STAGE_ORB)) return -1;
   if (batch == 0) return 0;
   if (!images || !keypoints || !descriptors || !counts) return fvo_fail(c, "null pointer argument");
   if (pitch < c->cfg.width || image_stride < (int64_t)pitch * c->cfg.height) return fvo_fail(c, "bad pitch/stride");
@@ -113,7 +129,7 @@ int fvo_orb_detect_compute(fvo_ctx* c, const uint8_t* images, int32_t batch, int
 int fvo_bf_match(fvo_ctx* c, const uint8_t* query, const int32_t* n_query, const uint8_t* train,
                  const int32_t* n_train, int32_t batch, int32_t cap, int32_t* matches, int32_t* n_matches,
                  fvo_stream stream) {
-  if (check_batch(c, batch)) return -1;
+  if (check_batch(c, batch, FVO_STAGE_BF)) return -1;
   if (batch == 0) return 0;
   if (!query || !n_query || !train || !n_train || !matches || !n_matches) return fvo_fail(c, "null pointer argument");
   if (cap < 1 || cap > c->kp_cap) return fvo_fail(c, "cap must be in [1, fvo_kp_capacity()]");
@@ -122,7 +138,7 @@ int fvo_bf_match(fvo_ctx* c, const uint8_t* query, const int32_t* n_query, const
 
 int fvo_sgbm(fvo_ctx* c, const uint8_t* left, const uint8_t* right, int32_t batch, int64_t image_stride,
              int32_t pitch, int16_t* disparity, fvo_stream stream) {
-  if (check_batch(c, batch)) return -1;
+  if (check_batch(c, batch, FVO_STAGE_SGBM)) return -1;
   if (batch == 0) return 0;
   if (!left || !right || !disparity) return fvo_fail(c, "null pointer argument");
   if (pitch < c->cfg.width || image_stride < (int64_t)pitch * c->cfg.height) return fvo_fail(c, "bad pitch/stride");
@@ -132,7 +148,7 @@ int fvo_sgbm(fvo_ctx* c, const uint8_t* left, const uint8_t* right, int32_t batc
 int fvo_backproject(fvo_ctx* c, const int16_t* disparity, const float* kp0, const float* kp1, const int32_t* matches,
                     const int32_t* n_matches, int32_t batch, int32_t cap, const double* K, double baseline,
                     float* points3d, float* points2d, int32_t* n_points, fvo_stream stream) {
-  if (check_batch(c, batch)) return -1;
+  if (check_batch(c, batch, FVO_STAGE_POSE)) return -1;
   if (batch == 0) return 0;
   if (!disparity || !kp0 || !kp1 || !matches || !n_matches || !K || !points3d || !points2d || !n_points)
     return fvo_fail(c, "null pointer argument");
@@ -145,7 +161,7 @@ int fvo_pnp_ransac(fvo_ctx* c, const float* points3d, const float* points2d, con
                    int32_t cap, const double* K, const double* dist, float reprojection_error, double confidence,
                    int32_t iterations, double* rvec, double* tvec, double* T, int32_t* status, uint8_t* inliers,
                    fvo_stream stream) {
-  if (check_batch(c, batch)) return -1;
+  if (check_batch(c, batch, FVO_STAGE_POSE)) return -1;
   if (batch == 0) return 0;
   if (!points3d || !points2d || !n_points || !K || !dist || !rvec || !tvec || !T || !status)
     return fvo_fail(c, "null pointer argument");

@@ -706,7 +706,6 @@ int orb_init(fvo_ctx* ctx) {
     }
     g.nfeat[c.nlevels - 1] = std::max(c.nfeatures - sum, 0);
   }
-  ctx->kp_cap = c.kp_capacity > 0 ? c.kp_capacity : 2 * c.nfeatures + 64;
 
   // resize tables (levels 1..L-1), INTER_LINEAR_EXACT coefficient rule
   std::vector<int32_t> xo, xc, yo, yc;

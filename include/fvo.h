@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define FVO_ABI_VERSION 1
+#define FVO_ABI_VERSION 2
 
 typedef struct fvo_ctx fvo_ctx;
 typedef void* fvo_stream; /* hipStream_t */
@@ -72,7 +72,16 @@ typedef struct fvo_config {
   int32_t uniqueness_ratio; /* 0 (only 0 supported) */
   int32_t sgbm_stripes;     /* 4: OpenCV's fixed stripe count for MODE_SGBM_3WAY */
   int32_t kp_capacity;      /* per-image keypoint capacity of the ORB outputs (0 = auto) */
+  int32_t stages;           /* FVO_STAGE_* mask of the workspaces to allocate (0 = all) */
 } fvo_config;
+
+/* fvo_config.stages: a context only serves the stages it was created for (e.g. a
+ * BFMatcher-only context needs no image-sized workspace). */
+#define FVO_STAGE_ORB 1
+#define FVO_STAGE_BF 2
+#define FVO_STAGE_SGBM 4
+#define FVO_STAGE_POSE 8
+#define FVO_STAGE_ALL 15
 
 /* Fill `cfg` with the reference's parameters for a width x height image. */
 void fvo_config_default(fvo_config* cfg, int32_t width, int32_t height);

@@ -222,6 +222,21 @@ def rodrigues(rvec: np.ndarray) -> np.ndarray:
     return R.reshape(3, 3)
 
 
+def rodrigues_jac(rvec: np.ndarray):
+    """(R 3x3, J 3x9) as cv2.Rodrigues(rvec) returns them."""
+    rvec = np.ascontiguousarray(rvec, dtype=np.float64).reshape(3)
+    R, J = np.zeros(9), np.zeros(27)
+    lib().ref_rodrigues_jac(_p(rvec, _f64p), _p(R, _f64p), _p(J, _f64p))
+    return R.reshape(3, 3), J.reshape(3, 9)
+
+
+def rodrigues_inv(R: np.ndarray) -> np.ndarray:
+    R = np.ascontiguousarray(R, dtype=np.float64).reshape(9)
+    r = np.zeros(3)
+    lib().ref_rodrigues_inv(_p(R, _f64p), _p(r, _f64p))
+    return r
+
+
 def project_points(P3, rvec, tvec, K, dist):
     P3 = np.ascontiguousarray(P3, dtype=np.float64)
     rvec = np.ascontiguousarray(rvec, dtype=np.float64).reshape(3)

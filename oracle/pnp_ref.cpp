@@ -813,6 +813,8 @@ int ref_solve_pnp_ransac(const double* P3d, const float* p2, int n, const double
 }
 
 void ref_rodrigues(const double* rvec, double* R) { pnp::rodrigues_r2R(rvec, R, nullptr); }
+void ref_rodrigues_jac(const double* rvec, double* R, double* J) { pnp::rodrigues_r2R(rvec, R, J); }
+void ref_rodrigues_inv(const double* R, double* rvec) { pnp::rodrigues_R2r(R, rvec); }
 
 void ref_project_points(const double* P3, int n, const double* rvec, const double* tvec, const double* Kmat,
                         const double* dist, double* uv) {

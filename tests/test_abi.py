@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(path)
     missing = [n for n in _declared() if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.fvo_abi_version() == 1
+    assert lib.fvo_abi_version() == 2
 
 
 def test_binding_signatures_cover_header():
@@ -46,6 +46,7 @@ def test_config_default_matches_reference_constants():
     assert abs(cfg.scale_factor - 1.2) < 1e-6
     assert (cfg.num_disparities, cfg.min_disparity, cfg.block_size, cfg.P1, cfg.P2) == (96, 0, 7, 392, 1568)
     assert cfg.sgbm_stripes == 4
+    assert cfg.stages == 15  # FVO_STAGE_ALL
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-GPU failure path")
