@@ -24,11 +24,12 @@ class FvoConfig(ctypes.Structure):
         ("scale_factor", ctypes.c_float)] + [(n, ctypes.c_int32) for n in (
             "nlevels", "edge_threshold", "first_level", "wta_k", "score_type", "patch_size", "fast_threshold",
             "min_disparity", "num_disparities", "block_size", "P1", "P2", "disp12_max_diff", "pre_filter_cap",
-            "uniqueness_ratio", "sgbm_stripes", "kp_capacity", "stages")]
+            "uniqueness_ratio", "sgbm_stripes", "kp_capacity", "stages", "ba_window", "ba_max_landmarks",
+            "ba_max_obs")]
 
 
 ABI_VERSION = 2  # FVO_ABI_VERSION of include/fvo.h
-STAGE_ORB, STAGE_BF, STAGE_SGBM, STAGE_POSE = 1, 2, 4, 8
+STAGE_ORB, STAGE_BF, STAGE_SGBM, STAGE_POSE, STAGE_BA = 1, 2, 4, 8, 16
 
 # name -> (restype, argtypes); mirrors include/fvo.h
 _P = ctypes.c_void_p
@@ -48,6 +49,9 @@ SIGNATURES = {
     "fvo_backproject": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, _P, ctypes.c_double, _P, _P, _P, _P]),
     "fvo_pnp_ransac": (ctypes.c_int, [_P, _P, _P, _P, _I, _I, _P, _P, ctypes.c_float, ctypes.c_double, _I, _P, _P,
                                       _P, _P, _P, _P]),
+    "fvo_keypoint_stereo": (ctypes.c_int, [_P, _P, _P, _P, _I, _I, _P, ctypes.c_double, _P, _P]),
+    "fvo_ba_windows": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, ctypes.c_double, _P, _I, _I,
+                                      _P, _P, _P]),
     "fvo_test_retain_best": (ctypes.c_int, [_P, _P, _I, _I, _P, _P, _P]),
     "fvo_debug_buffer": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     "fvo_kernel_count": (ctypes.c_int, []),
@@ -241,6 +245,37 @@ class Context:
                                           float(confidence), int(iterations), _ptr(rvec), _ptr(tvec), _ptr(T),
                                           _ptr(st), _ptr(inl), _stream(self.device)))
         return rvec, tvec, T, st, inl
+
+    def keypoint_stereo(self, disp, kp, nkp, K, baseline, out=None):
+        """Stereo point (X, Y, Z, d) of every keypoint (fvo_keypoint_stereo); Z = 0 invalid."""
+        B, cap = kp.shape[0], kp.shape[1]
+        if out is None:
+            out = torch.empty((B, cap, 4), dtype=torch.float32, device=self.device)
+        Kh = (ctypes.c_double * 9)(*[float(v) for v in K.reshape(-1)])
+        self._check(self.L.fvo_keypoint_stereo(self.h, _ptr(disp), _ptr(kp), _ptr(nkp), B, cap, Kh, float(baseline),
+                                               _ptr(out), _stream(self.device)))
+        return out
+
+    def ba_windows(self, kp, nkp, matches, nmatch, stereo, T_rel, first_end, n_windows, first_valid, K, baseline,
+                   iterations=10, scale_factor=1.2, out=None):
+        """Windowed local BA over frame arrays [F,...] (fvo_ba_windows).  Observation
+        weights 1 / scale_factor^(2 octave) (scale_factor as a Python float, the value
+        ORB_create() receives).  Returns (T_out f64[n_windows,4,4] refined last-pair
+        transforms, stats f64[n_windows,6])."""
+        F, cap = kp.shape[0], kp.shape[1]
+        if out is None:
+            Tout = torch.empty((n_windows, 4, 4), dtype=torch.float64, device=self.device)
+            stats = torch.empty((n_windows, 6), dtype=torch.float64, device=self.device)
+        else:
+            Tout, stats = out
+        Kh = (ctypes.c_double * 9)(*[float(v) for v in K.reshape(-1)])
+        nl = int(self.cfg.nlevels)
+        isig = (ctypes.c_double * nl)(*[1.0 / (float(scale_factor) ** (2 * o)) for o in range(nl)])
+        self._check(self.L.fvo_ba_windows(self.h, _ptr(kp), _ptr(nkp), _ptr(matches), _ptr(nmatch), _ptr(stereo),
+                                          _ptr(T_rel), F, cap, int(first_end), int(n_windows), int(first_valid), Kh,
+                                          float(baseline), isig, nl, int(iterations), _ptr(Tout), _ptr(stats),
+                                          _stream(self.device)))
+        return Tout, stats
 
     def debug_buffer(self, which: int) -> torch.Tensor:
         """Host copy (u8 CPU tensor) of an internal workspace buffer (fvo_debug_buffer)."""

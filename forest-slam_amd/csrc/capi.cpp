@@ -50,6 +50,9 @@ void fvo_config_default(fvo_config* c, int32_t width, int32_t height) {
   c->sgbm_stripes = 4;
   c->kp_capacity = 0;
   c->stages = FVO_STAGE_ALL;
+  c->ba_window = 10;
+  c->ba_max_landmarks = 4096;
+  c->ba_max_obs = 32768;
 }
 
 static void release(fvo_ctx* c) {
@@ -57,7 +60,7 @@ static void release(fvo_ctx* c) {
                   c->ncand,      c->nsel1,     c->nsel2,     c->koff,     c->scratch, c->rt.xofs,  c->rt.xc1,
                   c->rt.yofs,    c->rt.yc1,    c->umax,      c->bf_sidx,  c->bf_sdist, c->bf_tidx, c->sg_cost,
                   c->sg_L,       c->sg_V,      c->sg_raw,    c->sg_d2,    c->sg_d2c,  c->pnp_hyp,  c->pnp_good,
-                  c->pnp_sub,    c->pnp_subsets, c->pnp_models, c->pnp_state};
+                  c->pnp_sub,    c->pnp_subsets, c->pnp_models, c->pnp_state, c->ba_ws};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
 }
@@ -83,14 +86,15 @@ int fvo_create(int device, const fvo_config* cfg, fvo_ctx** out) {
     c->err = "image size must be at least 64x64";
     return bail(-1);
   }
-  if (!(st & FVO_STAGE_ORB) && (st & (FVO_STAGE_BF | FVO_STAGE_POSE)) && cfg->kp_capacity < 1) {
+  if (!(st & FVO_STAGE_ORB) && (st & (FVO_STAGE_BF | FVO_STAGE_POSE | FVO_STAGE_BA)) && cfg->kp_capacity < 1) {
     c->err = "kp_capacity must be set when the ORB stage is not enabled";
     return bail(-1);
   }
   c->kp_cap = cfg->kp_capacity > 0 ? cfg->kp_capacity : 2 * cfg->nfeatures + 64;
   int rc = 0;
   if (((st & FVO_STAGE_ORB) && (rc = orb_init(c))) || ((st & FVO_STAGE_BF) && (rc = bf_init(c))) ||
-      ((st & FVO_STAGE_SGBM) && (rc = sgbm_init(c))) || ((st & FVO_STAGE_POSE) && (rc = pose_init(c))))
+      ((st & FVO_STAGE_SGBM) && (rc = sgbm_init(c))) || ((st & FVO_STAGE_POSE) && (rc = pose_init(c))) ||
+      ((st & FVO_STAGE_BA) && (rc = ba_init(c))))
     return bail(rc);
   *out = c;
   return 0;
@@ -172,6 +176,32 @@ int fvo_pnp_ransac(fvo_ctx* c, const float* points3d, const float* points2d, con
                  rvec, tvec, T, status, inliers, (hipStream_t)stream);
 }
 
+int fvo_keypoint_stereo(fvo_ctx* c, const int16_t* disparity, const float* keypoints, const int32_t* n_keypoints,
+                        int32_t batch, int32_t cap, const double* K, double baseline, float* stereo,
+                        fvo_stream stream) {
+  if (check_batch(c, batch, FVO_STAGE_BA)) return -1;
+  if (batch == 0) return 0;
+  if (!disparity || !keypoints || !n_keypoints || !K || !stereo) return fvo_fail(c, "null pointer argument");
+  if (cap < 1 || cap > c->kp_cap) return fvo_fail(c, "cap must be in [1, fvo_kp_capacity()]");
+  if (reinterpret_cast<uintptr_t>(stereo) & 15) return fvo_fail(c, "stereo buffer must be 16-byte aligned");
+  return ba_stereo_run(c, disparity, keypoints, n_keypoints, batch, cap, K, baseline, stereo, (hipStream_t)stream);
+}
+
+int fvo_ba_windows(fvo_ctx* c, const float* keypoints, const int32_t* n_keypoints, const int32_t* matches,
+                   const int32_t* n_matches, const float* stereo, const double* T_rel, int32_t n_frames,
+                   int32_t cap, int32_t first_end, int32_t n_windows, int32_t first_valid, const double* K,
+                   double baseline, const double* inv_sigma2, int32_t n_levels, int32_t iterations,
+                   double* T_out, double* stats, fvo_stream stream) {
+  if (check_batch(c, n_windows, FVO_STAGE_BA)) return -1;
+  if (n_windows == 0) return 0;
+  if (!keypoints || !n_keypoints || !matches || !n_matches || !stereo || !T_rel || !K || !inv_sigma2 || !T_out ||
+      !stats)
+    return fvo_fail(c, "null pointer argument");
+  if (reinterpret_cast<uintptr_t>(stereo) & 15) return fvo_fail(c, "stereo buffer must be 16-byte aligned");
+  return ba_run(c, keypoints, n_keypoints, matches, n_matches, stereo, T_rel, n_frames, cap, first_end, n_windows,
+                first_valid, K, baseline, inv_sigma2, n_levels, iterations, T_out, stats, (hipStream_t)stream);
+}
+
 int fvo_kernel_count(void) { return KN_COUNT; }
 
 const char* fvo_kernel_name(int id) {
@@ -179,7 +209,7 @@ const char* fvo_kernel_name(int id) {
       "orb_copy_level0", "orb_resize", "orb_fast_score", "orb_nms_count", "orb_row_scan", "orb_nms_compact",
       "orb_select_fast", "orb_harris", "orb_select_harris", "orb_offsets", "orb_angle", "orb_blur", "orb_brief",
       "bf_argmin", "bf_finish", "sgbm_hsum", "sgbm_vert", "sgbm_horiz", "sgbm_median", "backproject",
-      "pnp_ransac"};
+      "pnp_ransac", "ba_stereo", "ba_build", "ba_solve"};
   return (id >= 0 && id < KN_COUNT) ? names[id] : "";
 }
 

@@ -39,7 +39,8 @@ struct ResizeTab {
 enum FvoKernel {
   KN_ORB_COPY, KN_ORB_RESIZE, KN_ORB_FAST, KN_ORB_NMS_COUNT, KN_ORB_ROW_SCAN, KN_ORB_COMPACT, KN_ORB_SELECT1,
   KN_ORB_HARRIS, KN_ORB_SELECT2, KN_ORB_OFFSETS, KN_ORB_ANGLE, KN_ORB_BLUR, KN_ORB_BRIEF, KN_BF_ARGMIN,
-  KN_BF_FINISH, KN_SG_HSUM, KN_SG_VERT, KN_SG_HORIZ, KN_SG_MEDIAN, KN_BACKPROJECT, KN_PNP, KN_COUNT
+  KN_BF_FINISH, KN_SG_HSUM, KN_SG_VERT, KN_SG_HORIZ, KN_SG_MEDIAN, KN_BACKPROJECT, KN_PNP, KN_BA_STEREO,
+  KN_BA_BUILD, KN_BA_SOLVE, KN_COUNT
 };
 
 struct TimingRec {
@@ -92,6 +93,9 @@ struct fvo_ctx {
   int32_t* pnp_good = nullptr;    // [B][max_iters] inlier counts
   void* pnp_state = nullptr;      // [B] PnpState
   int32_t pnp_max_iters = 0;
+  // local BA workspace (per window w < max_batch; strides in ba_* counts)
+  void* ba_ws = nullptr;          // one allocation, carved per window (ba.hip)
+  int64_t ba_win_bytes = 0;
 };
 
 // Error helpers: set ctx->err and return negative status.
@@ -138,6 +142,14 @@ int backproject_run(fvo_ctx* ctx, const int16_t* disp, const float* kp0, const f
 int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts, int batch, int cap, const double* K,
             const double* dist, float reproj, double conf, int iters, double* rvec, double* tvec, double* T,
             int32_t* status, uint8_t* inliers, hipStream_t s);
+
+int ba_init(fvo_ctx* ctx);
+int ba_stereo_run(fvo_ctx* ctx, const int16_t* disp, const float* kp, const int32_t* nkp, int batch, int cap,
+                  const double* K, double baseline, float* stereo, hipStream_t s);
+int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* matches, const int32_t* nmatch,
+           const float* stereo, const double* Trel, int nframes, int cap, int first_end, int nwin, int first_valid,
+           const double* K, double baseline, const double* inv_sigma2, int nlev, int iters, double* Tout,
+           double* stats, hipStream_t s);
 
 template <typename T>
 int fvo_alloc(fvo_ctx* ctx, T** p, size_t n) {

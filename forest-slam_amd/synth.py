@@ -38,15 +38,22 @@ def gt_path(n: int | None = None, stride: int = 1) -> tuple[np.ndarray, np.ndarr
     """Returns (timestamps f64[n], camera-to-world f64[n,4,4]) along the 1018_00 path."""
     gt = load_tum(_GT)
     t, p = gt[:, 0], gt[:, 1:4].copy()
-    # heading from smoothed velocity in the horizontal (x, z) plane; y is down.
-    k = 5
+    # heading from the displacement over +-1.5 s in the horizontal (x, z) plane; y is down.
+    # While the vehicle (nearly) stands still the GT jitter would make that direction
+    # spin, so the heading is held: frames whose 3 s displacement is under 0.3 m keep the
+    # previous heading (the first moving heading for a stationary start).
+    k = 15
     pad = np.pad(p, ((k, k), (0, 0)), mode="edge")
     fwd = pad[2 * k:] - pad[:-2 * k]
     fwd[:, 1] = 0.0
     nrm = np.linalg.norm(fwd, axis=1, keepdims=True)
-    fwd = np.where(nrm > 1e-6, fwd / np.maximum(nrm, 1e-12), np.array([0.0, 0.0, 1.0]))
-    for i in range(1, len(fwd)):  # hold heading while stationary
-        if nrm[i, 0] <= 1e-6:
+    moving = nrm[:, 0] > 0.3
+    fwd = np.where(moving[:, None], fwd / np.maximum(nrm, 1e-12), np.array([0.0, 0.0, 1.0]))
+    if moving.any():
+        first = int(np.argmax(moving))
+        fwd[:first] = fwd[first]
+    for i in range(1, len(fwd)):
+        if not moving[i]:
             fwd[i] = fwd[i - 1]
     down = np.array([0.0, 1.0, 0.0])
     T = np.zeros((len(p), 4, 4))
@@ -201,8 +208,9 @@ class StereoSequence:
     """Rectified synthetic stereo sequence along the 1018_00 path."""
 
     def __init__(self, seed: int = 0, n_frames: int = 963, W: int = 960, H: int = 600, device="cpu",
-                 stride: int = 1, n_trees: int = 400):
-        self.t, self.T_wc = gt_path(n_frames, stride)
+                 stride: int = 1, n_trees: int = 400, start: int = 0):
+        t, T_wc = gt_path(start + n_frames, stride)
+        self.t, self.T_wc = t[start:], T_wc[start:]
         self.n = len(self.t)
         self.W, self.H = W, H
         self.K = scaled_K(W, H)

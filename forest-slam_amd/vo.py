@@ -1,4 +1,4 @@
-"""Batched stereo-VO front end on the GPU — the ORB branch of ros_ws/src/stereo_slam.py.
+"""Batched stereo-VO front end + local BA on the GPU — the ORB branch of ros_ws/src/stereo_slam.py.
 
 One ``StereoFrontEnd.step`` processes B consecutive stereo frames of one sequence in a
 fixed sequence of HIP launches (no host synchronisation inside):
@@ -9,11 +9,14 @@ fixed sequence of HIP launches (no host synchronisation inside):
   SGBM of the B *previous* stereo pairs                         (:262 -> :108-117)
   back-projection of the matched previous-left keypoints        (:265-289)
   PnP-RANSAC + Rodrigues -> relative T                          (:292-303)
+  local BA over the last K frames of every new frame            (north_star; oracle/ba_ref.py)
 
 Frames of a sequence are independent except through the chained pose (:306), which the
 host composes left to right in float64 (``eval.chain``), so batching B frames per step is
 exact.  The previous image / keypoints of the last frame are carried to
-the next step.
+the next step, and the BA keeps the per-frame keypoints, matches, stereo points and PnP
+transforms of the last K-1 frames as history so that every window spans K frames
+regardless of where the step boundaries fall.
 """
 from __future__ import annotations
 
@@ -25,13 +28,21 @@ from . import _lib
 
 class StereoFrontEnd:
     def __init__(self, width: int, height: int, K: np.ndarray, dist: np.ndarray, baseline: float, batch: int,
-                 nfeatures: int = 500, match_right: bool = True, device=None, **params):
+                 nfeatures: int = 500, match_right: bool = True, device=None, ba_window: int = 10,
+                 ba_iters: int = 10, **params):
         self.B = batch
         self.K = np.asarray(K, np.float64)
         self.dist = np.resize(np.asarray(dist, np.float64), 5)
         self.baseline = float(baseline)
         self.match_right = match_right
-        self.ctx = _lib.Context(width, height, max_batch=2 * batch, device=device, nfeatures=nfeatures, **params)
+        self.ba_window = int(ba_window)
+        self.ba_iters = int(ba_iters)
+        stages = _lib.STAGE_ORB | _lib.STAGE_BF | _lib.STAGE_SGBM | _lib.STAGE_POSE
+        if self.ba_window:
+            stages |= _lib.STAGE_BA
+            params.setdefault("ba_window", self.ba_window)
+        self.ctx = _lib.Context(width, height, max_batch=2 * batch, device=device, nfeatures=nfeatures,
+                                stages=stages, **params)
         self.dev = self.ctx.device
         self.cap = self.ctx.kp_cap
         self.W, self.H = width, height
@@ -58,20 +69,45 @@ class StereoFrontEnd:
         self.status = e((B,), torch.int32)
         self.inl = e((B, cap), torch.uint8)
         self.imgs = e((2 * B, height, width), torch.uint8)
+        self.lastL = e((height, width), torch.uint8)
+        self.lastR = e((height, width), torch.uint8)
+        self.last_kp = e((cap, _lib.KP_STRIDE), torch.float32)
+        self.last_desc = e((2, cap, _lib.DESC_BYTES), torch.uint8)
+        self.last_cnt = e((2,), torch.int32)
+        if self.ba_window:
+            Kw = self.ba_window
+            F = Kw - 1 + B  # history slots [0, K-1) + the step's frames
+            self.hkp = e((F, cap, _lib.KP_STRIDE), torch.float32)
+            self.hnkp = torch.zeros((F,), dtype=torch.int32, device=dev)
+            self.hmatch = e((F, cap, 3), torch.int32)
+            self.hnmatch = torch.zeros((F,), dtype=torch.int32, device=dev)
+            self.hstereo = e((F, cap, 4), torch.float32)
+            self.hT = torch.zeros((F, 4, 4), dtype=torch.float64, device=dev)
+            self.T_ba = e((B, 4, 4), torch.float64)
+            self.ba_stats = e((B, 6), torch.float64)
+            self.valid_from = Kw - 2
         self.has_prev = False
-        self.last = None  # (L, R, kpL, descL, cntL, descR, cntR) of the last processed image pair
 
     def prime(self, L0: torch.Tensor, R0: torch.Tensor):
         """Feed the first stereo pair of a sequence (no pose is produced for it)."""
         imgs = torch.stack([L0, R0]).to(self.dev)
         kp, desc, cnt = self.ctx.orb(imgs)
-        self.last = (imgs[0].clone(), imgs[1].clone(), kp[0].clone(), desc[0].clone(), cnt[0:1].clone(),
-                     desc[1].clone(), cnt[1:2].clone())
+        self.lastL.copy_(imgs[0])
+        self.lastR.copy_(imgs[1])
+        self.last_kp.copy_(kp[0])
+        self.last_desc.copy_(desc[:2])
+        self.last_cnt.copy_(cnt[:2])
+        if self.ba_window:
+            Kw = self.ba_window
+            self.hkp[Kw - 2].copy_(kp[0])
+            self.hnkp[Kw - 2:Kw - 1].copy_(cnt[0:1])
+            self.valid_from = Kw - 2
         self.has_prev = True
 
     def step(self, L: torch.Tensor, R: torch.Tensor):
         """L, R: u8 [n,H,W] device tensors, n <= B consecutive frames after the primed/last
-        pair.  Returns (T_rel f64[n,4,4], status i32[n]) device tensors (async)."""
+        pair.  Returns (T f64[n,4,4], status i32[n]) device tensors (async): the BA-refined
+        relative transforms when local BA is enabled, else the PnP ones (``self.T``)."""
         if not self.has_prev:
             raise RuntimeError("call prime() with the first stereo pair first")
         n = L.shape[0]
@@ -82,15 +118,14 @@ class StereoFrontEnd:
         self.imgs[:n].copy_(L)
         self.imgs[n:2 * n].copy_(R)
         kp, desc, cnt = ctx.orb(self.imgs[:2 * n], out=(self.kp[:2 * n], self.desc[:2 * n], self.cnt[:2 * n]))
-        lastL, lastR, lkp, ldesc, lcnt, rdesc, rcnt = self.last
         # query (previous) descriptor sets: left frames then right frames
-        self.q_desc[0].copy_(ldesc)
-        self.q_cnt[0:1].copy_(lcnt)
+        self.q_desc[0].copy_(self.last_desc[0])
+        self.q_cnt[0:1].copy_(self.last_cnt[0:1])
         if n > 1:
             self.q_desc[1:n].copy_(desc[:n - 1])
             self.q_cnt[1:n].copy_(cnt[:n - 1])
-        self.q_desc[n].copy_(rdesc)
-        self.q_cnt[n:n + 1].copy_(rcnt)
+        self.q_desc[n].copy_(self.last_desc[1])
+        self.q_cnt[n:n + 1].copy_(self.last_cnt[1:2])
         if n > 1:
             self.q_desc[n + 1:2 * n].copy_(desc[n:2 * n - 1])
             self.q_cnt[n + 1:2 * n].copy_(cnt[n:2 * n - 1])
@@ -98,9 +133,9 @@ class StereoFrontEnd:
         m, nm = ctx.bf_match(self.q_desc[:nb], self.q_cnt[:nb], desc[:nb], cnt[:nb],
                              out=(self.matches[:nb], self.nmatch[:nb]))
         # previous stereo pairs for SGBM and previous-left keypoints for back-projection
-        self.prevL[0].copy_(lastL)
-        self.prevR[0].copy_(lastR)
-        self.q_kp[0].copy_(lkp)
+        self.prevL[0].copy_(self.lastL)
+        self.prevR[0].copy_(self.lastR)
+        self.q_kp[0].copy_(self.last_kp)
         if n > 1:
             self.prevL[1:n].copy_(L[:n - 1])
             self.prevR[1:n].copy_(R[:n - 1])
@@ -111,13 +146,46 @@ class StereoFrontEnd:
         rv, tv, T, st, _ = ctx.pnp_ransac(P3, p2, npts, self.K, self.dist,
                                           out=(self.rvec[:n], self.tvec[:n], self.T[:n], self.status[:n],
                                                self.inl[:n]))
-        self.last = (L[n - 1].clone(), R[n - 1].clone(), kp[n - 1].clone(), desc[n - 1].clone(),
-                     cnt[n - 1:n].clone(), desc[2 * n - 1].clone(), cnt[2 * n - 1:2 * n].clone())
-        return T, st
+        out = T
+        if self.ba_window:
+            out = self._local_ba(n, kp, cnt, m, nm, disp, T)
+        self.lastL.copy_(L[n - 1])
+        self.lastR.copy_(R[n - 1])
+        self.last_kp.copy_(kp[n - 1])
+        self.last_desc[0].copy_(desc[n - 1])
+        self.last_desc[1].copy_(desc[2 * n - 1])
+        self.last_cnt[0:1].copy_(cnt[n - 1:n])
+        self.last_cnt[1:2].copy_(cnt[2 * n - 1:2 * n])
+        return out, st
+
+    def _local_ba(self, n, kp, cnt, m, nm, disp, T):
+        Kw, ctx = self.ba_window, self.ctx
+        a, b = Kw - 2, Kw - 1  # first pair slot, first new-frame slot
+        self.hkp[b:b + n].copy_(kp[:n])
+        self.hnkp[b:b + n].copy_(cnt[:n])
+        self.hmatch[a:a + n].copy_(m[:n])
+        self.hnmatch[a:a + n].copy_(nm[:n])
+        self.hT[a:a + n].copy_(T[:n])
+        ctx.keypoint_stereo(disp[:n], self.q_kp[:n], self.hnkp[a:a + n], self.K, self.baseline,
+                            out=self.hstereo[a:a + n])
+        F = b + n
+        Tba, _ = ctx.ba_windows(self.hkp[:F], self.hnkp[:F], self.hmatch[:F], self.hnmatch[:F], self.hstereo[:F],
+                                self.hT[:F], b, n, self.valid_from, self.K, self.baseline, iterations=self.ba_iters,
+                                out=(self.T_ba[:n], self.ba_stats[:n]))
+        # slide the history: frames [n, n+K-1) -> [0, K-1), pair data [n, n+K-2) -> [0, K-2)
+        self.hkp[:b].copy_(self.hkp[n:n + b].clone())
+        self.hnkp[:b].copy_(self.hnkp[n:n + b].clone())
+        if a > 0:
+            for t in (self.hmatch, self.hnmatch, self.hstereo, self.hT):
+                t[:a].copy_(t[n:n + a].clone())
+        self.valid_from = max(0, self.valid_from - n)
+        return Tba
 
 
-def run_sequence(frontend: StereoFrontEnd, L_all: torch.Tensor, R_all: torch.Tensor, stamps=None):
-    """Process a whole sequence (images on device) -> (TUM rows, relative poses, statuses)."""
+def run_sequence(frontend: StereoFrontEnd, L_all: torch.Tensor, R_all: torch.Tensor, stamps=None,
+                 use_ba: bool = True):
+    """Process a whole sequence (images on device) -> (TUM rows, relative poses, statuses).
+    With local BA enabled the chain uses the BA-refined relative transforms (``use_ba``)."""
     from . import eval as ev
     n = L_all.shape[0]
     frontend.prime(L_all[0], R_all[0])
@@ -125,6 +193,8 @@ def run_sequence(frontend: StereoFrontEnd, L_all: torch.Tensor, R_all: torch.Ten
     for s in range(1, n, frontend.B):
         e = min(s + frontend.B, n)
         T, st = frontend.step(L_all[s:e], R_all[s:e])
+        if not use_ba:
+            T = frontend.T[:e - s]
         Ts.append(T.cpu().numpy())
         sts.append(st.cpu().numpy())
     T = np.concatenate(Ts) if Ts else np.zeros((0, 4, 4))

@@ -73,6 +73,10 @@ typedef struct fvo_config {
   int32_t sgbm_stripes;     /* 4: OpenCV's fixed stripe count for MODE_SGBM_3WAY */
   int32_t kp_capacity;      /* per-image keypoint capacity of the ORB outputs (0 = auto) */
   int32_t stages;           /* FVO_STAGE_* mask of the workspaces to allocate (0 = all) */
+  /* local bundle adjustment (no reference counterpart: BASELINE.json north_star) */
+  int32_t ba_window;        /* frames per BA window K (10); max 21 */
+  int32_t ba_max_landmarks; /* per-window landmark cap (4096) */
+  int32_t ba_max_obs;       /* per-window observation cap (32768) */
 } fvo_config;
 
 /* fvo_config.stages: a context only serves the stages it was created for (e.g. a
@@ -81,7 +85,8 @@ typedef struct fvo_config {
 #define FVO_STAGE_BF 2
 #define FVO_STAGE_SGBM 4
 #define FVO_STAGE_POSE 8
-#define FVO_STAGE_ALL 15
+#define FVO_STAGE_BA 16
+#define FVO_STAGE_ALL 31
 
 /* Fill `cfg` with the reference's parameters for a width x height image. */
 void fvo_config_default(fvo_config* cfg, int32_t width, int32_t height);
@@ -139,6 +144,32 @@ int fvo_pnp_ransac(fvo_ctx* ctx, const float* points3d, const float* points2d, c
                    int32_t batch, int32_t cap, const double* K, const double* dist, float reprojection_error,
                    double confidence, int32_t iterations, double* rvec, double* tvec, double* T, int32_t* status,
                    uint8_t* inliers, fvo_stream stream);
+
+/* Stereo point of every keypoint of `batch` left images: the back-projection of
+ * fvo_backproject (same float32 arithmetic, stereo_slam.py:265-289) applied to all
+ * keypoints instead of the matched ones.  stereo: [batch][cap][4] f32 (X, Y, Z, d) in
+ * camera coordinates with d the disparity used; Z = 0 when 0.1 < Z < 1000 fails.
+ * Feeds fvo_ba_windows (stage FVO_STAGE_BA). */
+int fvo_keypoint_stereo(fvo_ctx* ctx, const int16_t* disparity, const float* keypoints, const int32_t* n_keypoints,
+                        int32_t batch, int32_t cap, const double* K, double baseline, float* stereo,
+                        fvo_stream stream);
+
+/* Windowed local bundle adjustment (specification: oracle/ba_ref.py).
+ * Frame arrays cover `n_frames` consecutive frames f of one sequence:
+ *   keypoints [F][cap][8], n_keypoints [F]      left-image ORB records
+ *   matches [F][cap][3], n_matches [F]          BF matches frame f -> f+1 (f < F-1)
+ *   stereo [F][cap][4]                          fvo_keypoint_stereo of frame f (f < F-1)
+ *   T_rel [F][16]                               camera f -> camera f+1 (PnP), f < F-1
+ * Window w (0 <= w < n_windows) ends at frame e = first_end + w and spans frames
+ * max(first_valid, e - ba_window + 1) .. e; windows of fewer than 3 frames copy T_rel.
+ * inv_sigma2: host double[nlevels] = 1 / scale_factor^(2*octave) observation weights.
+ * Outputs: T_out [n_windows][16] refined camera (e-1) -> camera e transform;
+ *          stats [n_windows][6] f64: cost0, cost, landmarks, observations, frames, accepted. */
+int fvo_ba_windows(fvo_ctx* ctx, const float* keypoints, const int32_t* n_keypoints, const int32_t* matches,
+                   const int32_t* n_matches, const float* stereo, const double* T_rel, int32_t n_frames,
+                   int32_t cap, int32_t first_end, int32_t n_windows, int32_t first_valid, const double* K,
+                   double baseline, const double* inv_sigma2, int32_t n_levels, int32_t iterations,
+                   double* T_out, double* stats, fvo_stream stream);
 
 /* Test hook: KeyPointsFilter::retainBest on `n` float responses (device memory) with the
  * product's selection kernel.  idx_out [n] receives the surviving original indices in

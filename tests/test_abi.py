@@ -46,7 +46,8 @@ def test_config_default_matches_reference_constants():
     assert abs(cfg.scale_factor - 1.2) < 1e-6
     assert (cfg.num_disparities, cfg.min_disparity, cfg.block_size, cfg.P1, cfg.P2) == (96, 0, 7, 392, 1568)
     assert cfg.sgbm_stripes == 4
-    assert cfg.stages == 15  # FVO_STAGE_ALL
+    assert cfg.stages == 31  # FVO_STAGE_ALL
+    assert (cfg.ba_window, cfg.ba_max_landmarks, cfg.ba_max_obs) == (10, 4096, 32768)
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-GPU failure path")

@@ -1,0 +1,161 @@
+"""Local BA: the oracle (oracle/ba_ref.py) recovers known geometry, and
+the HIP solver (fvo_ba_windows) reproduces the oracle on the same inputs.
+
+Tolerance: the solver is fp64 throughout (the reduced-camera GEMM on f64 MFMA), so GPU and
+oracle LM iterates differ only by summation order: measured <= 2.3e-10 on the refined
+poses and <= 1.3e-10 (relative) on the final cost; checked at 1e-8 (poses: entries of the
+4x4 relative transform, far inside north_star's 1e-4) and 1e-8 relative (cost).  The
+initial cost at 1e-9, landmark / observation counts exactly."""
+import numpy as np
+import pytest
+import torch
+
+import ba_synth
+from conftest import gpu_available
+
+
+def _ba_ref():
+    import ba_ref
+    return ba_ref
+
+
+def test_oracle_recovers_clean_geometry():
+    ba_ref = _ba_ref()
+    p = ba_synth.clean_problem(n=8, seed=0)
+    kps, matches, st, rel = ba_synth.oracle_lists(p, 0, 7)
+    out = ba_ref.ba_window(kps, matches, st, rel, p["K"], p["B"], iters=10)
+    assert out["cost"] < 0.1 * out["cost0"]
+    err0 = np.abs(rel[:, :3, 3] - p["relg"][:, :3, 3]).max()
+    err1 = np.abs(out["rel"][:, :3, 3] - p["relg"][:, :3, 3]).max()
+    assert err0 > 0.02 and err1 < 0.01
+
+
+def test_oracle_landmark_rules():
+    """Births only for untracked keypoints with valid depth; tracks follow match chains."""
+    ba_ref = _ba_ref()
+    p = ba_synth.clean_problem(n=5, n_pts=400, seed=1)
+    kps, matches, st, rel = ba_synth.oracle_lists(p, 0, 4)
+    T, X, obs = ba_ref.build_problem(kps, matches, st, rel)
+    # every landmark starts with one stereo observation, then consecutive frames
+    starts = np.nonzero(~np.isnan(obs["ur"]))[0]
+    assert len(starts) == len(X)
+    for a, b in zip(starts, list(starts[1:]) + [len(obs["lm"])]):
+        fr = obs["frame"][a:b]
+        assert b - a >= 2 and np.all(np.diff(fr) == 1) and np.all(obs["lm"][a:b] == obs["lm"][a])
+    # a keypoint tracked from the previous frame never starts a landmark
+    for a in starts:
+        f = obs["frame"][a]
+        if f > 0:
+            q = np.nonzero((kps[f][:, 0] == np.float32(obs["u"][a])) & (kps[f][:, 1] == np.float32(obs["v"][a])))[0]
+            assert not np.isin(q, matches[f - 1][:, 1]).any()
+    # caps: creation stops at the first landmark that does not fit
+    T2, X2, obs2 = ba_ref.build_problem(kps, matches, st, rel, lmax=50)
+    assert len(X2) == 50 and np.array_equal(obs2["u"], obs["u"][:len(obs2["u"])])
+    T3, X3, obs3 = ba_ref.build_problem(kps, matches, st, rel, omax=333)
+    assert len(obs3["lm"]) <= 333 and np.array_equal(obs3["u"], obs["u"][:len(obs3["u"])])
+
+
+def _gpu_ba(p, first_end, n_windows, first_valid=0, window=10, iters=10, **cfg):
+    from forest_slam_amd import _lib
+    F, cap = p["kp"].shape[0], p["kp"].shape[1]
+    ctx = _lib.Context(64, 64, max_batch=max(n_windows, 1), stages=_lib.STAGE_BA, kp_capacity=cap, ba_window=window,
+                       **cfg)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    Tout, stats = ctx.ba_windows(t(p["kp"]), t(p["nkp"]), t(p["matches"]), t(p["nmatch"]), t(p["stereo"]),
+                                 t(p["T_rel"]), first_end, n_windows, first_valid, p["K"], p["B"], iterations=iters)
+    torch.cuda.synchronize()
+    return Tout.cpu().numpy(), stats.cpu().numpy()
+
+
+def _check(p, Tg, sg, s, e, iters=10, lmax=4096, omax=32768):
+    ba_ref = _ba_ref()
+    kps, matches, st, rel = ba_synth.oracle_lists(p, s, e)
+    ref = ba_ref.ba_window(kps, matches, st, rel, p["K"], p["B"], iters=iters, lmax=lmax, omax=omax)
+    assert sg[2] == len(ref["X"]) and sg[3] == len(ref["obs"]["lm"]) and sg[4] == e - s + 1
+    assert abs(sg[0] - ref["cost0"]) <= 1e-9 * ref["cost0"]
+    assert abs(sg[1] - ref["cost"]) <= 1e-8 * ref["cost0"]
+    assert np.abs(Tg - ref["rel"][-1]).max() < 1e-8
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_gpu_ba_matches_oracle_clean():
+    p = ba_synth.clean_problem(n=10, seed=0)
+    Tout, stats = _gpu_ba(p, first_end=9, n_windows=1)
+    _check(p, Tout[0], stats[0], 0, 9)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_gpu_ba_sliding_windows_and_outliers():
+    """12 frames, windows ending at frames 2..11 (the first ones shorter than K), outlier
+    matches handled by the Huber weights."""
+    p = ba_synth.clean_problem(n=12, seed=3, drop=0.05)
+    Tout, stats = _gpu_ba(p, first_end=2, n_windows=10, first_valid=0)
+    for w in range(10):
+        e = 2 + w
+        _check(p, Tout[w], stats[w], max(0, e - 9), e)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_gpu_ba_caps_and_short_windows():
+    p = ba_synth.clean_problem(n=6, seed=4)
+    Tout, stats = _gpu_ba(p, first_end=5, n_windows=1, ba_max_landmarks=100, ba_max_obs=900)
+    _check(p, Tout[0], stats[0], 0, 5, lmax=100, omax=900)
+    # a window of 2 frames passes the PnP transform through
+    Tout, stats = _gpu_ba(p, first_end=1, n_windows=1)
+    assert np.array_equal(Tout[0], p["T_rel"][0]) and stats[0][2] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_gpu_frontend_local_ba_matches_oracle(oracle_mod):
+    """StereoFrontEnd with local BA (K = 4, batch 2, so windows span step boundaries) on a
+    rendered forest sequence vs the oracle pipeline: ORB / BF / SGBM / PnP restated on
+    the CPU, stereo points by ba_ref.stereo_points, then ba_ref.ba_window per frame."""
+    ba_ref = _ba_ref()
+    from forest_slam_amd import synth, vo
+    W, H, n, Kw = 640, 400, 6, 4
+    seq = synth.StereoSequence(seed=9, n_frames=n, W=W, H=H, device="cpu", start=150)
+    fr = [tuple(x.numpy() for x in seq.frame(i)) for i in range(n)]
+    fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=2, nfeatures=500, ba_window=Kw)
+    Ls = torch.from_numpy(np.stack([f[0] for f in fr])).cuda()
+    Rs = torch.from_numpy(np.stack([f[1] for f in fr])).cuda()
+    fe.prime(Ls[0], Rs[0])
+    got, pnp = [], []
+    for s in range(1, n, 2):
+        T, _ = fe.step(Ls[s:s + 2], Rs[s:s + 2])
+        got.append(T.cpu().numpy())
+        pnp.append(fe.T[:2].cpu().numpy())
+    got, pnp = np.concatenate(got), np.concatenate(pnp)
+    # oracle pipeline
+    kps, descs = [], []
+    for L, _ in fr:
+        kp, d = oracle_mod.orb_detect_compute(L, 500)
+        kps.append(kp)
+        descs.append(d)
+    matches = [oracle_mod.bf_match(descs[j], descs[j + 1]) for j in range(n - 1)]
+    stereo = []
+    for j in range(n - 1):
+        stereo.append(ba_ref.stereo_points(kps[j], oracle_mod.sgbm(fr[j][0], fr[j][1]), seq.K, synth.BASELINE))
+    # the BA is initialised with the product's PnP transforms (PnP parity is covered by
+    # test_gpu_parity; a RANSAC model can flip between implementations when an EPnP
+    # subset is ill-conditioned), so this checks the BA in isolation
+    rel = pnp
+    for e in range(1, n):
+        s = max(0, e - Kw + 1)
+        if e - s + 1 < 3:
+            assert np.array_equal(got[e - 1], pnp[e - 1])
+            continue
+        ref = ba_ref.ba_window(kps[s:e + 1], matches[s:e], stereo[s:e], rel[s:e], seq.K, synth.BASELINE, iters=10)
+        assert np.abs(got[e - 1] - ref["rel"][-1]).max() < 1e-8, e
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_gpu_ba_window_20():
+    """Config 5's K = 20 (reduced system 114 x 114, 128-row MFMA tiles)."""
+    p = ba_synth.clean_problem(n=20, seed=5, n_pts=2500)
+    Tout, stats = _gpu_ba(p, first_end=19, n_windows=1, window=20)
+    _check(p, Tout[0], stats[0], 0, 19)

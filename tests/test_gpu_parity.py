@@ -205,9 +205,9 @@ def test_frontend_matches_oracle_pipeline(oracle_mod, frames):
     Ls = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
     Rs = torch.from_numpy(np.stack([f[1] for f in frames])).cuda()
     fe.prime(Ls[0], Rs[0])
-    T, st = fe.step(Ls[1:3], Rs[1:3])
+    _, st = fe.step(Ls[1:3], Rs[1:3])
     torch.cuda.synchronize()
-    T, st = T.cpu().numpy(), st.cpu().numpy()
+    T, st = fe.T[:2].cpu().numpy(), st.cpu().numpy()  # the PnP transforms (before local BA)
     for i in range(2):
         ref = oracle_mod.frame_pose(frames[i][0], frames[i][1], frames[i + 1][0], synth.K0, synth.DIST_L,
                                     synth.BASELINE, 500)
