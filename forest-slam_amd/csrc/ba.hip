@@ -2,25 +2,31 @@
 // "extract+match+local-BA").  The reference chains PnP poses only (stereo_slam.py:306);
 // this stage refines each frame's relative pose over the window of the last K frames.
 // The specification — landmark construction, residuals, robust weights, LM schedule —
-// is oracle/ba_ref.py; this file implements it (fp64 except the reduced-camera GEMM).
+// is oracle/ba_ref.py; this file implements it in fp64.
 //
-// k_ba_stereo  per keypoint (thread), the reference's float32 back-projection through the
-//              disparity map (the fvo_backproject arithmetic) -> (X, Y, Z, d)
-// k_ba_build   one block per window: match-chain landmarks (ordered births via block
-//              scans), landmark-major observations, per-frame observation lists
-// k_ba_solve   one block (4 waves) per window, the whole LM loop in one launch:
-//   P1 per-frame pose blocks H_pp, g_p (a wave per frame, lanes over the frame's obs,
-//      deterministic wave reductions) and per-observation W = J_p^T w J_l
-//   P2 per-landmark H_ll, g_l, damped 3x3 Cholesky L_l; Y = W L_l^-T and z = L_l^-1 g_l
-//      written as the columns 3l..3l+2 of Yt [3L][NR] (row NR-1 carries z)
-//   P3 MFMA: G = Yt^T Yt (v_mfma_f64_16x16x4_f64, upper tiles, 2 accumulators), which is
-//      sum_l W H_ll^-1 W^T (the Schur complement term) and its last column W H_ll^-1 g.
-//      fp64, not the fp32 SURVEY.md a15 suggests: S = H_pp - G cancels, and with fp32
-//      operands the refined poses moved by 1.3e-4 against the fp64 oracle (measured),
-//      outside north_star's 1e-4; the f64 MFMA keeps them at ~1e-12.
-//   P4 reduced camera system S = H_pp + lam diag - G, Cholesky in LDS (fp64), solve
-//   P5 landmark back-substitution, pose update R <- Exp(w) R, t <- Exp(w) t + v
-//   P6 cost at the tentative point (deterministic block reduction), P7 accept / reject
+// Problem construction, one block per window:
+//   k_ba_stereo  per keypoint, the reference's float32 back-projection through the
+//                disparity map (the fvo_backproject arithmetic) -> (X, Y, Z, d)
+//   k_ba_build   match-chain landmarks (ordered births via block scans), landmark-major
+//                observations, per-frame observation lists, initial poses / LM state
+// One LM iteration = five launches whose grids span every window x chunk, so the whole
+// GPU works on the batch of windows (one block per window would leave most CUs idle and
+// every phase latency-bound):
+//   k_ba_pp      (window, frame): H_pp, g_p of the frame's observations (deterministic
+//                block reduction) and W = J_p^T w J_l per observation
+//   k_ba_lin     (window, landmark chunk): H_ll, g_l, damped 3x3 Cholesky L_l; the chunk's
+//                Y = W L_l^-T rows and z = L_l^-1 g_l are laid out in LDS as Yt [3 LPC][NR]
+//                and contracted on MFMA (v_mfma_f64_16x16x4_f64, upper 16x16 tiles):
+//                G_chunk = Yt^T Yt = sum_l W H_ll^-1 W^T (the Schur complement term) with
+//                its last column W H_ll^-1 g — the dense J^T J block contraction
+//   k_ba_solve   (window): S = H_pp + lam diag + 1e-6 I - sum_chunks G, Cholesky (fp64, LDS),
+//                pose step, tentative poses
+//   k_ba_upd     (window, 256 landmarks): back-substitution X' = X + H_ll^-1 (-g - W^T dp),
+//                cost partials at the tentative point
+//   k_ba_accept  (window): LM accept / reject, lambda update
+// fp64 everywhere (the GEMM too): S = H_pp - G cancels, and with fp32 operands the refined
+// poses moved by 1.3e-4 against the fp64 oracle (measured), outside north_star's 1e-4.
+// All reductions have a fixed order, so results are run-to-run deterministic.
 #include <cfloat>
 
 #include "fvo_internal.h"
@@ -29,8 +35,8 @@ namespace {
 
 struct BaObs {
   int lm;
-  short frame, oct;   // window-relative frame, ORB octave (weight 1 / scale^(2 oct))
-  float u, v, ur;     // ur NaN: mono observation
+  short frame, oct;  // window-relative frame; ORB octave (weight 1 / scale^(2 oct)), -1 = rejected
+  float u, v, ur;    // ur NaN: mono observation
 };
 
 struct BaCam {
@@ -41,38 +47,45 @@ constexpr int kKMax = 21;
 constexpr int kBlock = 256;
 constexpr double kD2Mono = 5.991, kD2Stereo = 7.815, kMinZ = 0.01, kLam0 = 1e-3;
 
+struct BaState {
+  double T[kKMax][12], Tt[kKMax][12];  // poses [R row-major | t], current / tentative
+  double dp[6 * kKMax];
+  double Hpp[kKMax][27];  // per frame: 21 upper entries of H_pp, then g_p
+  double lam, cost, cost0;
+  int parity, fail, acc, active, L, O, n, s;
+};
+
 struct BaDims {
-  int Lmax, Omax, K, cap, NR, KP;
-  int64_t oX, oXt, oL, oG, oLs, oObs, oFl, oW, oYt, oNext, oSg, oHdr, oCm, win;
+  int Lmax, Omax, K, cap, NR, LPC, NCH, NCU;
+  int64_t oSt, oX0, oX1, oL, oG, oLs, oObs, oFl, oW, oGp, oCp, oNext, oHdr, win;
 };
 
 struct BaWin {
-  double *X, *Xt, *Lf, *gl, *W;
+  BaState* st;
+  double *X0, *X1, *Lf, *gl, *W, *Gp, *cp;
   int *lstart, *flist, *next, *hdr;
-  uint32_t* cmask;  // per 4-row chunk of Yt: frames its landmarks touch (bit 31: z row)
   BaObs* obs;
-  double *Yt, *Sg;
 };
 
 __device__ __forceinline__ BaWin view(void* base, const BaDims& d, int w) {
   char* p = (char*)base + d.win * w;
   BaWin v;
-  v.X = (double*)(p + d.oX);
-  v.Xt = (double*)(p + d.oXt);
+  v.st = (BaState*)(p + d.oSt);
+  v.X0 = (double*)(p + d.oX0);
+  v.X1 = (double*)(p + d.oX1);
   v.Lf = (double*)(p + d.oL);
   v.gl = (double*)(p + d.oG);
   v.lstart = (int*)(p + d.oLs);
   v.obs = (BaObs*)(p + d.oObs);
   v.flist = (int*)(p + d.oFl);
   v.W = (double*)(p + d.oW);
-  v.Yt = (double*)(p + d.oYt);
+  v.Gp = (double*)(p + d.oGp);
+  v.cp = (double*)(p + d.oCp);
   v.next = (int*)(p + d.oNext);
-  v.Sg = (double*)(p + d.oSg);
   v.hdr = (int*)(p + d.oHdr);
-  v.cmask = (uint32_t*)(p + d.oCm);
   return v;
 }
-// hdr: [0] landmarks [1] observations [2] frames n [3] first frame s [8 + f] frame list offsets
+// hdr: [8 + f] per-frame observation list offsets
 
 // exclusive block scan of v (blockDim = kBlock); returns prefix, *total = block sum
 __device__ int block_scan(int v, int* s_tmp, int* total) {
@@ -96,7 +109,7 @@ __device__ int block_scan(int v, int* s_tmp, int* total) {
   return pre + x - v;
 }
 
-// deterministic block sum of doubles (fixed tree)
+// deterministic block sum of doubles (fixed tree); result valid in every thread
 __device__ double block_sum(double v, double* s_red) {
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
@@ -145,8 +158,8 @@ struct BaIn {
   int nlev;
 };
 
-// T = [R (9, row-major) | t (3)]
-__device__ __forceinline__ void mat_mul_T(const double* A, const double* B, double* C) {  // C = A * B (rigid)
+// T = [R (9, row-major) | t (3)];  C = A * B (rigid)
+__device__ __forceinline__ void mat_mul_T(const double* A, const double* B, double* C) {
   for (int i = 0; i < 3; ++i) {
     for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
     C[9 + i] = A[3 * i] * B[9] + A[3 * i + 1] * B[10] + A[3 * i + 2] * B[11] + A[9 + i];
@@ -193,9 +206,9 @@ __device__ __forceinline__ void ba_eval(const double* T, const double* X, const 
   rho = ok ? (inl ? s : 2.0 * sqrt(d2 * s) - d2) : 0.0;
   w = ok ? (inl ? 1.0 : sqrt(d2 / fmax(s, 1e-300))) * is2 : 0.0;
   if (!J) return;
-  double Jc[3][3] = {{c.fx * iz, 0.0, -c.fx * x * iz * iz},
-                     {0.0, c.fy * iz, -c.fy * y * iz * iz},
-                     {st ? c.fx * iz : 0.0, 0.0, st ? -c.fx * (x - c.b) * iz * iz : 0.0}};
+  const double Jc[3][3] = {{c.fx * iz, 0.0, -c.fx * x * iz * iz},
+                           {0.0, c.fy * iz, -c.fy * y * iz * iz},
+                           {st ? c.fx * iz : 0.0, 0.0, st ? -c.fx * (x - c.b) * iz * iz : 0.0}};
   // d(Xc)/d(w, v) = [-[Xc]x | I]
   const double sk[3][6] = {{0.0, z, -y, 1.0, 0.0, 0.0}, {-z, 0.0, x, 0.0, 1.0, 0.0}, {y, -x, 0.0, 0.0, 0.0, 1.0}};
   for (int k = 0; k < 3; ++k) {
@@ -204,9 +217,24 @@ __device__ __forceinline__ void ba_eval(const double* T, const double* X, const 
   }
 }
 
+// outlier test of oracle/ba_ref.py _reject (current estimate)
+__device__ __forceinline__ bool ba_outlier(const double* T, const double* X, const BaObs& o, const BaCam& c,
+                                           double is2) {
+  const double x = T[0] * X[0] + T[1] * X[1] + T[2] * X[2] + T[9];
+  const double y = T[3] * X[0] + T[4] * X[1] + T[5] * X[2] + T[10];
+  const double z = T[6] * X[0] + T[7] * X[1] + T[8] * X[2] + T[11];
+  const bool ok = z > kMinZ;
+  const double iz = 1.0 / (ok ? z : 1.0);
+  const bool st = !isnan(o.ur);
+  const double r0 = c.fx * x * iz + c.cx - (double)o.u;
+  const double r1 = c.fy * y * iz + c.cy - (double)o.v;
+  const double r2 = st ? c.fx * (x - c.b) * iz + c.cx - (double)o.ur : 0.0;
+  const double s = (r0 * r0 + r1 * r1 + r2 * r2) * is2;
+  return !(ok && s <= (st ? kD2Stereo : kD2Mono));
+}
+
 // ------------------------------------------------------------------ problem construction
-__global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims dm, BaCam cam, int first_end,
-                                                    int first_valid) {
+__global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims dm, int first_end, int first_valid) {
   extern __shared__ uint8_t s_tracked[];  // [cap]
   __shared__ double sT[kKMax][12];
   __shared__ int s_tmp[kBlock / 64];
@@ -216,12 +244,14 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
   const int s = max(first_valid, e - dm.K + 1);
   const int n = e - s + 1;
   BaWin v = view(ws, dm, w);
+  BaState* S = v.st;
   const int cap = dm.cap;
   if (tid == 0) {
-    v.hdr[0] = 0;
-    v.hdr[1] = 0;
-    v.hdr[2] = n;
-    v.hdr[3] = s;
+    S->L = 0;
+    S->O = 0;
+    S->n = n;
+    S->s = s;
+    S->active = 0;
     s_L = 0;
     s_O = 0;
     s_stop = 0;
@@ -257,7 +287,6 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
     __syncthreads();
     const int M = min(max(in.nmatch[f], 0), cap);
     const int32_t* m = in.matches + (int64_t)f * cap * 3;
-    // inverse of the initial pose j (world <- camera j)
     const double* Tj = sT[j];
     for (int base = 0; base < M; base += kBlock) {
       if (s_stop) break;  // uniform: written before the last barrier
@@ -285,6 +314,8 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
       const int lid = block_scan(cand ? 1 : 0, s_tmp, &tl);
       const int oof = block_scan(len, s_tmp, &to);
       const int L0 = s_L, O0 = s_O;
+      // creation stops at the first landmark that does not fit (the failing rows are a
+      // suffix of this chunk's candidates: both prefix sums are monotone)
       const bool ok = cand && (L0 + lid < dm.Lmax) && (O0 + oof + len <= dm.Omax);
       const int nok = __syncthreads_count(ok);
       const int nfail = __syncthreads_count(cand && !ok);
@@ -293,7 +324,7 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
         int o = O0 + oof;
         // X_world = R^T (Xc - t)
         const double Xc[3] = {(double)sp.x - Tj[9], (double)sp.y - Tj[10], (double)sp.z - Tj[11]};
-        for (int i = 0; i < 3; ++i) v.X[3 * id + i] = Tj[i] * Xc[0] + Tj[3 + i] * Xc[1] + Tj[6 + i] * Xc[2];
+        for (int i = 0; i < 3; ++i) v.X0[3 * id + i] = Tj[i] * Xc[0] + Tj[3 + i] * Xc[1] + Tj[6 + i] * Xc[2];
         v.lstart[id] = o;
         const float* kq = in.kp + ((int64_t)f * cap + q) * FVO_KP_STRIDE;
         const int oq = min(max((int)kq[5], 0), in.nlev - 1);
@@ -309,9 +340,8 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
           b = nb;
         }
       }
-      // totals of the ok rows (failing rows are a suffix of the candidates)
-      int okl = ok ? len : 0, tot_ok;
-      (void)block_scan(okl, s_tmp, &tot_ok);
+      int tot_ok;
+      (void)block_scan(ok ? len : 0, s_tmp, &tot_ok);
       if (tid == 0) {
         s_L = L0 + nok;
         s_O = O0 + tot_ok;
@@ -324,11 +354,6 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
   }
   __syncthreads();
   const int L = s_L, O = s_O;
-  if (tid == 0) {
-    v.hdr[0] = L;
-    v.hdr[1] = O;
-    v.lstart[L] = O;
-  }
   // per-frame observation lists (stable, landmark-major order inside a frame)
   int fbase = 0;
   for (int f = 0; f < n; ++f) {
@@ -342,369 +367,384 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
       fbase += tot;
     }
   }
-  if (tid == 0) v.hdr[8 + n] = fbase;
-}
-
-// ------------------------------------------------------------------ LM solve
-struct BaOut {
-  double* Tout;
-  double* stats;
-};
-
-__device__ double ba_cost(const BaWin& v, int O, const double (*T)[12], const double* X, const BaCam& cam,
-                          const BaIn& in, double* s_red) {
-  double acc = 0;
-  for (int i = threadIdx.x; i < O; i += kBlock) {
-    const BaObs o = v.obs[i];
-    double r[3], w, rho;
-    ba_eval<false>(T[o.frame], X + 3 * o.lm, o, cam, obs_is2(in, o), r, w, rho, nullptr, nullptr);
-    acc += rho;
+  if (tid == 0) {
+    v.hdr[8 + n] = fbase;
+    v.lstart[L] = O;
+    S->L = L;
+    S->O = O;
+    S->active = L > 0;
+    S->lam = kLam0;
+    S->parity = 0;
+    S->fail = 0;
+    S->acc = 0;
+    S->cost = 0.0;
+    S->cost0 = 0.0;
   }
-  return 0.5 * block_sum(acc, s_red);
+  for (int i = tid; i < n * 12; i += kBlock) S->T[i / 12][i % 12] = sT[i / 12][i % 12];
 }
 
-__global__ __launch_bounds__(kBlock) void k_ba_solve(BaIn in, void* ws, BaDims dm, BaCam cam, int first_end,
-                                                    int iters, BaOut out) {
-  extern __shared__ double sS[];  // [np*np] + rhs[np]
-  __shared__ double sT[kKMax][12], sTt[kKMax][12];
-  __shared__ double sH[kKMax][21], sg[kKMax][6];
-  __shared__ double sdp[6 * kKMax];
+// ------------------------------------------------------------------ LM iteration kernels
+__device__ __forceinline__ const double* cur_X(const BaWin& v, const BaState* S) { return S->parity ? v.X1 : v.X0; }
+__device__ __forceinline__ double* new_X(const BaWin& v, const BaState* S) { return S->parity ? v.X0 : v.X1; }
+
+// cost partials at the current estimate, optionally rejecting outliers first
+__global__ __launch_bounds__(kBlock) void k_ba_cost(BaIn in, void* ws, BaDims dm, BaCam cam, int reject) {
   __shared__ double s_red[kBlock / 64];
-  __shared__ double s_lam, s_cost, s_costn;
-  __shared__ int s_fail, s_acc;
-  const int wi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  BaWin v = view(ws, dm, wi);
-  const int L = v.hdr[0], O = v.hdr[1], n = v.hdr[2], s = v.hdr[3];
-  const int e = first_end + wi;
-  double* Tout = out.Tout + (int64_t)wi * 16;
-  double* st = out.stats + (int64_t)wi * 6;
-  if (n < 3 || L == 0) {
-    for (int i = tid; i < 16; i += kBlock) Tout[i] = in.Trel[(int64_t)(e - 1) * 16 + i];
-    if (tid < 6) st[tid] = tid == 4 ? (double)n : 0.0;
+  const BaWin v = view(ws, dm, blockIdx.x);
+  const BaState* S = v.st;
+  if (!S->active) return;
+  const int L = S->L, c = blockIdx.y;
+  if (c * kBlock >= L) return;
+  const double* X = cur_X(v, S);
+  const int l = c * kBlock + threadIdx.x;
+  double acc = 0;
+  if (l < L) {
+    for (int oi = v.lstart[l]; oi < v.lstart[l + 1]; ++oi) {
+      BaObs o = v.obs[oi];
+      if (reject && o.oct >= 0 && ba_outlier(S->T[o.frame], X + 3 * l, o, cam, in.isig2[o.oct])) {
+        o.oct = -1;
+        v.obs[oi].oct = -1;
+      }
+      double r[3], w, rho;
+      ba_eval<false>(S->T[o.frame], X + 3 * l, o, cam, obs_is2(in, o), r, w, rho, nullptr, nullptr);
+      acc += rho;
+    }
+  }
+  const double t = block_sum(acc, s_red);
+  if (threadIdx.x == 0) v.cp[c] = t;
+}
+
+__global__ void k_ba_setcost(void* ws, BaDims dm, int first) {
+  const BaWin v = view(ws, dm, blockIdx.x);
+  BaState* S = v.st;
+  if (threadIdx.x != 0 || !S->active) return;
+  const int nc = (S->L + kBlock - 1) / kBlock;
+  double c = 0;
+  for (int i = 0; i < nc; ++i) c += v.cp[i];
+  S->cost = 0.5 * c;
+  if (first) S->cost0 = 0.5 * c;
+}
+
+// pose blocks of one frame + W of its observations
+__global__ __launch_bounds__(kBlock) void k_ba_pp(BaIn in, void* ws, BaDims dm, BaCam cam) {
+  __shared__ double s_red[kBlock / 64];
+  const BaWin v = view(ws, dm, blockIdx.x);
+  BaState* S = v.st;
+  const int f = blockIdx.y + 1;
+  if (!S->active || f >= S->n) return;
+  const double* X = cur_X(v, S);
+  const double* T = S->T[f];
+  double h[27];
+  for (int i = 0; i < 27; ++i) h[i] = 0;
+  const int b0 = v.hdr[8 + f], b1 = v.hdr[8 + f + 1];
+  for (int ii = b0 + threadIdx.x; ii < b1; ii += kBlock) {
+    const int oi = v.flist[ii];
+    const BaObs o = v.obs[oi];
+    double r[3], w, rho, Jp[3][6], Jl[3][3];
+    ba_eval<true>(T, X + 3 * o.lm, o, cam, obs_is2(in, o), r, w, rho, Jp, Jl);
+    int q = 0;
+    for (int a = 0; a < 6; ++a) {
+      for (int bb = a; bb < 6; ++bb) h[q++] += w * (Jp[0][a] * Jp[0][bb] + Jp[1][a] * Jp[1][bb] + Jp[2][a] * Jp[2][bb]);
+      h[21 + a] += w * (Jp[0][a] * r[0] + Jp[1][a] * r[1] + Jp[2][a] * r[2]);
+    }
+    double* Wo = v.W + (int64_t)oi * 18;
+    for (int a = 0; a < 6; ++a)
+      for (int bb = 0; bb < 3; ++bb)
+        Wo[3 * a + bb] = w * (Jp[0][a] * Jl[0][bb] + Jp[1][a] * Jl[1][bb] + Jp[2][a] * Jl[2][bb]);
+  }
+  for (int i = 0; i < 27; ++i) {
+    const double t = block_sum(h[i], s_red);
+    if (threadIdx.x == 0) S->Hpp[f][i] = t;
+  }
+}
+
+// landmark blocks of a chunk + its share of the reduced camera system on MFMA
+__global__ __launch_bounds__(kBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm, BaCam cam) {
+  extern __shared__ double sY[];  // [3 LPC][NR + 2]
+  const BaWin v = view(ws, dm, blockIdx.x);
+  const BaState* S = v.st;
+  if (!S->active) return;
+  const int L = S->L, c = blockIdx.y, LPC = dm.LPC;
+  if (c * LPC >= L) return;
+  const int n = S->n;
+  const int np = 6 * (n - 1);
+  const int NR = dm.NR, NRP = NR + 2, rows = 3 * LPC;
+  const double lam = S->lam;
+  const double* X = cur_X(v, S);
+  for (int i = threadIdx.x; i < rows * NRP; i += kBlock) sY[i] = 0.0;
+  __syncthreads();
+  const int t = threadIdx.x, l = c * LPC + t;
+  if (t < LPC && l < L) {
+    const int o0 = v.lstart[l], o1 = v.lstart[l + 1];
+    double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+    for (int oi = o0; oi < o1; ++oi) {
+      const BaObs o = v.obs[oi];
+      double r[3], w, rho, Jp[3][6], Jl[3][3];
+      ba_eval<true>(S->T[o.frame], X + 3 * l, o, cam, obs_is2(in, o), r, w, rho, Jp, Jl);
+      int q = 0;
+      for (int a = 0; a < 3; ++a) {
+        for (int b = a; b < 3; ++b) H[q++] += w * (Jl[0][a] * Jl[0][b] + Jl[1][a] * Jl[1][b] + Jl[2][a] * Jl[2][b]);
+        g[a] += w * (Jl[0][a] * r[0] + Jl[1][a] * r[1] + Jl[2][a] * r[2]);
+      }
+    }
+    // damped Cholesky of [H0 H1 H2; . H3 H4; . . H5]
+    const double a00 = H[0] + lam * H[0] + 1e-6, a11 = H[3] + lam * H[3] + 1e-6, a22 = H[5] + lam * H[5] + 1e-6;
+    const double l00 = sqrt(a00);
+    const double l10 = H[1] / l00, l20 = H[2] / l00;
+    const double l11 = sqrt(a11 - l10 * l10);
+    const double l21 = (H[4] - l20 * l10) / l11;
+    const double l22 = sqrt(a22 - l20 * l20 - l21 * l21);
+    double* Lf = v.Lf + 6 * l;
+    Lf[0] = l00; Lf[1] = l10; Lf[2] = l11; Lf[3] = l20; Lf[4] = l21; Lf[5] = l22;
+    v.gl[3 * l] = g[0]; v.gl[3 * l + 1] = g[1]; v.gl[3 * l + 2] = g[2];
+    double* Y0 = sY + 3 * t * NRP;
+    for (int oi = o0; oi < o1; ++oi) {
+      const int f = v.obs[oi].frame;
+      if (f == 0) continue;
+      const double* Wo = v.W + (int64_t)oi * 18;
+      for (int p = 0; p < 6; ++p) {  // row p of W L^-T: solve L y = W_p
+        const double y0 = Wo[3 * p] / l00;
+        const double y1 = (Wo[3 * p + 1] - l10 * y0) / l11;
+        const double y2 = (Wo[3 * p + 2] - l20 * y0 - l21 * y1) / l22;
+        const int col = 6 * (f - 1) + p;
+        Y0[col] = y0;
+        Y0[NRP + col] = y1;
+        Y0[2 * NRP + col] = y2;
+      }
+    }
+    const double z0 = g[0] / l00, z1 = (g[1] - l10 * z0) / l11, z2 = (g[2] - l20 * z0 - l21 * z1) / l22;
+    Y0[NR - 1] = z0;
+    Y0[NRP + NR - 1] = z1;
+    Y0[2 * NRP + NR - 1] = z2;
+  }
+  __syncthreads();
+  // G_chunk = Yt^T Yt on MFMA, upper 16x16 tiles that intersect the np x np system or
+  // its z column; A[i][k] = Yt[k][16I + i], B[k][j] = Yt[k][16J + j], lane holds k = lane >> 4
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int NT = NR / 16, ntu = (np + 15) / 16;  // tiles covering the pose rows
+  double* Gc = v.Gp + (int64_t)c * NR * NR;
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  int pidx = 0;
+  for (int I = 0; I < ntu; ++I)
+    for (int J = I; J < NT; ++J) {
+      if (J >= ntu && J != NT - 1) continue;  // only the z column beyond the pose rows
+      if ((pidx++ & 3) != wid) continue;
+      d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+      const double* ya = sY + (lane >> 4) * NRP + 16 * I + (lane & 15);
+      const double* yb = sY + (lane >> 4) * NRP + 16 * J + (lane & 15);
+      for (int k0 = 0; k0 < rows; k0 += 8) {
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[k0 * NRP], yb[k0 * NRP], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[(k0 + 4) * NRP], yb[(k0 + 4) * NRP], acc1, 0, 0, 0);
+      }
+      // f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
+      for (int i = 0; i < 4; ++i) Gc[(16 * I + (lane >> 4) + 4 * i) * NR + 16 * J + (lane & 15)] = acc0[i] + acc1[i];
+    }
+}
+
+// reduced camera system, Cholesky, pose step and tentative poses
+__global__ __launch_bounds__(kBlock) void k_ba_solve(void* ws, BaDims dm) {
+  extern __shared__ double sS[];  // [np*np] + rhs[np]
+  __shared__ int s_fail;
+  const BaWin v = view(ws, dm, blockIdx.x);
+  BaState* S = v.st;
+  if (!S->active) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int n = S->n, L = S->L, NR = dm.NR;
+  const int np = 6 * (n - 1);
+  const int nch = (L + dm.LPC - 1) / dm.LPC;
+  const double lam = S->lam;
+  double* rhs = sS + np * np;
+  for (int idx = tid; idx < np * np; idx += kBlock) {
+    const int a = idx / np, b = idx % np;
+    if (a > b) continue;
+    const int fa = a / 6 + 1, fb = b / 6 + 1;
+    double hv = 0.0;
+    if (fa == fb) {
+      const int i = a % 6, j = b % 6;
+      const int q = i * 6 - i * (i - 1) / 2 + (j - i);
+      hv = S->Hpp[fa][q];
+      if (i == j) hv += lam * hv + 1e-6;
+    }
+    double gs = 0.0;
+    for (int c = 0; c < nch; ++c) gs += v.Gp[(int64_t)c * NR * NR + a * NR + b];
+    sS[a * np + b] = hv - gs;
+    sS[b * np + a] = hv - gs;
+  }
+  for (int a = tid; a < np; a += kBlock) {
+    double gs = 0.0;
+    for (int c = 0; c < nch; ++c) gs += v.Gp[(int64_t)c * NR * NR + a * NR + NR - 1];
+    rhs[a] = -S->Hpp[a / 6 + 1][21 + a % 6] + gs;
+  }
+  if (tid == 0) s_fail = 0;
+  __syncthreads();
+  for (int k = 0; k < np; ++k) {
+    if (tid == 0) {
+      const double d = sS[k * np + k];
+      if (!(d > 0.0)) s_fail = 1;
+      else sS[k * np + k] = sqrt(d);
+    }
+    __syncthreads();
+    if (s_fail) break;
+    const double dk = sS[k * np + k];
+    for (int i = k + 1 + tid; i < np; i += kBlock) sS[i * np + k] /= dk;
+    __syncthreads();
+    const int m = np - k - 1;
+    for (int idx = tid; idx < m * m; idx += kBlock) {
+      const int i = k + 1 + idx / m, j = k + 1 + idx % m;
+      if (j <= i) sS[i * np + j] -= sS[i * np + k] * sS[j * np + k];
+    }
+    __syncthreads();
+  }
+  if (s_fail) {
+    if (tid == 0) S->fail = 1;
     return;
   }
-  const int np = 6 * (n - 1);
-  const int NR = np < 63 ? 64 : 128;
-  const int KP = ((3 * L + 7) / 8) * 8;
-  double* rhs = sS + np * np;
-  if (tid == 0) {
-    for (int i = 0; i < 12; ++i) sT[0][i] = (i < 9 && i % 4 == 0) ? 1.0 : 0.0;
-    for (int k = 0; k + 1 < n; ++k) {
-      const double* M = in.Trel + (int64_t)(s + k) * 16;
-      const double A[12] = {M[0], M[1], M[2], M[4], M[5], M[6], M[8], M[9], M[10], M[3], M[7], M[11]};
-      mat_mul_T(A, sT[k], sT[k + 1]);
+  if (wid == 0) {  // L y = rhs, L^T x = y (wave 0)
+    for (int i = 0; i < np; ++i) {
+      double p = 0;
+      for (int j = lane; j < i; j += 64) p += sS[i * np + j] * rhs[j];
+      p = wave_sum(p);
+      if (lane == 0) rhs[i] = (rhs[i] - p) / sS[i * np + i];
+      __builtin_amdgcn_wave_barrier();
     }
-    s_lam = kLam0;
+    for (int i = np - 1; i >= 0; --i) {
+      double p = 0;
+      for (int j = i + 1 + lane; j < np; j += 64) p += sS[j * np + i] * rhs[j];
+      p = wave_sum(p);
+      if (lane == 0) rhs[i] = (rhs[i] - p) / sS[i * np + i];
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  __syncthreads();
+  for (int a = tid; a < 6 * n; a += kBlock) S->dp[a] = a < 6 ? 0.0 : rhs[a - 6];
+  if (tid < n) {
+    const int f = tid;
+    double* Tt = S->Tt[f];
+    const double* T = S->T[f];
+    if (f == 0) {
+      for (int i = 0; i < 12; ++i) Tt[i] = T[i];
+    } else {
+      double Rw[9];
+      const double* d = rhs + 6 * (f - 1);
+      exp_so3(d, Rw);
+      for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) Tt[3 * i + j] = Rw[3 * i] * T[j] + Rw[3 * i + 1] * T[3 + j] + Rw[3 * i + 2] * T[6 + j];
+        Tt[9 + i] = Rw[3 * i] * T[9] + Rw[3 * i + 1] * T[10] + Rw[3 * i + 2] * T[11] + d[3 + i];
+      }
+    }
+  }
+}
+
+// landmark back-substitution + cost partials at the tentative point
+__global__ __launch_bounds__(kBlock) void k_ba_upd(BaIn in, void* ws, BaDims dm, BaCam cam) {
+  __shared__ double s_red[kBlock / 64];
+  const BaWin v = view(ws, dm, blockIdx.x);
+  const BaState* S = v.st;
+  if (!S->active || S->fail) return;
+  const int L = S->L, c = blockIdx.y;
+  if (c * kBlock >= L) return;
+  const double* X = cur_X(v, S);
+  double* Xn = new_X(v, S);
+  const int l = c * kBlock + threadIdx.x;
+  double acc = 0;
+  if (l < L) {
+    const int o0 = v.lstart[l], o1 = v.lstart[l + 1];
+    double b[3] = {-v.gl[3 * l], -v.gl[3 * l + 1], -v.gl[3 * l + 2]};
+    for (int oi = o0; oi < o1; ++oi) {
+      const int f = v.obs[oi].frame;
+      if (f == 0) continue;
+      const double* Wo = v.W + (int64_t)oi * 18;
+      const double* dp = S->dp + 6 * f;
+      for (int k = 0; k < 3; ++k)
+        b[k] -= Wo[k] * dp[0] + Wo[3 + k] * dp[1] + Wo[6 + k] * dp[2] + Wo[9 + k] * dp[3] + Wo[12 + k] * dp[4] +
+                Wo[15 + k] * dp[5];
+    }
+    const double* Lf = v.Lf + 6 * l;
+    const double y0 = b[0] / Lf[0], y1 = (b[1] - Lf[1] * y0) / Lf[2], y2 = (b[2] - Lf[3] * y0 - Lf[4] * y1) / Lf[5];
+    const double x2 = y2 / Lf[5], x1 = (y1 - Lf[4] * x2) / Lf[2], x0 = (y0 - Lf[1] * x1 - Lf[3] * x2) / Lf[0];
+    const double Xl[3] = {X[3 * l] + x0, X[3 * l + 1] + x1, X[3 * l + 2] + x2};
+    Xn[3 * l] = Xl[0];
+    Xn[3 * l + 1] = Xl[1];
+    Xn[3 * l + 2] = Xl[2];
+    for (int oi = o0; oi < o1; ++oi) {
+      const BaObs o = v.obs[oi];
+      double r[3], w, rho;
+      ba_eval<false>(S->Tt[o.frame], Xl, o, cam, obs_is2(in, o), r, w, rho, nullptr, nullptr);
+      acc += rho;
+    }
+  }
+  const double t = block_sum(acc, s_red);
+  if (threadIdx.x == 0) v.cp[c] = t;
+}
+
+__global__ void k_ba_accept(void* ws, BaDims dm) {
+  const BaWin v = view(ws, dm, blockIdx.x);
+  BaState* S = v.st;
+  if (!S->active) return;
+  const int n = S->n;
+  __shared__ int s_acc;
+  if (threadIdx.x == 0) {
     s_acc = 0;
-  }
-  // Yt is zeroed once (coalesced); every iteration rewrites only the structurally nonzero
-  // entries (the 6x3 block of each observation and the z row), whose positions are fixed.
-  for (int64_t i = tid; i < (int64_t)KP * NR; i += kBlock) v.Yt[i] = 0.0;
-  // frame mask of every 4-row chunk of Yt, so P3 skips chunks that cannot touch a tile
-  for (int c = tid; c < KP / 4; c += kBlock) {
-    uint32_t m = 0;
-    for (int k = 4 * c; k < 4 * c + 4 && k < 3 * L; ++k) {
-      const int l = k / 3;
-      m |= 1u << 31;
-      for (int oi = v.lstart[l]; oi < v.lstart[l + 1]; ++oi) m |= 1u << v.obs[oi].frame;
-    }
-    v.cmask[c] = m;
-  }
-  __syncthreads();
-  double* X = v.X;
-  double* Xt = v.Xt;
-  {
-    const double c = ba_cost(v, O, sT, X, cam, in, s_red);
-    if (tid == 0) {
-      s_cost = c;
-      st[0] = c;
+    if (S->fail) {
+      S->lam = fmin(S->lam * 10.0, 1e7);
+      S->fail = 0;
+    } else {
+      const int nc = (S->L + kBlock - 1) / kBlock;
+      double c = 0;
+      for (int i = 0; i < nc; ++i) c += v.cp[i];
+      c *= 0.5;
+      if (c < S->cost) {
+        S->cost = c;
+        S->lam = fmax(S->lam / 10.0, 1e-7);
+        S->parity ^= 1;
+        S->acc += 1;
+        s_acc = 1;
+      } else {
+        S->lam = fmin(S->lam * 10.0, 1e7);
+      }
     }
   }
   __syncthreads();
-  for (int it = 0; it < iters; ++it) {
-    if (it == iters / 2 && iters >= 2) {
-      // outlier rejection at the current estimate (oracle/ba_ref.py _reject)
-      for (int i = tid; i < O; i += kBlock) {
-        const BaObs o = v.obs[i];
-        if (o.oct < 0) continue;
-        const double* T = sT[o.frame];
-        const double* Xl = X + 3 * o.lm;
-        const double x = T[0] * Xl[0] + T[1] * Xl[1] + T[2] * Xl[2] + T[9];
-        const double y = T[3] * Xl[0] + T[4] * Xl[1] + T[5] * Xl[2] + T[10];
-        const double z = T[6] * Xl[0] + T[7] * Xl[1] + T[8] * Xl[2] + T[11];
-        const bool ok = z > kMinZ;
-        const double iz = 1.0 / (ok ? z : 1.0);
-        const bool st = !isnan(o.ur);
-        const double r0 = cam.fx * x * iz + cam.cx - (double)o.u;
-        const double r1 = cam.fy * y * iz + cam.cy - (double)o.v;
-        const double r2 = st ? cam.fx * (x - cam.b) * iz + cam.cx - (double)o.ur : 0.0;
-        const double s = (r0 * r0 + r1 * r1 + r2 * r2) * in.isig2[o.oct];
-        if (!(ok && s <= (st ? kD2Stereo : kD2Mono))) v.obs[i].oct = -1;
-      }
-      __syncthreads();
-      const double c = ba_cost(v, O, sT, X, cam, in, s_red);
-      if (tid == 0) s_cost = c;
-      __syncthreads();
-    }
-    const double lam = s_lam;
-    // ---- P1: pose blocks (wave per frame)
-    for (int f = 1 + wid; f < n; f += kBlock / 64) {
-      double h[21], g[6];
-      for (int i = 0; i < 21; ++i) h[i] = 0;
-      for (int i = 0; i < 6; ++i) g[i] = 0;
-      const int b0 = v.hdr[8 + f], b1 = v.hdr[8 + f + 1];
-      for (int ii = b0 + lane; ii < b1; ii += 64) {
-        const int oi = v.flist[ii];
-        const BaObs o = v.obs[oi];
-        double r[3], w, rho, Jp[3][6], Jl[3][3];
-        ba_eval<true>(sT[f], X + 3 * o.lm, o, cam, obs_is2(in, o), r, w, rho, Jp, Jl);
-        int q = 0;
-        for (int a = 0; a < 6; ++a) {
-          for (int b = a; b < 6; ++b) h[q++] += w * (Jp[0][a] * Jp[0][b] + Jp[1][a] * Jp[1][b] + Jp[2][a] * Jp[2][b]);
-          g[a] += w * (Jp[0][a] * r[0] + Jp[1][a] * r[1] + Jp[2][a] * r[2]);
-        }
-        double* Wo = v.W + (int64_t)oi * 18;
-        for (int a = 0; a < 6; ++a)
-          for (int b = 0; b < 3; ++b) Wo[3 * a + b] = w * (Jp[0][a] * Jl[0][b] + Jp[1][a] * Jl[1][b] + Jp[2][a] * Jl[2][b]);
-      }
-      for (int i = 0; i < 21; ++i) h[i] = wave_sum(h[i]);
-      for (int i = 0; i < 6; ++i) g[i] = wave_sum(g[i]);
-      if (lane == 0) {
-        for (int i = 0; i < 21; ++i) sH[f][i] = h[i];
-        for (int i = 0; i < 6; ++i) sg[f][i] = g[i];
-      }
-    }
-    __syncthreads();  // W of every observation is complete before P2 reads it
-    // ---- P2: landmarks -> L_l, g_l, Yt columns
-    for (int l = tid; l < L; l += kBlock) {
-      const int o0 = v.lstart[l], o1 = v.lstart[l + 1];
-      double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-      for (int oi = o0; oi < o1; ++oi) {
-        const BaObs o = v.obs[oi];
-        double r[3], w, rho, Jp[3][6], Jl[3][3];
-        ba_eval<true>(sT[o.frame], X + 3 * l, o, cam, obs_is2(in, o), r, w, rho, Jp, Jl);
-        int q = 0;
-        for (int a = 0; a < 3; ++a) {
-          for (int b = a; b < 3; ++b) H[q++] += w * (Jl[0][a] * Jl[0][b] + Jl[1][a] * Jl[1][b] + Jl[2][a] * Jl[2][b]);
-          g[a] += w * (Jl[0][a] * r[0] + Jl[1][a] * r[1] + Jl[2][a] * r[2]);
-        }
-      }
-      // damped Cholesky of [H0 H1 H2; . H3 H4; . . H5]
-      const double a00 = H[0] + lam * H[0] + 1e-6, a11 = H[3] + lam * H[3] + 1e-6, a22 = H[5] + lam * H[5] + 1e-6;
-      const double l00 = sqrt(a00);
-      const double l10 = H[1] / l00, l20 = H[2] / l00;
-      const double l11 = sqrt(a11 - l10 * l10);
-      const double l21 = (H[4] - l20 * l10) / l11;
-      const double l22 = sqrt(a22 - l20 * l20 - l21 * l21);
-      double* Lf = v.Lf + 6 * l;
-      Lf[0] = l00; Lf[1] = l10; Lf[2] = l11; Lf[3] = l20; Lf[4] = l21; Lf[5] = l22;
-      v.gl[3 * l] = g[0]; v.gl[3 * l + 1] = g[1]; v.gl[3 * l + 2] = g[2];
-      double* Y0 = v.Yt + (int64_t)(3 * l) * NR;
-      for (int oi = o0; oi < o1; ++oi) {
-        const int f = v.obs[oi].frame;
-        if (f == 0) continue;
-        const double* Wo = v.W + (int64_t)oi * 18;
-        for (int p = 0; p < 6; ++p) {  // row p of W L^-T: solve L y = W_p
-          const double y0 = Wo[3 * p] / l00;
-          const double y1 = (Wo[3 * p + 1] - l10 * y0) / l11;
-          const double y2 = (Wo[3 * p + 2] - l20 * y0 - l21 * y1) / l22;
-          const int row = 6 * (f - 1) + p;
-          Y0[row] = y0;
-          Y0[NR + row] = y1;
-          Y0[2 * NR + row] = y2;
-        }
-      }
-      const double z0 = g[0] / l00, z1 = (g[1] - l10 * z0) / l11, z2 = (g[2] - l20 * z0 - l21 * z1) / l22;
-      Y0[NR - 1] = z0;
-      Y0[2 * NR - 1] = z1;
-      Y0[3 * NR - 1] = z2;
-    }
-    __syncthreads();
-    // ---- P3: G = Yt^T Yt on MFMA (upper 16x16 tiles)
-    {
-      const int NT = NR / 16;
-      const int npairs = NT * (NT + 1) / 2;
-      for (int pidx = wid; pidx < npairs; pidx += kBlock / 64) {
-        int I = 0, rem = pidx;
-        while (rem >= NT - I) {
-          rem -= NT - I;
-          ++I;
-        }
-        const int J = I + rem;
-        typedef double d4 __attribute__((ext_vector_type(4)));
-        d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-        // A[i][k] = Yt[k][16I + i], B[k][j] = Yt[k][16J + j]; lane holds k = lane >> 4
-        const double* ya = v.Yt + (lane >> 4) * NR + 16 * I + (lane & 15);
-        const double* yb = v.Yt + (lane >> 4) * NR + 16 * J + (lane & 15);
-        // frames whose pose rows fall in tile I / J (bit 31: the z column NR-1); a 4-row
-        // chunk contributes only if its landmarks touch both (skipped chunks add exact 0)
-        uint32_t mI = 0, mJ = 0;
-        for (int r = 0; r < 16; ++r) {
-          const int ra = 16 * I + r, rb = 16 * J + r;
-          mI |= ra < np ? 1u << (ra / 6 + 1) : (ra == NR - 1 ? 1u << 31 : 0u);
-          mJ |= rb < np ? 1u << (rb / 6 + 1) : (rb == NR - 1 ? 1u << 31 : 0u);
-        }
-        int par = 0;
-        for (int c = 0; c < KP / 4; ++c) {
-          const uint32_t cm = v.cmask[c];
-          if (!(cm & mI) || !(cm & mJ)) continue;
-          const int64_t o = (int64_t)(4 * c) * NR;
-          if (par)
-            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[o], yb[o], acc1, 0, 0, 0);
-          else
-            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[o], yb[o], acc0, 0, 0, 0);
-          par ^= 1;
-        }
-        // f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
-        for (int i = 0; i < 4; ++i)
-          v.Sg[(16 * I + (lane >> 4) + 4 * i) * NR + 16 * J + (lane & 15)] = acc0[i] + acc1[i];
-      }
-    }
-    __syncthreads();
-    // ---- P4: reduced camera system, Cholesky
-    for (int idx = tid; idx < np * np; idx += kBlock) {
-      const int a = idx / np, b = idx % np;
-      const int fa = a / 6 + 1, fb = b / 6 + 1;
-      double hv = 0.0;
-      if (fa == fb) {
-        const int i = min(a % 6, b % 6), j = max(a % 6, b % 6);
-        const int q = i * 6 - i * (i - 1) / 2 + (j - i);
-        hv = sH[fa][q];
-        if (i == j) hv += lam * hv + 1e-6;
-      }
-      const double gv = a <= b ? v.Sg[a * NR + b] : v.Sg[b * NR + a];
-      sS[idx] = hv - gv;
-    }
-    for (int a = tid; a < np; a += kBlock) rhs[a] = -sg[a / 6 + 1][a % 6] + v.Sg[a * NR + NR - 1];
-    if (tid == 0) s_fail = 0;
-    __syncthreads();
-    for (int k = 0; k < np; ++k) {
-      if (tid == 0) {
-        const double d = sS[k * np + k];
-        if (!(d > 0.0)) s_fail = 1;
-        else sS[k * np + k] = sqrt(d);
-      }
-      __syncthreads();
-      if (s_fail) break;
-      const double dk = sS[k * np + k];
-      for (int i = k + 1 + tid; i < np; i += kBlock) sS[i * np + k] /= dk;
-      __syncthreads();
-      const int m = np - k - 1;
-      for (int idx = tid; idx < m * m; idx += kBlock) {
-        const int i = k + 1 + idx / m, j = k + 1 + idx % m;
-        if (j <= i) sS[i * np + j] -= sS[i * np + k] * sS[j * np + k];
-      }
-      __syncthreads();
-    }
-    if (s_fail) {
-      if (tid == 0) s_lam = fmin(s_lam * 10.0, 1e7);
-      __syncthreads();
-      continue;
-    }
-    if (wid == 0) {  // L y = rhs, L^T x = y (wave 0)
-      for (int i = 0; i < np; ++i) {
-        double p = 0;
-        for (int j = lane; j < i; j += 64) p += sS[i * np + j] * rhs[j];
-        p = wave_sum(p);
-        if (lane == 0) rhs[i] = (rhs[i] - p) / sS[i * np + i];
-        __builtin_amdgcn_s_waitcnt(0);
-        __builtin_amdgcn_wave_barrier();
-      }
-      for (int i = np - 1; i >= 0; --i) {
-        double p = 0;
-        for (int j = i + 1 + lane; j < np; j += 64) p += sS[j * np + i] * rhs[j];
-        p = wave_sum(p);
-        if (lane == 0) rhs[i] = (rhs[i] - p) / sS[i * np + i];
-        __builtin_amdgcn_s_waitcnt(0);
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-    __syncthreads();
-    for (int a = tid; a < 6 * n; a += kBlock) sdp[a] = a < 6 ? 0.0 : rhs[a - 6];
-    __syncthreads();
-    // ---- P5: landmark back-substitution and pose update
-    for (int l = tid; l < L; l += kBlock) {
-      const int o0 = v.lstart[l], o1 = v.lstart[l + 1];
-      double b[3] = {-v.gl[3 * l], -v.gl[3 * l + 1], -v.gl[3 * l + 2]};
-      for (int oi = o0; oi < o1; ++oi) {
-        const int f = v.obs[oi].frame;
-        if (f == 0) continue;
-        const double* Wo = v.W + (int64_t)oi * 18;
-        const double* dp = sdp + 6 * f;
-        for (int c = 0; c < 3; ++c)
-          b[c] -= Wo[c] * dp[0] + Wo[3 + c] * dp[1] + Wo[6 + c] * dp[2] + Wo[9 + c] * dp[3] + Wo[12 + c] * dp[4] +
-                  Wo[15 + c] * dp[5];
-      }
-      const double* Lf = v.Lf + 6 * l;
-      const double y0 = b[0] / Lf[0], y1 = (b[1] - Lf[1] * y0) / Lf[2], y2 = (b[2] - Lf[3] * y0 - Lf[4] * y1) / Lf[5];
-      const double x2 = y2 / Lf[5], x1 = (y1 - Lf[4] * x2) / Lf[2], x0 = (y0 - Lf[1] * x1 - Lf[3] * x2) / Lf[0];
-      Xt[3 * l] = X[3 * l] + x0;
-      Xt[3 * l + 1] = X[3 * l + 1] + x1;
-      Xt[3 * l + 2] = X[3 * l + 2] + x2;
-    }
-    if (tid < n) {
-      const int f = tid;
-      if (f == 0) {
-        for (int i = 0; i < 12; ++i) sTt[0][i] = sT[0][i];
-      } else {
-        double Rw[9];
-        exp_so3(sdp + 6 * f, Rw);
-        const double* T = sT[f];
-        for (int i = 0; i < 3; ++i) {
-          for (int j = 0; j < 3; ++j) sTt[f][3 * i + j] = Rw[3 * i] * T[j] + Rw[3 * i + 1] * T[3 + j] + Rw[3 * i + 2] * T[6 + j];
-          sTt[f][9 + i] = Rw[3 * i] * T[9] + Rw[3 * i + 1] * T[10] + Rw[3 * i + 2] * T[11] + sdp[6 * f + 3 + i];
-        }
-      }
-    }
-    __syncthreads();
-    // ---- P6/P7: cost at the tentative point, accept / reject
-    const double cn = ba_cost(v, O, sTt, Xt, cam, in, s_red);
-    if (tid == 0) {
-      if (cn < s_cost) {
-        s_cost = cn;
-        s_lam = fmax(s_lam / 10.0, 1e-7);
-        s_fail = 0;
-        ++s_acc;
-      } else {
-        s_lam = fmin(s_lam * 10.0, 1e7);
-        s_fail = 1;
-      }
-    }
-    __syncthreads();
-    if (!s_fail) {
-      if (tid < n)
-        for (int i = 0; i < 12; ++i) sT[tid][i] = sTt[tid][i];
-      double* tmp = X;
-      X = Xt;
-      Xt = tmp;
-    }
-    __syncthreads();
-  }
-  // refined relative transform of the last pair: T_{n-1} T_{n-2}^-1
-  if (tid == 0) {
-    const double* A = sT[n - 1];
-    const double* B = sT[n - 2];
-    double Bi[12];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) Bi[3 * i + j] = B[3 * j + i];
-    for (int i = 0; i < 3; ++i) Bi[9 + i] = -(Bi[3 * i] * B[9] + Bi[3 * i + 1] * B[10] + Bi[3 * i + 2] * B[11]);
-    double C[12];
-    mat_mul_T(A, Bi, C);
-    for (int i = 0; i < 3; ++i) {
-      for (int j = 0; j < 3; ++j) Tout[4 * i + j] = C[3 * i + j];
-      Tout[4 * i + 3] = C[9 + i];
-    }
-    Tout[12] = Tout[13] = Tout[14] = 0.0;
-    Tout[15] = 1.0;
-    st[1] = s_cost;
-    st[2] = (double)L;
-    st[3] = (double)O;
+  if (s_acc)
+    for (int i = threadIdx.x; i < n * 12; i += blockDim.x) S->T[i / 12][i % 12] = S->Tt[i / 12][i % 12];
+}
+
+// refined relative transform of the last pair: T_{n-1} T_{n-2}^-1, and statistics
+__global__ void k_ba_final(const double* __restrict__ Trel, void* ws, BaDims dm, int first_end,
+                           double* __restrict__ Tout_all, double* __restrict__ stats) {
+  const int wi = blockIdx.x;
+  const BaWin v = view(ws, dm, wi);
+  const BaState* S = v.st;
+  double* Tout = Tout_all + (int64_t)wi * 16;
+  double* st = stats + (int64_t)wi * 6;
+  if (threadIdx.x != 0) return;
+  const int e = first_end + wi, n = S->n;
+  if (!S->active) {
+    for (int i = 0; i < 16; ++i) Tout[i] = Trel[(int64_t)(e - 1) * 16 + i];
+    for (int i = 0; i < 6; ++i) st[i] = 0.0;
     st[4] = (double)n;
-    st[5] = (double)s_acc;
+    return;
   }
-  // the final landmark estimate lives in X (either buffer); keep v.X current for debugging
-  if (X != v.X)
-    for (int i = tid; i < 3 * L; i += kBlock) v.X[i] = X[i];
+  const double* A = S->T[n - 1];
+  const double* B = S->T[n - 2];
+  double Bi[12];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Bi[3 * i + j] = B[3 * j + i];
+  for (int i = 0; i < 3; ++i) Bi[9 + i] = -(Bi[3 * i] * B[9] + Bi[3 * i + 1] * B[10] + Bi[3 * i + 2] * B[11]);
+  double C[12];
+  mat_mul_T(A, Bi, C);
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) Tout[4 * i + j] = C[3 * i + j];
+    Tout[4 * i + 3] = C[9 + i];
+  }
+  Tout[12] = Tout[13] = Tout[14] = 0.0;
+  Tout[15] = 1.0;
+  st[0] = S->cost0;
+  st[1] = S->cost;
+  st[2] = (double)S->L;
+  st[3] = (double)S->O;
+  st[4] = (double)n;
+  st[5] = (double)S->acc;
 }
 
 BaDims make_dims(const fvo_ctx* ctx) {
@@ -715,28 +755,36 @@ BaDims make_dims(const fvo_ctx* ctx) {
   d.K = c.ba_window;
   d.cap = ctx->kp_cap;
   d.NR = 6 * (d.K - 1) < 63 ? 64 : 128;
-  d.KP = ((3 * d.Lmax + 7) / 8) * 8;
+  d.LPC = d.NR == 64 ? 64 : 32;  // LDS slice 3 LPC x (NR + 2) doubles <= 99 KB
+  d.NCH = (d.Lmax + d.LPC - 1) / d.LPC;
+  d.NCU = (d.Lmax + kBlock - 1) / kBlock;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
     int64_t r = o;
     o += (bytes + 255) / 256 * 256;
     return r;
   };
-  d.oX = take(8ll * 3 * d.Lmax);
-  d.oXt = take(8ll * 3 * d.Lmax);
+  d.oSt = take((int64_t)sizeof(BaState));
+  d.oX0 = take(8ll * 3 * d.Lmax);
+  d.oX1 = take(8ll * 3 * d.Lmax);
   d.oL = take(8ll * 6 * d.Lmax);
   d.oG = take(8ll * 3 * d.Lmax);
   d.oLs = take(4ll * (d.Lmax + 1));
   d.oObs = take((int64_t)sizeof(BaObs) * d.Omax);
   d.oFl = take(4ll * d.Omax);
   d.oW = take(8ll * 18 * d.Omax);
-  d.oYt = take(8ll * d.KP * d.NR);
+  d.oGp = take(8ll * d.NCH * d.NR * d.NR);
+  d.oCp = take(8ll * d.NCU);
   d.oNext = take(4ll * kKMax * d.cap);
-  d.oSg = take(8ll * d.NR * d.NR);
   d.oHdr = take(4ll * (8 + kKMax + 1));
-  d.oCm = take(4ll * (d.KP / 4));
   d.win = o;
   return d;
+}
+
+size_t lin_shm(const BaDims& d) { return (size_t)8 * 3 * d.LPC * (d.NR + 2); }
+size_t solve_shm(int K) {
+  const int np = 6 * (K - 1);
+  return (size_t)8 * (np * np + np);
 }
 
 }  // namespace
@@ -751,10 +799,12 @@ int ba_init(fvo_ctx* ctx) {
   int rc = fvo_alloc(ctx, &p, (size_t)d.win * c.max_batch);
   if (rc) return rc;
   ctx->ba_ws = p;
-  // the solver's dynamic LDS (reduced camera system) can exceed 64 KiB for K > 11
-  const int np = 6 * (c.ba_window - 1);
-  const size_t shm = (size_t)8 * (np * np + np);
-  if (shm > 65536) FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  // dynamic LDS above 64 KiB: the MFMA slice always, the reduced system for K > 11
+  FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_lin, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lin_shm(d)));
+  if (solve_shm(c.ba_window) > 65536)
+    FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)solve_shm(c.ba_window)));
   return 0;
 }
 
@@ -779,18 +829,31 @@ int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* mat
   if (first_valid < 0 || first_valid >= first_end) return fvo_fail(ctx, "ba: first_valid out of range");
   if (nlev < 1 || nlev > FVO_MAX_LEVELS) return fvo_fail(ctx, "ba: bad level count");
   if (iters < 0 || iters > 100) return fvo_fail(ctx, "ba: iterations out of range");
-  BaDims d = make_dims(ctx);
+  const BaDims d = make_dims(ctx);
   BaIn in{kp, nkp, matches, nmatch, reinterpret_cast<const float4*>(stereo), Trel, {}, nlev};
   for (int i = 0; i < nlev; ++i) in.isig2[i] = inv_sigma2[i];
-  BaCam cam{K[0], K[4], K[2], K[5], baseline};
+  const BaCam cam{K[0], K[4], K[2], K[5], baseline};
+  void* ws = ctx->ba_ws;
   FVO_TIMED(ctx, KN_BA_BUILD, s,
-            hipLaunchKernelGGL(k_ba_build, dim3(nwin), dim3(kBlock), (size_t)cap, s, in, ctx->ba_ws, d, cam,
-                               first_end, first_valid));
-  const int np = 6 * (ctx->cfg.ba_window - 1);
-  const size_t shm = (size_t)8 * (np * np + np);
-  FVO_TIMED(ctx, KN_BA_SOLVE, s,
-            hipLaunchKernelGGL(k_ba_solve, dim3(nwin), dim3(kBlock), shm, s, in, ctx->ba_ws, d, cam, first_end, iters,
-                               BaOut{Tout, stats}));
+            hipLaunchKernelGGL(k_ba_build, dim3(nwin), dim3(kBlock), (size_t)cap, s, in, ws, d, first_end, first_valid));
+  const dim3 gcu(nwin, d.NCU), gch(nwin, d.NCH), gfr(nwin, d.K - 1);
+  const size_t shl = lin_shm(d), shs = solve_shm(d.K);
+  FVO_TIMED(ctx, KN_BA_SOLVE, s, {
+    hipLaunchKernelGGL(k_ba_cost, gcu, dim3(kBlock), 0, s, in, ws, d, cam, 0);
+    hipLaunchKernelGGL(k_ba_setcost, dim3(nwin), dim3(64), 0, s, ws, d, 1);
+    for (int it = 0; it < iters; ++it) {
+      if (it == iters / 2 && iters >= 2) {  // outlier rejection, then the cost of the kept set
+        hipLaunchKernelGGL(k_ba_cost, gcu, dim3(kBlock), 0, s, in, ws, d, cam, 1);
+        hipLaunchKernelGGL(k_ba_setcost, dim3(nwin), dim3(64), 0, s, ws, d, 0);
+      }
+      hipLaunchKernelGGL(k_ba_pp, gfr, dim3(kBlock), 0, s, in, ws, d, cam);
+      hipLaunchKernelGGL(k_ba_lin, gch, dim3(kBlock), shl, s, in, ws, d, cam);
+      hipLaunchKernelGGL(k_ba_solve, dim3(nwin), dim3(kBlock), shs, s, ws, d);
+      hipLaunchKernelGGL(k_ba_upd, gcu, dim3(kBlock), 0, s, in, ws, d, cam);
+      hipLaunchKernelGGL(k_ba_accept, dim3(nwin), dim3(64), 0, s, ws, d);
+    }
+    hipLaunchKernelGGL(k_ba_final, dim3(nwin), dim3(64), 0, s, Trel, ws, d, first_end, Tout, stats);
+  });
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }
