@@ -7,10 +7,13 @@
 Workload (BASELINE.json configs[1]): 960x600 synthetic forest stereo along the 1018_00
 ground-truth path, ORB nfeatures=1000, cross-checked BF-Hamming matching (left and the
 reference's unused right matches), StereoSGBM-3way (96 disparities), back-projection,
-PnP-RANSAC(+LM) — stereo_slam.py:232-306 per frame.  A step = one batch of B consecutive
-frames of the rank's own sequence (seed = rank), inputs resident in HBM before timing.
-Multi-GPU: one sequence per GPU, no data-path collective (weak scaling); the only
-collectives are the timing barrier and the max-over-ranks reduction.
+PnP-RANSAC(+LM) — stereo_slam.py:232-306 per frame — then the local BA over the window
+of the last K = 10 frames of every frame (north_star "extract+match+local-BA").  A step =
+one batch of B consecutive frames of the rank's own sequence (seed = rank), inputs
+resident in HBM before timing.
+Multi-GPU: one sequence per GPU (weak scaling); the data-path collective is the per-step
+map exchange (RCCL all-gather of the step's refined poses and the latest keyframe
+window's landmarks, ~100 KB per rank), plus the timing barrier / max-over-ranks.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement for the roofline definition.
 """
@@ -141,8 +144,17 @@ def main():
     fe.prime(L_all[0], R_all[0])
     Lb, Rb = L_all[1:].contiguous(), R_all[1:].contiguous()
 
+    map_exchange = dist is not None and args.ba_window > 0
+    if map_exchange:
+        from forest_slam_amd import dist as fdist
+        lm_out = (torch.empty((int(fe.ctx.cfg.ba_max_landmarks), 3), dtype=torch.float64, device=dev),
+                  torch.empty((1,), dtype=torch.int32, device=dev))
+
     def step():
-        fe.step(Lb, Rb)
+        T, _ = fe.step(Lb, Rb)
+        if map_exchange:  # the multi-sequence map: refined poses + latest keyframe window (RCCL)
+            xyz, cnt = fe.ctx.ba_landmarks(B - 1, out=lm_out)
+            fdist.exchange_window_map(T, xyz, cnt)
 
     for _ in range(max(args.warmup, 1)):
         step()
@@ -226,7 +238,8 @@ def main():
             "data": "synthetic: ray-cast forest stereo along the 1018_00 GT path (seed = rank), "
                     "BotanicGarden bag not available",
             "config": {"workload": "stereo VO front end, configs[1]: 960x600, ORB nfeatures=1000, "
-                                   "BF-Hamming xcheck (L+R), SGBM-3way 96 disp, back-projection, PnP-RANSAC",
+                                   "BF-Hamming xcheck (L+R), SGBM-3way 96 disp, back-projection, PnP-RANSAC"
+                                   + (f", local BA K={args.ba_window}" if args.ba_window else ""),
                        "frames_per_step_per_gpu": B, "width": W, "height": H, "nfeatures": args.nfeatures,
                        "local_ba": (f"window K={args.ba_window} per frame, 10 LM iterations (fvo_ba_windows)"
                                     if args.ba_window else "off"),

@@ -52,6 +52,7 @@ SIGNATURES = {
     "fvo_keypoint_stereo": (ctypes.c_int, [_P, _P, _P, _P, _I, _I, _P, ctypes.c_double, _P, _P]),
     "fvo_ba_windows": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, ctypes.c_double, _P, _I, _I,
                                       _P, _P, _P]),
+    "fvo_ba_landmarks": (ctypes.c_int, [_P, _I, _P, _P, _P]),
     "fvo_test_retain_best": (ctypes.c_int, [_P, _P, _I, _I, _P, _P, _P]),
     "fvo_debug_buffer": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     "fvo_kernel_count": (ctypes.c_int, []),
@@ -276,6 +277,17 @@ class Context:
                                           float(baseline), isig, nl, int(iterations), _ptr(Tout), _ptr(stats),
                                           _stream(self.device)))
         return Tout, stats
+
+    def ba_landmarks(self, window: int, out=None):
+        """Refined landmarks of one window of the last ba_windows call (device tensors,
+        no host sync): (xyz f64[ba_max_landmarks,3], count i32[1])."""
+        if out is None:
+            xyz = torch.empty((int(self.cfg.ba_max_landmarks), 3), dtype=torch.float64, device=self.device)
+            cnt = torch.empty((1,), dtype=torch.int32, device=self.device)
+        else:
+            xyz, cnt = out
+        self._check(self.L.fvo_ba_landmarks(self.h, int(window), _ptr(xyz), _ptr(cnt), _stream(self.device)))
+        return xyz, cnt
 
     def debug_buffer(self, which: int) -> torch.Tensor:
         """Host copy (u8 CPU tensor) of an internal workspace buffer (fvo_debug_buffer)."""

@@ -747,6 +747,16 @@ __global__ void k_ba_final(const double* __restrict__ Trel, void* ws, BaDims dm,
   st[5] = (double)S->acc;
 }
 
+// copy of one window's current landmark estimate (keyframe map export)
+__global__ void k_ba_export(void* ws, BaDims dm, int wi, double* __restrict__ xyz, int32_t* __restrict__ count) {
+  const BaWin v = view(ws, dm, wi);
+  const BaState* S = v.st;
+  const int L = S->active ? S->L : 0;
+  const double* X = cur_X(v, S);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *count = L;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * L; i += gridDim.x * blockDim.x) xyz[i] = X[i];
+}
+
 BaDims make_dims(const fvo_ctx* ctx) {
   const fvo_config& c = ctx->cfg;
   BaDims d{};
@@ -854,6 +864,14 @@ int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* mat
     }
     hipLaunchKernelGGL(k_ba_final, dim3(nwin), dim3(64), 0, s, Trel, ws, d, first_end, Tout, stats);
   });
+  FVO_LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+int ba_export_run(fvo_ctx* ctx, int window, double* xyz, int32_t* count, hipStream_t s) {
+  if (window < 0 || window >= ctx->cfg.max_batch) return fvo_fail(ctx, "ba: window index out of range");
+  const BaDims d = make_dims(ctx);
+  hipLaunchKernelGGL(k_ba_export, dim3(32), dim3(256), 0, s, ctx->ba_ws, d, window, xyz, count);
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }

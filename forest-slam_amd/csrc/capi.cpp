@@ -202,6 +202,12 @@ int fvo_ba_windows(fvo_ctx* c, const float* keypoints, const int32_t* n_keypoint
                 first_valid, K, baseline, inv_sigma2, n_levels, iterations, T_out, stats, (hipStream_t)stream);
 }
 
+int fvo_ba_landmarks(fvo_ctx* c, int32_t window, double* xyz, int32_t* count, fvo_stream stream) {
+  if (check_batch(c, 1, FVO_STAGE_BA)) return -1;
+  if (!xyz || !count) return fvo_fail(c, "null pointer argument");
+  return ba_export_run(c, window, xyz, count, (hipStream_t)stream);
+}
+
 int fvo_kernel_count(void) { return KN_COUNT; }
 
 const char* fvo_kernel_name(int id) {

@@ -144,6 +144,7 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
             int32_t* status, uint8_t* inliers, hipStream_t s);
 
 int ba_init(fvo_ctx* ctx);
+int ba_export_run(fvo_ctx* ctx, int window, double* xyz, int32_t* count, hipStream_t s);
 int ba_stereo_run(fvo_ctx* ctx, const int16_t* disp, const float* kp, const int32_t* nkp, int batch, int cap,
                   const double* K, double baseline, float* stereo, hipStream_t s);
 int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* matches, const int32_t* nmatch,

@@ -54,6 +54,22 @@ def gather_relative_poses(T_local: torch.Tensor, status_local: torch.Tensor, n_p
     return T, S
 
 
+def exchange_window_map(T_step: torch.Tensor, lm_xyz: torch.Tensor, lm_count: torch.Tensor, group=None):
+    """The per-step map exchange of the multi-sequence run: every rank's
+    BA-refined relative poses of the step (f64 [B,4,4]) and its latest window's landmarks
+    (f64 [Lmax,3] + i32 [1] count, fixed size) are all-gathered over RCCL.  Fixed shapes and
+    device-side counts: no host synchronisation, the collectives queue behind the step's
+    kernels.  Returns (T [world,B,4,4], xyz [world,Lmax,3], counts [world,1])."""
+    world = dist.get_world_size(group)
+    outT = [torch.empty_like(T_step) for _ in range(world)]
+    outX = [torch.empty_like(lm_xyz) for _ in range(world)]
+    outC = [torch.empty_like(lm_count) for _ in range(world)]
+    dist.all_gather(outT, T_step.contiguous(), group=group)
+    dist.all_gather(outX, lm_xyz.contiguous(), group=group)
+    dist.all_gather(outC, lm_count.contiguous(), group=group)
+    return torch.stack(outT), torch.stack(outX), torch.stack(outC)
+
+
 def allgather_keyframes(poses: torch.Tensor, landmarks: torch.Tensor, group=None):
     """Exchange each rank's window keyframe poses (f32 [K,7]) and active landmarks
     (f32 [L_r,3], variable L_r) -> lists indexed by rank."""

@@ -171,6 +171,11 @@ int fvo_ba_windows(fvo_ctx* ctx, const float* keypoints, const int32_t* n_keypoi
                    double baseline, const double* inv_sigma2, int32_t n_levels, int32_t iterations,
                    double* T_out, double* stats, fvo_stream stream);
 
+/* Refined landmarks of BA window `window` of the most recent fvo_ba_windows call (the
+ * keyframe map a rank shares with the others): xyz [ba_max_landmarks][3] f64
+ * in the window's first-camera frame, count [1] i32.  Device-side, no host sync. */
+int fvo_ba_landmarks(fvo_ctx* ctx, int32_t window, double* xyz, int32_t* count, fvo_stream stream);
+
 /* Test hook: KeyPointsFilter::retainBest on `n` float responses (device memory) with the
  * product's selection kernel.  idx_out [n] receives the surviving original indices in
  * OpenCV's output order, *n_out the survivor count.  Allocates (stream-ordered). */

@@ -87,6 +87,26 @@ def test_gpu_ba_matches_oracle_clean():
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_gpu_ba_landmark_export():
+    """fvo_ba_landmarks: the refined landmarks of a window, as the oracle's X."""
+    from forest_slam_amd import _lib
+    p = ba_synth.clean_problem(n=6, seed=2, n_pts=800)
+    cap = p["kp"].shape[1]
+    ctx = _lib.Context(64, 64, max_batch=2, stages=_lib.STAGE_BA, kp_capacity=cap, ba_window=6)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    ctx.ba_windows(t(p["kp"]), t(p["nkp"]), t(p["matches"]), t(p["nmatch"]), t(p["stereo"]), t(p["T_rel"]), 4, 2, 0,
+                   p["K"], p["B"], iterations=10)
+    xyz, cnt = ctx.ba_landmarks(1)
+    torch.cuda.synchronize()
+    kps, matches, st, rel = ba_synth.oracle_lists(p, 0, 5)
+    ref = _ba_ref().ba_window(kps, matches, st, rel, p["K"], p["B"], iters=10)
+    n = int(cnt.item())
+    assert n == len(ref["X"])
+    assert np.abs(xyz[:n].cpu().numpy() - ref["X"]).max() < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
 def test_gpu_ba_sliding_windows_and_outliers():
     """12 frames, windows ending at frames 2..11 (the first ones shorter than K), outlier
     matches handled by the Huber weights."""

@@ -31,7 +31,11 @@ def _worker(rank, world, port, n_pairs, out):
     s, e = fd.frame_shard(n_pairs, rank, world)
     T, S = fd.gather_relative_poses(torch.from_numpy(allT[s - 1:e - 1]), torch.from_numpy(allS[s - 1:e - 1]), n_pairs)
     poses, lms = fd.allgather_keyframes(torch.full((10, 7), float(rank)), torch.ones((rank + 2, 3)) * rank)
-    out[rank] = (T, S, [p[0, 0].item() for p in poses], [l.shape[0] for l in lms])
+    Tw, Xw, Cw = fd.exchange_window_map(torch.full((4, 4, 4), float(rank), dtype=torch.float64),
+                                        torch.full((16, 3), 10.0 + rank, dtype=torch.float64),
+                                        torch.tensor([rank + 5], dtype=torch.int32))
+    out[rank] = (T, S, [p[0, 0].item() for p in poses], [l.shape[0] for l in lms],
+                 (Tw[:, 0, 0, 0].tolist(), Xw[:, 0, 0].tolist(), Cw[:, 0].tolist()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -57,7 +61,8 @@ def test_gather_poses_two_ranks_gloo():
     allT = np.tile(np.eye(4), (n_pairs, 1, 1))
     allT[:, :3, 3] = rng.normal(0, 0.1, (n_pairs, 3))
     for r in range(2):
-        T, S, kf, nl = out[r]
+        T, S, kf, nl, wm = out[r]
+        assert wm == ([0.0, 1.0], [10.0, 11.0], [5, 6])
         assert np.array_equal(T, allT)
         assert S[3] == -1 and (S[np.arange(n_pairs) != 3] == 1).all()
         assert kf == [0.0, 1.0] and nl == [2, 3]
