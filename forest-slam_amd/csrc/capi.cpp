@@ -60,7 +60,7 @@ static void release(fvo_ctx* c) {
                   c->ncand,      c->nsel1,     c->nsel2,     c->koff,     c->scratch, c->rt.xofs,  c->rt.xc1,
                   c->rt.yofs,    c->rt.yc1,    c->umax,      c->bf_sidx,  c->bf_sdist, c->bf_tidx, c->sg_cost,
                   c->sg_L,       c->sg_V,      c->sg_raw,    c->sg_d2,    c->sg_d2c,  c->pnp_hyp,  c->pnp_good,
-                  c->pnp_sub,    c->pnp_subsets, c->pnp_models, c->pnp_state, c->ba_ws};
+                  c->pnp_sub,    c->pnp_subsets, c->pnp_models, c->pnp_state, c->ba_ws, c->keepbits};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
 }

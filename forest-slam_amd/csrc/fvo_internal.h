@@ -93,6 +93,8 @@ struct fvo_ctx {
   int32_t* pnp_good = nullptr;    // [B][max_iters] inlier counts
   void* pnp_state = nullptr;      // [B] PnpState
   int32_t pnp_max_iters = 0;
+  uint64_t* keepbits = nullptr;   // [B][total_rows][keep_words] FAST+NMS keep bits
+  int keep_words = 0;
   // local BA workspace (per window w < max_batch; strides in ba_* counts)
   void* ba_ws = nullptr;          // one allocation, carved per window (ba.hip)
   int64_t ba_win_bytes = 0;

@@ -25,23 +25,30 @@
 
 namespace {
 
-__constant__ int c_row0[FVO_MAX_LEVELS + 1];
-__constant__ int c_w[FVO_MAX_LEVELS];
-__constant__ int c_h[FVO_MAX_LEVELS];
-__constant__ long long c_off[FVO_MAX_LEVELS + 1];
-__constant__ long long c_cand_off[FVO_MAX_LEVELS + 1];
-__constant__ float c_scale[FVO_MAX_LEVELS];
-__constant__ int c_nfeat[FVO_MAX_LEVELS];
+// Pyramid geometry, passed BY VALUE to every kernel (kernarg segment, scalar loads): each
+// context has its own image size, so module-global __constant__ tables would be clobbered
+// by the next fvo_create of a different size.
+struct OrbDev {
+  int nlevels, total_rows;
+  int row0[FVO_MAX_LEVELS + 1];
+  int w[FVO_MAX_LEVELS], h[FVO_MAX_LEVELS];
+  long long off[FVO_MAX_LEVELS + 1];
+  long long cand_off[FVO_MAX_LEVELS + 1];
+  float scale[FVO_MAX_LEVELS];
+  int nfeat[FVO_MAX_LEVELS];
+  int tile0[FVO_MAX_LEVELS + 1];  // first 64x16 tile of each level (per image)
+  int ntx[FVO_MAX_LEVELS];        // tiles per row of each level
+};
 __constant__ int c_umax[20];
 __constant__ signed char c_pattern[256 * 4];
 
 constexpr int kSelThreads = 512;
 
-__device__ __forceinline__ int level_of_row(int r, int nlevels) {
+__device__ __forceinline__ int level_of_row(const OrbDev& G, int r) {
   int l = 0;
 #pragma unroll
   for (int k = 1; k < FVO_MAX_LEVELS; ++k)
-    if (k < nlevels && r >= c_row0[k]) l = k;
+    if (k < G.nlevels && r >= G.row0[k]) l = k;
   return l;
 }
 
@@ -55,17 +62,17 @@ __global__ void k_copy_level0(const uint8_t* __restrict__ img, int64_t stride, i
   pyr[b * total + (int64_t)y * W + x] = img[b * stride + (int64_t)y * pitch + x];
 }
 
-__global__ void k_resize(uint8_t* __restrict__ pyr, int64_t total, int l, const int32_t* __restrict__ xofs,
+__global__ void k_resize(const OrbDev G, uint8_t* __restrict__ pyr, int64_t total, int l, const int32_t* __restrict__ xofs,
                          const int32_t* __restrict__ xc1, const int32_t* __restrict__ yofs,
                          const int32_t* __restrict__ yc1) {
   int x = blockIdx.x * blockDim.x + threadIdx.x;
   int y = blockIdx.y;
   int b = blockIdx.z;
-  int w = c_w[l];
+  int w = G.w[l];
   if (x >= w) return;
-  int sw = c_w[l - 1], sh = c_h[l - 1];
-  const uint8_t* src = pyr + b * total + c_off[l - 1];
-  uint8_t* dst = pyr + b * total + c_off[l];
+  int sw = G.w[l - 1], sh = G.h[l - 1];
+  const uint8_t* src = pyr + b * total + G.off[l - 1];
+  uint8_t* dst = pyr + b * total + G.off[l];
   int ox = xofs[x], cx1 = xc1[x], cx0 = 256 - cx1;
   auto hrow = [&](int r) -> uint32_t {
     const uint8_t* s = src + (int64_t)r * sw;
@@ -88,91 +95,167 @@ __global__ void k_resize(uint8_t* __restrict__ pyr, int64_t total, int l, const 
 __constant__ int c_cdx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 __constant__ int c_cdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 
-__global__ void k_fast_score(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ score, int64_t total, int nlevels,
-                             int thr) {
-  int r = blockIdx.y;
-  int l = level_of_row(r, nlevels);
-  int y = r - c_row0[l];
-  int x = blockIdx.x * blockDim.x + threadIdx.x;
-  int w = c_w[l], h = c_h[l];
-  if (x >= w) return;
-  int b = blockIdx.z;
-  const uint8_t* im = pyr + b * total + c_off[l];
-  uint8_t* sc = score + b * total + c_off[l];
-  int out = 0;
-  if (x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
-    int v = im[(int64_t)y * w + x];
-    int p[16];
-    unsigned bright = 0, dark = 0;
+// ------------------------------------------------------------------ FAST + NMS (tiled)
+// One block per 64 x 16 tile of a level: the image patch (tile + 4-px apron) is staged in
+// LDS; the FAST test runs on the tile + 1-px halo, the positions that pass are packed into
+// an LDS list so cornerScore<16> runs on dense lanes (textured frames make ~80 % of waves
+// contain a corner, so per-pixel scoring ran the score code on nearly every wave); then the
+// strict 3x3 NMS + border filter of the tile is evaluated from the LDS score tile.  Output:
+// the full score map (debug / tests), one keep bit per pixel (a 64-bit word per tile row)
+// and per-row keep counts.
+constexpr int kTW = 64, kTH = 16;
+constexpr int kFW = kTW + 2, kFH = kTH + 2;     // FAST region (NMS halo)
+constexpr int kIW = kTW + 8, kIH = kTH + 8;     // image patch (FAST radius 3 + halo)
+
+__device__ __forceinline__ int tile_level(const OrbDev& G, int t) {
+  int l = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      p[k] = im[(int64_t)(y + c_cdy[k]) * w + x + c_cdx[k]];
-      bright |= (unsigned)(p[k] > v + thr) << k;
-      dark |= (unsigned)(p[k] < v - thr) << k;
-    }
-    auto has9 = [](unsigned m) {
-      unsigned mm = m | (m << 16);
-      unsigned c = mm;
-#pragma unroll
-      for (int j = 1; j <= 8; ++j) c &= mm >> j;
-      return (c & 0xFFFFu) != 0;
-    };
-    if (has9(bright) || has9(dark)) {
-      // cornerScore<16>: max(t, max over 9-arcs of min(v-p), max over 9-arcs of min(p-v)) - 1
-      int a0 = thr, b0 = thr;
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        int mn = 1 << 20, mx = 1 << 20;
-#pragma unroll
-        for (int j = 0; j < 9; ++j) {
-          int d = v - p[(s + j) & 15];
-          mn = min(mn, d);
-          mx = min(mx, -d);
-        }
-        a0 = max(a0, mn);
-        b0 = max(b0, mx);
-      }
-      out = max(a0, b0) - 1;
-    }
-  }
-  sc[(int64_t)y * w + x] = (uint8_t)out;
+  for (int k = 1; k < FVO_MAX_LEVELS; ++k)
+    if (k < G.nlevels && t >= G.tile0[k]) l = k;
+  return l;
 }
 
-__device__ __forceinline__ bool nms_keep(const uint8_t* sc, int w, int x, int y) {
-  const uint8_t* p = sc + (int64_t)y * w + x;
-  int s = p[0];
-  if (!s) return false;
-  return s > p[-w - 1] && s > p[-w] && s > p[-w + 1] && s > p[-1] && s > p[1] && s > p[w - 1] && s > p[w] &&
-         s > p[w + 1];
-}
-
-__global__ void k_nms_count(const uint8_t* __restrict__ score, int32_t* __restrict__ rowcnt, int64_t total,
-                            int total_rows, int nlevels, int edge) {
-  int r = blockIdx.x;
-  int b = blockIdx.y;
-  int l = level_of_row(r, nlevels);
-  int y = r - c_row0[l];
-  int w = c_w[l], h = c_h[l];
-  __shared__ int s_part[16];
-  int cnt = 0;
-  if (y >= edge && y < h - edge) {
-    const uint8_t* sc = score + b * total + c_off[l];
-    for (int x = edge + (int)threadIdx.x; x < w - edge; x += blockDim.x) cnt += nms_keep(sc, w, x, y);
+__global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t* __restrict__ pyr,
+                                                  uint8_t* __restrict__ score, uint64_t* __restrict__ keep,
+                                                  int32_t* __restrict__ rowcnt, int64_t total, int thr, int edge,
+                                                  int kw) {
+  __shared__ uint8_t s_img[kIH][kIW];
+  __shared__ uint8_t s_sc[kFH][kFW];
+  __shared__ uint16_t s_list[kFH * kFW];
+  __shared__ int s_n;
+  const int b = blockIdx.y, t = blockIdx.x;
+  const int l = tile_level(G, t);
+  const int lt = t - G.tile0[l];
+  const int tx = lt % G.ntx[l], ty = lt / G.ntx[l];
+  const int x0 = tx * kTW, y0 = ty * kTH;
+  const int w = G.w[l], h = G.h[l];
+  const uint8_t* im = pyr + b * total + G.off[l];
+  for (int i = threadIdx.x; i < kIH * kIW; i += 256) {
+    const int r = i / kIW, c = i % kIW;
+    const int y = min(max(y0 - 4 + r, 0), h - 1), x = min(max(x0 - 4 + c, 0), w - 1);
+    s_img[r][c] = im[(int64_t)y * w + x];
   }
-  cnt = wave_sum(cnt);
-  if (wave_lane() == 0) s_part[threadIdx.x >> 6] = cnt;
+  for (int i = threadIdx.x; i < kFH * kFW; i += 256) (&s_sc[0][0])[i] = 0;
+  if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += s_part[i];
-    rowcnt[(int64_t)b * total_rows + r] = t;
+  // FAST-9 test on the tile + halo; positions that pass go to the list
+  for (int i0 = 0; i0 < kFH * kFW; i0 += 256) {  // uniform trip count: ballots see whole waves
+    const int i = i0 + threadIdx.x;
+    const int r = i / kFW, c = i % kFW;
+    const int y = y0 - 1 + r, x = x0 - 1 + c;
+    bool corner = false;
+    if (i < kFH * kFW && x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
+      const int v = s_img[r + 3][c + 3];
+      unsigned bright = 0, dark = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int p = s_img[r + 3 + c_cdy[k]][c + 3 + c_cdx[k]];
+        bright |= (unsigned)(p > v + thr) << k;
+        dark |= (unsigned)(p < v - thr) << k;
+      }
+      auto has9 = [](unsigned m) {
+        unsigned mm = m | (m << 16);
+        unsigned cc = mm;
+#pragma unroll
+        for (int j = 1; j <= 8; ++j) cc &= mm >> j;
+        return (cc & 0xFFFFu) != 0;
+      };
+      corner = has9(bright) || has9(dark);
+    }
+    const unsigned long long m = __ballot(corner);
+    int base = 0;
+    if ((threadIdx.x & 63) == 0 && m) base = atomicAdd(&s_n, __popcll(m));
+    base = __shfl(base, 0, 64);
+    if (corner) s_list[base + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1ull))] = (uint16_t)i;
+  }
+  __syncthreads();
+  // cornerScore<16>: max(t, max over 9-arcs of min(v-p), max over 9-arcs of min(p-v)) - 1
+  const int nc = s_n;
+  for (int j = threadIdx.x; j < nc; j += 256) {
+    const int i = s_list[j];
+    const int r = i / kFW, c = i % kFW;
+    const int v = s_img[r + 3][c + 3];
+    int p[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) p[k] = s_img[r + 3 + c_cdy[k]][c + 3 + c_cdx[k]];
+    int a0 = thr, b0 = thr;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      int mn = 1 << 20, mx = 1 << 20;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        const int d = v - p[(s + q) & 15];
+        mn = min(mn, d);
+        mx = min(mx, -d);
+      }
+      a0 = max(a0, mn);
+      b0 = max(b0, mx);
+    }
+    s_sc[r][c] = (uint8_t)(max(a0, b0) - 1);
+  }
+  __syncthreads();
+  // NMS + border filter of the tile; one wave row = 64 pixels = one keep word
+  const int c = threadIdx.x & 63;
+  const int x = x0 + c;
+  for (int rr = threadIdx.x >> 6; rr < kTH; rr += 4) {
+    const int y = y0 + rr;
+    if (y >= h) break;  // uniform per wave
+    const int s = s_sc[rr + 1][c + 1];
+    bool k = false;
+    if (x < w) {
+      score[b * total + G.off[l] + (int64_t)y * w + x] = (uint8_t)s;
+      k = s && x >= edge && x < w - edge && y >= edge && y < h - edge && s > s_sc[rr][c] && s > s_sc[rr][c + 1] &&
+          s > s_sc[rr][c + 2] && s > s_sc[rr + 1][c] && s > s_sc[rr + 1][c + 2] && s > s_sc[rr + 2][c] &&
+          s > s_sc[rr + 2][c + 1] && s > s_sc[rr + 2][c + 2];
+    }
+    const unsigned long long m = __ballot(k);
+    if (c == 0) {
+      const int grow = G.row0[l] + y;
+      keep[((int64_t)b * G.total_rows + grow) * kw + tx] = m;
+      if (m) atomicAdd(&rowcnt[(int64_t)b * G.total_rows + grow], __popcll(m));
+    }
   }
 }
 
-__global__ void k_row_scan(const int32_t* __restrict__ rowcnt, int32_t* __restrict__ rowoff,
+// ordered (row-major) compaction of the kept pixels: one wave per row
+__global__ __launch_bounds__(64) void k_keep_compact(const OrbDev G, const uint8_t* __restrict__ score,
+                                                     const uint64_t* __restrict__ keep,
+                                                     const int32_t* __restrict__ rowoff, uint32_t* __restrict__ cand,
+                                                     int64_t total, int64_t cand_total, int edge, int kw) {
+  const int r = blockIdx.x, b = blockIdx.y;
+  const int l = level_of_row(G, r);
+  const int y = r - G.row0[l];
+  const int w = G.w[l], h = G.h[l];
+  if (y < edge || y >= h - edge) return;
+  const int lane = threadIdx.x, ntx = G.ntx[l];
+  const uint64_t* kr = keep + ((int64_t)b * G.total_rows + r) * kw;
+  const unsigned long long word = lane < ntx ? kr[lane] : 0ull;
+  const int cnt = __popcll(word);
+  int inc = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  const int pre_lane = inc - cnt;
+  const int base = rowoff[(int64_t)b * G.total_rows + r];
+  const uint8_t* sc = score + b * total + G.off[l] + (int64_t)y * w;
+  uint32_t* out = cand + b * cand_total + G.cand_off[l];
+  for (int j = 0; j < ntx; ++j) {
+    const unsigned long long wj = __shfl(word, j, 64);
+    const int pj = __shfl(pre_lane, j, 64);
+    if ((wj >> lane) & 1ull) {
+      const int x = 64 * j + lane;
+      out[base + pj + __popcll(wj & ((1ull << lane) - 1ull))] =
+          ((uint32_t)sc[x] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+    }
+  }
+}
+
+__global__ void k_row_scan(const OrbDev G, const int32_t* __restrict__ rowcnt, int32_t* __restrict__ rowoff,
                            int32_t* __restrict__ ncand, int total_rows, int nlevels) {
   int l = blockIdx.x, b = blockIdx.y;
-  int r0 = c_row0[l], h = c_h[l];
+  int r0 = G.row0[l], h = G.h[l];
   const int32_t* rc = rowcnt + (int64_t)b * total_rows + r0;
   int32_t* ro = rowoff + (int64_t)b * total_rows + r0;
   __shared__ int s_w[16];
@@ -201,43 +284,6 @@ __global__ void k_row_scan(const int32_t* __restrict__ rowcnt, int32_t* __restri
     __syncthreads();
   }
   if (threadIdx.x == 0) ncand[b * nlevels + l] = s_carry;
-}
-
-__global__ void k_nms_compact(const uint8_t* __restrict__ score, const int32_t* __restrict__ rowoff,
-                              uint32_t* __restrict__ cand, int64_t total, int64_t cand_total, int total_rows,
-                              int nlevels, int edge) {
-  int r = blockIdx.x;
-  int b = blockIdx.y;
-  int l = level_of_row(r, nlevels);
-  int y = r - c_row0[l];
-  int w = c_w[l], h = c_h[l];
-  if (y < edge || y >= h - edge) return;
-  const uint8_t* sc = score + b * total + c_off[l];
-  uint32_t* out = cand + b * cand_total + c_cand_off[l];
-  __shared__ int s_w[16];
-  __shared__ int s_carry;
-  if (threadIdx.x == 0) s_carry = rowoff[(int64_t)b * total_rows + r];
-  __syncthreads();
-  for (int base = edge; base < w - edge; base += blockDim.x) {
-    int x = base + threadIdx.x;
-    bool k = x < w - edge && nms_keep(sc, w, x, y);
-    unsigned long long m = __ballot(k);
-    int pre = __popcll(m & ((1ull << wave_lane()) - 1ull));
-    if (wave_lane() == 0) s_w[threadIdx.x >> 6] = __popcll(m);
-    __syncthreads();
-    int wpre = 0, tot = 0;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
-      if (i < (int)(threadIdx.x >> 6)) wpre += s_w[i];
-      tot += s_w[i];
-    }
-    if (k) {
-      uint32_t s = sc[(int64_t)y * w + x];
-      out[s_carry + wpre + pre] = (s << 24) | ((uint32_t)y << 12) | (uint32_t)x;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) s_carry += tot;
-    __syncthreads();
-  }
 }
 
 // ------------------------------------------------------------------ retainBest
@@ -458,32 +504,32 @@ __device__ int select_block(SelShared& sh, typename E::T* a, int n, int keep, in
 }
 
 template <class E>
-__global__ __launch_bounds__(kSelThreads) void k_select(typename E::T* __restrict__ arr,
+__global__ __launch_bounds__(kSelThreads) void k_select(const OrbDev G, typename E::T* __restrict__ arr,
                                                         const int32_t* __restrict__ nin, int32_t* __restrict__ nout,
                                                         int32_t* __restrict__ scratch, int64_t scratch_per,
                                                         int64_t cand_total, int nlevels, int keep_mult) {
   int l = blockIdx.x, b = blockIdx.y;
   __shared__ SelShared sh;
-  typename E::T* a = arr + b * cand_total + c_cand_off[l];
+  typename E::T* a = arr + b * cand_total + G.cand_off[l];
   int n = nin[b * nlevels + l];
   int* SA = scratch + (int64_t)(b * nlevels + l) * scratch_per;
   int* SB = SA + scratch_per / 2;
-  int r = select_block<E>(sh, a, n, keep_mult * c_nfeat[l], SA, SB);
+  int r = select_block<E>(sh, a, n, keep_mult * G.nfeat[l], SA, SB);
   if (threadIdx.x == 0) nout[b * nlevels + l] = r;
 }
 
 // ------------------------------------------------------------------ Harris
-__global__ void k_harris(const uint8_t* __restrict__ pyr, const uint32_t* __restrict__ cand,
+__global__ void k_harris(const OrbDev G, const uint8_t* __restrict__ pyr, const uint32_t* __restrict__ cand,
                          const int32_t* __restrict__ nsel, uint64_t* __restrict__ hel, int64_t total,
                          int64_t cand_total, int nlevels) {
   int l = blockIdx.y, b = blockIdx.z;
   int n = nsel[b * nlevels + l];
   int wpb = blockDim.x >> 6;
   int lane = wave_lane();
-  const uint8_t* im = pyr + b * total + c_off[l];
-  int w = c_w[l];
-  const uint32_t* cin = cand + b * cand_total + c_cand_off[l];
-  uint64_t* hout = hel + b * cand_total + c_cand_off[l];
+  const uint8_t* im = pyr + b * total + G.off[l];
+  int w = G.w[l];
+  const uint32_t* cin = cand + b * cand_total + G.cand_off[l];
+  uint64_t* hout = hel + b * cand_total + G.cand_off[l];
   for (int i = blockIdx.x * wpb + (threadIdx.x >> 6); i < n; i += gridDim.x * wpb) {
     uint32_t e = cin[i];
     int x0 = e & 0xFFF, y0 = (e >> 12) & 0xFFF;
@@ -540,16 +586,16 @@ __device__ __forceinline__ float fast_atan2_deg(float y, float x) {
   return a;
 }
 
-__global__ void k_angle(const uint8_t* __restrict__ pyr, const uint64_t* __restrict__ hel,
+__global__ void k_angle(const OrbDev G, const uint8_t* __restrict__ pyr, const uint64_t* __restrict__ hel,
                         const int32_t* __restrict__ nsel2, const int32_t* __restrict__ koff, float* __restrict__ kp,
                         int64_t total, int64_t cand_total, int nlevels, int cap, int patch) {
   int l = blockIdx.y, b = blockIdx.z;
   int n = nsel2[b * nlevels + l];
   int base = koff[b * (nlevels + 1) + l];
   int wpb = blockDim.x >> 6, lane = wave_lane();
-  const uint8_t* im = pyr + b * total + c_off[l];
-  int w = c_w[l];
-  const uint64_t* hin = hel + b * cand_total + c_cand_off[l];
+  const uint8_t* im = pyr + b * total + G.off[l];
+  int w = G.w[l];
+  const uint64_t* hin = hel + b * cand_total + G.cand_off[l];
   const int half = patch / 2;
   for (int i = blockIdx.x * wpb + (threadIdx.x >> 6); i < n; i += gridDim.x * wpb) {
     if (base + i >= cap) break;
@@ -573,7 +619,7 @@ __global__ void k_angle(const uint8_t* __restrict__ pyr, const uint64_t* __restr
     m10 = wave_sum(m10);
     m01 = wave_sum(m01);
     if (lane == 0) {
-      float s = c_scale[l];
+      float s = G.scale[l];
       float* o = kp + ((int64_t)b * cap + base + i) * FVO_KP_STRIDE;
       o[0] = (float)x0 * s;
       o[1] = (float)y0 * s;
@@ -588,6 +634,10 @@ __global__ void k_angle(const uint8_t* __restrict__ pyr, const uint64_t* __restr
 }
 
 // ------------------------------------------------------------------ Gaussian blur
+// 7x7 sigma-2 fixed-point kernel [18 34 49 55 49 34 18] (x) itself, REFLECT_101, on 64 x 16
+// tiles: the patch + 3-px apron is staged in LDS, the horizontal pass keeps exact integer
+// row sums in LDS, the vertical pass rounds once (the integer result is the separable
+// 8-bit path's, any summation order).
 __constant__ int c_gk[7] = {18, 34, 49, 55, 49, 34, 18};
 
 __device__ __forceinline__ int reflect101(int i, int n) {
@@ -595,33 +645,46 @@ __device__ __forceinline__ int reflect101(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
-__global__ void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, int64_t total, int nlevels) {
-  int r = blockIdx.y;
-  int l = level_of_row(r, nlevels);
-  int y = r - c_row0[l];
-  int x = blockIdx.x * blockDim.x + threadIdx.x;
-  int w = c_w[l], h = c_h[l];
-  if (x >= w) return;
-  int b = blockIdx.z;
-  const uint8_t* im = pyr + b * total + c_off[l];
-  int xs[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) xs[k] = reflect101(x + k - 3, w);
-  int s = 0;
-#pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    const uint8_t* row = im + (int64_t)reflect101(y + j - 3, h) * w;
+__global__ __launch_bounds__(256) void k_blur(const OrbDev G, const uint8_t* __restrict__ pyr,
+                                              uint8_t* __restrict__ blur, int64_t total) {
+  constexpr int BW = kTW + 6, BH = kTH + 6;
+  __shared__ uint8_t s_img[BH][BW];
+  __shared__ int s_rs[BH][kTW];
+  const int b = blockIdx.y, t = blockIdx.x;
+  const int l = tile_level(G, t);
+  const int lt = t - G.tile0[l];
+  const int tx = lt % G.ntx[l], ty = lt / G.ntx[l];
+  const int x0 = tx * kTW, y0 = ty * kTH;
+  const int w = G.w[l], h = G.h[l];
+  const uint8_t* im = pyr + b * total + G.off[l];
+  for (int i = threadIdx.x; i < BH * BW; i += 256) {
+    const int r = i / BW, c = i % BW;
+    const int y = reflect101(min(y0 - 3 + r, h - 1 + (h - 1)), h), x = reflect101(min(x0 - 3 + c, 2 * (w - 1)), w);
+    s_img[r][c] = im[(int64_t)y * w + x];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < BH * kTW; i += 256) {
+    const int r = i / kTW, c = i % kTW;
     int rs = 0;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) rs += c_gk[k] * row[xs[k]];
-    s += c_gk[j] * rs;
+    for (int k = 0; k < 7; ++k) rs += c_gk[k] * s_img[r][c + k];
+    s_rs[r][c] = rs;
   }
-  int q = (s + 32767 + ((s >> 16) & 1)) >> 16;  // round half to even
-  blur[b * total + c_off[l] + (int64_t)y * w + x] = (uint8_t)min(q, 255);
+  __syncthreads();
+  const int c = threadIdx.x & 63, x = x0 + c;
+  for (int rr = threadIdx.x >> 6; rr < kTH; rr += 4) {
+    const int y = y0 + rr;
+    if (y >= h || x >= w) continue;
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) s += c_gk[j] * s_rs[rr + j][c];
+    const int q = (s + 32767 + ((s >> 16) & 1)) >> 16;  // round half to even
+    blur[b * total + G.off[l] + (int64_t)y * w + x] = (uint8_t)min(q, 255);
+  }
 }
 
 // ------------------------------------------------------------------ rBRIEF
-__global__ void k_brief(const uint8_t* __restrict__ blur, const float* __restrict__ kp, const int32_t* __restrict__ counts,
+__global__ void k_brief(const OrbDev G, const uint8_t* __restrict__ blur, const float* __restrict__ kp, const int32_t* __restrict__ counts,
                         uint8_t* __restrict__ desc, int64_t total, int cap) {
   int b = blockIdx.y;
   int n = counts[b];
@@ -630,13 +693,13 @@ __global__ void k_brief(const uint8_t* __restrict__ blur, const float* __restric
   for (int j = blockIdx.x * wpb + (threadIdx.x >> 6); j < n; j += gridDim.x * wpb) {
     const float* k = kp + ((int64_t)b * cap + j) * FVO_KP_STRIDE;
     int l = (int)k[5];
-    float scale = 1.f / c_scale[l];
+    float scale = 1.f / G.scale[l];
     float angle = k[3];
     angle *= (float)(3.14159265358979323846 / 180.f);
     float a = (float)cos((double)angle), bb = (float)sin((double)angle);
     int cy = (int)rintf(k[1] * scale), cx = (int)rintf(k[0] * scale);
-    int w = c_w[l];
-    const uint8_t* c = blur + b * total + c_off[l] + (int64_t)cy * w + cx;
+    int w = G.w[l];
+    const uint8_t* c = blur + b * total + G.off[l] + (int64_t)cy * w + cx;
     unsigned long long words[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -758,15 +821,7 @@ int orb_init(fvo_ctx* ctx) {
     ++v0;
   }
 
-  long long offs[FVO_MAX_LEVELS + 1], coffs[FVO_MAX_LEVELS + 1];
-  for (int l = 0; l <= c.nlevels; ++l) { offs[l] = g.off[l]; coffs[l] = g.cand_off[l]; }
-  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_row0), g.row0, sizeof(int) * (c.nlevels + 1)));
-  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_w), g.w, sizeof(int) * c.nlevels));
-  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_h), g.h, sizeof(int) * c.nlevels));
-  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_off), offs, sizeof(long long) * (c.nlevels + 1)));
-  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_cand_off), coffs, sizeof(long long) * (c.nlevels + 1)));
-  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_scale), g.scale, sizeof(float) * c.nlevels));
-  FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_nfeat), g.nfeat, sizeof(int) * c.nlevels));
+  // size-independent tables only: the geometry travels by value (OrbDev)
   FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax.data(), sizeof(int) * 20));
   FVO_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), FVO_ORB_PATTERN, sizeof(FVO_ORB_PATTERN)));
 
@@ -782,8 +837,37 @@ int orb_init(fvo_ctx* ctx) {
       (rc = fvo_alloc(ctx, &ctx->koff, B * (c.nlevels + 1))) ||
       (rc = fvo_alloc(ctx, &ctx->scratch, B * c.nlevels * ctx->scratch_per)))
     return rc;
+  ctx->keep_words = (g.w[0] + kTW - 1) / kTW;
+  if (ctx->keep_words > 64) return fvo_fail(ctx, "ORB: image wider than 4096 px");
+  if ((rc = fvo_alloc(ctx, &ctx->keepbits, B * g.total_rows * ctx->keep_words))) return rc;
   return 0;
 }
+
+namespace {
+OrbDev make_dev(const OrbGeom& g) {
+  OrbDev G{};
+  G.nlevels = g.nlevels;
+  G.total_rows = g.total_rows;
+  int t = 0;
+  for (int l = 0; l < g.nlevels; ++l) {
+    G.row0[l] = g.row0[l];
+    G.w[l] = g.w[l];
+    G.h[l] = g.h[l];
+    G.off[l] = g.off[l];
+    G.cand_off[l] = g.cand_off[l];
+    G.scale[l] = g.scale[l];
+    G.nfeat[l] = g.nfeat[l];
+    G.ntx[l] = (g.w[l] + kTW - 1) / kTW;
+    G.tile0[l] = t;
+    t += G.ntx[l] * ((g.h[l] + kTH - 1) / kTH);
+  }
+  G.row0[g.nlevels] = g.row0[g.nlevels];
+  G.off[g.nlevels] = g.off[g.nlevels];
+  G.cand_off[g.nlevels] = g.cand_off[g.nlevels];
+  G.tile0[g.nlevels] = t;
+  return G;
+}
+}  // namespace
 
 int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride, int pitch, float* kp, uint8_t* desc,
             int32_t* counts, int cap, hipStream_t s) {
@@ -793,32 +877,32 @@ int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride
   const int W = c.width, H = c.height;
   const int64_t total = g.total_px;
   const int thr = std::min(std::max(c.fast_threshold, 0), 255);
+  const OrbDev G = make_dev(g);
+  const int ntiles = G.tile0[L];
   FVO_TIMED(ctx, KN_ORB_COPY, s, hipLaunchKernelGGL(k_copy_level0, dim3((W + 255) / 256, H, batch), dim3(256), 0, s, images, image_stride, pitch,
                      ctx->pyr, total, W, H));
   for (int l = 1; l < L; ++l)
-    FVO_TIMED(ctx, KN_ORB_RESIZE, s, hipLaunchKernelGGL(k_resize, dim3((g.w[l] + 255) / 256, g.h[l], batch), dim3(256), 0, s, ctx->pyr, total, l,
+    FVO_TIMED(ctx, KN_ORB_RESIZE, s, hipLaunchKernelGGL(k_resize, dim3((g.w[l] + 255) / 256, g.h[l], batch), dim3(256), 0, s, G, ctx->pyr, total, l,
                        ctx->rt.xofs + ctx->rt.xoff[l], ctx->rt.xc1 + ctx->rt.xoff[l], ctx->rt.yofs + ctx->rt.yoff[l],
                        ctx->rt.yc1 + ctx->rt.yoff[l]));
-  FVO_TIMED(ctx, KN_ORB_FAST, s, hipLaunchKernelGGL(k_fast_score, dim3((W + 255) / 256, g.total_rows, batch), dim3(256), 0, s, ctx->pyr, ctx->score,
-                     total, L, thr));
-  FVO_TIMED(ctx, KN_ORB_NMS_COUNT, s, hipLaunchKernelGGL(k_nms_count, dim3(g.total_rows, batch), dim3(256), 0, s, ctx->score, ctx->rowcnt, total,
-                     g.total_rows, L, c.edge_threshold));
-  FVO_TIMED(ctx, KN_ORB_ROW_SCAN, s, hipLaunchKernelGGL(k_row_scan, dim3(L, batch), dim3(256), 0, s, ctx->rowcnt, ctx->rowoff, ctx->ncand, g.total_rows,
+  FVO_HIP(ctx, hipMemsetAsync(ctx->rowcnt, 0, sizeof(int32_t) * (size_t)batch * g.total_rows, s));
+  FVO_TIMED(ctx, KN_ORB_FAST, s, hipLaunchKernelGGL(k_fast_nms, dim3(ntiles, batch), dim3(256), 0, s, G, ctx->pyr, ctx->score,
+                     ctx->keepbits, ctx->rowcnt, total, thr, c.edge_threshold, ctx->keep_words));
+  FVO_TIMED(ctx, KN_ORB_ROW_SCAN, s, hipLaunchKernelGGL(k_row_scan, dim3(L, batch), dim3(256), 0, s, G, ctx->rowcnt, ctx->rowoff, ctx->ncand, g.total_rows,
                      L));
-  FVO_TIMED(ctx, KN_ORB_COMPACT, s, hipLaunchKernelGGL(k_nms_compact, dim3(g.total_rows, batch), dim3(256), 0, s, ctx->score, ctx->rowoff, ctx->cand,
-                     total, g.cand_total, g.total_rows, L, c.edge_threshold));
-  FVO_TIMED(ctx, KN_ORB_SELECT1, s, hipLaunchKernelGGL(k_select<ElemFast>, dim3(L, batch), dim3(kSelThreads), 0, s, ctx->cand, ctx->ncand, ctx->nsel1,
+  FVO_TIMED(ctx, KN_ORB_COMPACT, s, hipLaunchKernelGGL(k_keep_compact, dim3(g.total_rows, batch), dim3(64), 0, s, G, ctx->score, ctx->keepbits,
+                     ctx->rowoff, ctx->cand, total, g.cand_total, c.edge_threshold, ctx->keep_words));
+  FVO_TIMED(ctx, KN_ORB_SELECT1, s, hipLaunchKernelGGL(k_select<ElemFast>, dim3(L, batch), dim3(kSelThreads), 0, s, G, ctx->cand, ctx->ncand, ctx->nsel1,
                      ctx->scratch, ctx->scratch_per, g.cand_total, L, 2));
-  FVO_TIMED(ctx, KN_ORB_HARRIS, s, hipLaunchKernelGGL(k_harris, dim3(32, L, batch), dim3(256), 0, s, ctx->pyr, ctx->cand, ctx->nsel1, ctx->hel, total,
+  FVO_TIMED(ctx, KN_ORB_HARRIS, s, hipLaunchKernelGGL(k_harris, dim3(32, L, batch), dim3(256), 0, s, G, ctx->pyr, ctx->cand, ctx->nsel1, ctx->hel, total,
                      g.cand_total, L));
-  FVO_TIMED(ctx, KN_ORB_SELECT2, s, hipLaunchKernelGGL(k_select<ElemHarris>, dim3(L, batch), dim3(kSelThreads), 0, s, ctx->hel, ctx->nsel1, ctx->nsel2,
+  FVO_TIMED(ctx, KN_ORB_SELECT2, s, hipLaunchKernelGGL(k_select<ElemHarris>, dim3(L, batch), dim3(kSelThreads), 0, s, G, ctx->hel, ctx->nsel1, ctx->nsel2,
                      ctx->scratch, ctx->scratch_per, g.cand_total, L, 1));
   FVO_TIMED(ctx, KN_ORB_OFFSETS, s, hipLaunchKernelGGL(k_offsets, dim3((batch + 63) / 64), dim3(64), 0, s, ctx->nsel2, ctx->koff, counts, batch, L, cap));
-  FVO_TIMED(ctx, KN_ORB_ANGLE, s, hipLaunchKernelGGL(k_angle, dim3(16, L, batch), dim3(256), 0, s, ctx->pyr, ctx->hel, ctx->nsel2, ctx->koff, kp,
+  FVO_TIMED(ctx, KN_ORB_ANGLE, s, hipLaunchKernelGGL(k_angle, dim3(16, L, batch), dim3(256), 0, s, G, ctx->pyr, ctx->hel, ctx->nsel2, ctx->koff, kp,
                      total, g.cand_total, L, cap, c.patch_size));
-  FVO_TIMED(ctx, KN_ORB_BLUR, s, hipLaunchKernelGGL(k_blur, dim3((W + 255) / 256, g.total_rows, batch), dim3(256), 0, s, ctx->pyr, ctx->blur, total,
-                     L));
-  FVO_TIMED(ctx, KN_ORB_BRIEF, s, hipLaunchKernelGGL(k_brief, dim3(64, batch), dim3(256), 0, s, ctx->blur, kp, counts, desc, total, cap));
+  FVO_TIMED(ctx, KN_ORB_BLUR, s, hipLaunchKernelGGL(k_blur, dim3(ntiles, batch), dim3(256), 0, s, G, ctx->pyr, ctx->blur, total));
+  FVO_TIMED(ctx, KN_ORB_BRIEF, s, hipLaunchKernelGGL(k_brief, dim3(64, batch), dim3(256), 0, s, G, ctx->blur, kp, counts, desc, total, cap));
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }
