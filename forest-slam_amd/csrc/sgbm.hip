@@ -236,6 +236,209 @@ __global__ __launch_bounds__(64) void k_sg_vert(const uint16_t* __restrict__ hsu
   }
 }
 
+// ------------------------------------------------------------------ fused cost + vertical pass
+// One block (4 waves) per (64 columns, stripe, pair); quad of lanes per column as in
+// k_sg_vert.  Per new hsum row (the row entering the 7-row window) the block stages the 3
+// image rows of its column range in LDS (left: 70 px, right: 70 + D - 1 px, +2 apron),
+// derives the (x-Sobel, intensity) channel words and their BT min/max, evaluates the packed
+// BT pixel cost of its 70 x D cells into LDS and box-sums 7 columns per lane.  The window's
+// 8 hsum rows are a shift register in VGPRs, so the hsum volume never goes to HBM.  The next
+// row's image bytes are fetched before the current row is processed.  Same integer
+// arithmetic as k_sg_hsum + k_sg_vert (order-independent sums).
+constexpr int kCB = 64;           // columns per block
+constexpr int kCX = kCB + 6;      // pixel-cost columns (7-wide box apron)
+
+template <int D>
+__global__ __launch_bounds__(256) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
+                                                    int64_t stride, int pitch, SgParams p, uint16_t* __restrict__ Cvol,
+                                                    uint16_t* __restrict__ Vvol) {
+  constexpr int DQ = D / 4, PQ = DQ / 2, NV4 = DQ / 8;
+  constexpr int NRC = kCX + D - 1;          // right-image core pixels
+  constexpr int NLI = kCX + 4, NRI = NRC + 4;  // staged pixels per image row (core + 2 each side)
+  constexpr int NIMG = 3 * (NLI + NRI);     // staged bytes per hsum row
+  constexpr int PER = (NIMG + 255) / 256;   // staged bytes per thread
+  __shared__ uint8_t sImg[3][NLI + NRI];
+  __shared__ uint32_t sCh[kCX + 2 + NRC + 2];                       // (Sobel, intensity), L then R
+  __shared__ uint32_t sW[3][kCX + NRC];                            // u, BT min, BT max, L then R
+  __shared__ __attribute__((aligned(16))) uint16_t sPC[kCX][D];    // pixel cost
+  const int tid = threadIdx.x, lane = tid & 63, q = lane & 3;
+  const int col = (tid >> 6) * 16 + (lane >> 2);  // 0..63
+  const int c0 = blockIdx.x * kCB;
+  const int s = blockIdx.y, b = blockIdx.z;
+  const int H = p.H, W = p.W;
+  const int start = max(min(s * p.ss - p.ov, H), 0);
+  const int end = min((s + 1) * p.ss, H);
+  const int first_out = min(s * p.ss, H);
+  if (start >= end) return;
+  const uint8_t* Lb = Limg + b * stride;
+  const uint8_t* Rb = Rimg + b * stride;
+  const int xl0 = max(c0 - 3, 0) + p.minX1;                    // first left core pixel
+  const int xl1 = min(c0 + kCB + 2, p.width1 - 1) + p.minX1;   // last left core pixel
+  const int nl = xl1 - xl0 + 1;                                // <= kCX
+  const int xr0 = xl0 - (D - 1) - p.minD;                      // first right core pixel (>= 1)
+  const int nr = nl + D - 1;                                   // <= NRC
+  const int ft = p.ftzero;
+  auto clip = [ft](int v) { return min(max(v, -ft), ft) + ft; };
+
+  // image bytes of hsum row r (rows r-1, r, r+1, clamped): thread-private prefetch slots
+  uint8_t pre[PER];
+  auto fetch = [&](int r) {
+    const int rows[3] = {r > 0 ? r - 1 : r, r, r < H - 1 ? r + 1 : r};
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + 256 * k;
+      uint8_t v = 0;
+      if (i < NIMG) {
+        const int rr = i / (NLI + NRI), j = i % (NLI + NRI);
+        if (j < NLI) v = Lb[(int64_t)rows[rr] * pitch + min(max(xl0 - 2 + j, 0), W - 1)];
+        else v = Rb[(int64_t)rows[rr] * pitch + min(max(xr0 - 2 + (j - NLI), 0), W - 1)];
+      }
+      pre[k] = v;
+    }
+  };
+  // hsum row from the staged bytes -> acc (this lane's column and disparity run)
+  auto hs_row = [&](uint32_t* acc) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + 256 * k;
+      if (i < NIMG) (&sImg[0][0])[i] = pre[k];
+    }
+    __syncthreads();
+    // channel words at core-1 .. core+1 of both images; borders (x < 1, x >= W-1) read ftzero
+    for (int j = tid; j < (nl + 2) + (nr + 2); j += 256) {
+      const bool left = j < nl + 2;
+      const int k = left ? j : j - (nl + 2);
+      const int x = (left ? xl0 : xr0) - 1 + k;
+      const uint8_t* r0 = &sImg[0][left ? 0 : NLI];
+      const uint8_t* r1 = &sImg[1][left ? 0 : NLI];
+      const uint8_t* r2 = &sImg[2][left ? 0 : NLI];
+      const int jj = k + 1;
+      uint32_t wv = (uint32_t)clip(0) * 0x10001u;
+      if (x >= 1 && x < W - 1) {
+        const int sb = (r1[jj + 1] - r1[jj - 1]) * 2 + r0[jj + 1] - r0[jj - 1] + r2[jj + 1] - r2[jj - 1];
+        wv = (uint32_t)clip(sb) | ((uint32_t)r1[jj] << 16);
+      }
+      sCh[left ? k : (kCX + 2) + k] = wv;
+    }
+    __syncthreads();
+    // BT words: u, min(u, (u+ul)/2, (u+ur)/2), max(...); at x = 0 / W-1 the half is u itself
+    for (int j = tid; j < nl + nr; j += 256) {
+      const bool left = j < nl;
+      const int k = left ? j : j - nl;
+      const int x = left ? xl0 + k : xr0 + k;
+      const uint32_t* ch = left ? sCh : sCh + (kCX + 2);
+      const u16x2 u = as_v(ch[k + 1]);
+      u16x2 hl = (u + as_v(ch[k])) >> 1, hr = (u + as_v(ch[k + 2])) >> 1;
+      if (x == 0) hl = u;
+      if (x == W - 1) hr = u;
+      const int o = left ? k : kCX + k;
+      sW[0][o] = as_u(u);
+      sW[1][o] = as_u(vmin(vmin(hl, hr), u));
+      sW[2][o] = as_u(__builtin_elementwise_max(__builtin_elementwise_max(hl, hr), u));
+    }
+    __syncthreads();
+    // pixel costs of the kCX (clamped) columns x D disparities, 8 disparities per task
+    for (int task = tid; task < kCX * (D / 8); task += 256) {
+      const int i = task / (D / 8), d0 = (task % (D / 8)) * 8;
+      const int x1c = min(max(c0 - 3 + i, 0), p.width1 - 1);
+      const int kl = x1c + p.minX1 - xl0;
+      const u16x2 u = as_v(sW[0][kl]), u0 = as_v(sW[1][kl]), u1 = as_v(sW[2][kl]);
+      uint32_t out[4];
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        const int kr = kCX + kl + (D - 1) - (d0 + h);
+        const u16x2 v = as_v(sW[0][kr]), v0 = as_v(sW[1][kr]), v1 = as_v(sW[2][kr]);
+        const u16x2 cA = __builtin_elementwise_max(__builtin_elementwise_sub_sat(u, v1), __builtin_elementwise_sub_sat(v0, u));
+        const u16x2 cB = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, u1), __builtin_elementwise_sub_sat(u0, v));
+        const uint32_t m = as_u(vmin(cA, cB));
+        const uint32_t cst = (m & 0xFFFFu) + (m >> 18);
+        if (h & 1) out[h >> 1] |= cst << 16; else out[h >> 1] = cst;
+      }
+      *reinterpret_cast<uint4*>(&sPC[i][d0]) = make_uint4(out[0], out[1], out[2], out[3]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PQ; ++k) acc[k] = 0;
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+      const uint4* src = reinterpret_cast<const uint4*>(&sPC[col + t][q * DQ]);
+#pragma unroll
+      for (int k = 0; k < NV4; ++k) {
+        const uint4 w4 = src[k];
+        acc[4 * k] = as_u(as_v(acc[4 * k]) + as_v(w4.x));
+        acc[4 * k + 1] = as_u(as_v(acc[4 * k + 1]) + as_v(w4.y));
+        acc[4 * k + 2] = as_u(as_v(acc[4 * k + 2]) + as_v(w4.z));
+        acc[4 * k + 3] = as_u(as_v(acc[4 * k + 3]) + as_v(w4.w));
+      }
+    }
+    __syncthreads();  // sImg / sPC are rewritten by the next row
+  };
+
+  // window shift register: win[k] = hsum(clamp(y - 3 + k)), k = 0..6, for the output row y
+  uint32_t win[7][PQ], crun[PQ], st[PQ];
+  fetch(start);
+  hs_row(win[6]);
+  for (int r = start + 1; r <= start + 3; ++r) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+#pragma unroll
+      for (int j = 0; j < PQ; ++j) win[k][j] = win[k + 1][j];
+    if (r <= H - 1) {  // rows past H-1 clamp to H-1 (win[6] keeps it)
+      fetch(r);
+      hs_row(win[6]);
+    }
+  }
+  // win[3..6] = hs(start..start+3 clamped); rows above start clamp to start
+  if (start + 4 <= H - 1) fetch(start + 4);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int j = 0; j < PQ; ++j) win[k][j] = win[3][j];
+#pragma unroll
+  for (int j = 0; j < PQ; ++j) {
+    u16x2 a = as_v(win[0][j]) + as_v(win[1][j]) + as_v(win[2][j]) + as_v(win[3][j]);
+    a = a + as_v(win[4][j]) + as_v(win[5][j]) + as_v(win[6][j]);
+    crun[j] = as_u(a);
+  }
+#pragma unroll
+  for (int k = 0; k < PQ; ++k) st[k] = 0;
+  uint32_t minPrev = 0;
+  const u16x2 P1 = splat(p.P1);
+  const int x1 = c0 + col;
+  const int64_t plane = (int64_t)p.width1 * D;
+  const int64_t colofs = (int64_t)b * H * plane + (int64_t)x1 * D + q * DQ;
+  for (int y = start; y < end; ++y) {
+    if (y > start) {  // window [y-3, y+3] clamped to [start, H-1]: out clamp(y-4), in clamp(y+3)
+      uint32_t nw[PQ];
+      if (y + 3 <= H - 1) {
+        hs_row(nw);
+        if (y + 4 <= H - 1) fetch(y + 4);
+      } else {
+#pragma unroll
+        for (int j = 0; j < PQ; ++j) nw[j] = win[6][j];
+      }
+#pragma unroll
+      for (int j = 0; j < PQ; ++j) crun[j] = as_u(as_v(crun[j]) - as_v(win[0][j]) + as_v(nw[j]));
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+#pragma unroll
+        for (int j = 0; j < PQ; ++j) win[k][j] = win[k + 1][j];
+#pragma unroll
+      for (int j = 0; j < PQ; ++j) win[6][j] = nw[j];
+    }
+    minPrev = hstep<PQ>(st, crun, q, P1, minPrev, p.P2);
+    if (y >= first_out && x1 < p.width1) {
+      uint4* cp = reinterpret_cast<uint4*>(Cvol + colofs + (int64_t)y * plane);
+      uint4* vp = reinterpret_cast<uint4*>(Vvol + colofs + (int64_t)y * plane);
+#pragma unroll
+      for (int i = 0; i < NV4; ++i) {
+        cp[i] = make_uint4(crun[4 * i], crun[4 * i + 1], crun[4 * i + 2], crun[4 * i + 3]);
+        vp[i] = make_uint4(st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3]);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ horizontal paths + WTA
 // raw / d2 / d2c are stored transposed, [x][row], so the rows of a wave are contiguous.
 template <int D>
@@ -407,16 +610,12 @@ SgParams make_params(const fvo_config& c) {
 template <int D>
 void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_t* R, int batch, int64_t stride,
                  int pitch, int16_t* disp, hipStream_t s) {
-  uint16_t* hsum = ctx->sg_cost;
   uint16_t* C = ctx->sg_L;
   uint16_t* V = ctx->sg_V;
-  uint16_t* LV = ctx->sg_cost;  // hsum is consumed by k_sg_vert before LV is written
-  const size_t shm = (size_t)24 * p.W;  // six u16x2 planes of the row
-  FVO_TIMED(ctx, KN_SG_HSUM, s,
-            hipLaunchKernelGGL(k_sg_hsum<D>, dim3((p.width1 + 2 * kSeg - 1) / (2 * kSeg), p.H, batch), dim3(2 * D),
-                               shm, s, L, R, stride, pitch, p, hsum));
-  FVO_TIMED(ctx, KN_SG_VERT, s, hipLaunchKernelGGL(k_sg_vert<D>, dim3((p.width1 + 15) / 16, p.nstripes, batch),
-                                                   dim3(64), 0, s, hsum, C, V, p));
+  uint16_t* LV = ctx->sg_cost;
+  FVO_TIMED(ctx, KN_SG_VERT, s,
+            hipLaunchKernelGGL(k_sg_costvert<D>, dim3((p.width1 + kCB - 1) / kCB, p.nstripes, batch), dim3(256), 0, s,
+                               L, R, stride, pitch, p, C, V));
   FVO_TIMED(ctx, KN_SG_HORIZ, s, hipLaunchKernelGGL(k_sg_horiz<D>, dim3((p.H + 15) / 16, batch), dim3(64), 0, s, C, V,
                                                     LV, ctx->sg_raw, ctx->sg_d2, ctx->sg_d2c, p));
   FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.H + 255) / 256, p.W, batch), dim3(256), 0, s,

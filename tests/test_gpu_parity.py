@@ -218,3 +218,18 @@ def test_frontend_matches_oracle_pipeline(oracle_mod, frames):
         assert np.array_equal(fe.P3[i, :n].cpu().numpy(), ref["P3"])
         assert ref["T"] is not None and st[i] == 1
         assert np.abs(T[i] - ref["T"]).max() <= 1e-4 * max(1.0, np.abs(ref["T"]).max())
+
+
+def test_contexts_of_different_sizes_coexist(oracle_mod):
+    """Two live contexts with different image sizes (e.g. a front end and a cv2 shim):
+    each keeps its own pyramid geometry (kernels take it by value)."""
+    from forest_slam_amd import _lib
+    import forest_slam_amd.synth as synth
+    a = synth.StereoSequence(seed=21, n_frames=1, W=320, H=200, device="cpu").frame(0)[0].numpy()
+    b = synth.StereoSequence(seed=22, n_frames=1, W=640, H=400, device="cpu").frame(0)[0].numpy()
+    ca = _lib.Context(320, 200, max_batch=1, nfeatures=300)
+    cb = _lib.Context(640, 400, max_batch=1, nfeatures=300)
+    for ctx, img in ((ca, a), (cb, b), (ca, a)):
+        (res,), _ = _orb_gpu(ctx, [img])
+        kp, d = oracle_mod.orb_detect_compute(img, 300)
+        assert np.array_equal(res[0][:, :6], kp) and np.array_equal(res[1], d)
