@@ -28,8 +28,8 @@ class FvoConfig(ctypes.Structure):
             "ba_max_obs")]
 
 
-ABI_VERSION = 2  # FVO_ABI_VERSION of include/fvo.h
-STAGE_ORB, STAGE_BF, STAGE_SGBM, STAGE_POSE, STAGE_BA = 1, 2, 4, 8, 16
+ABI_VERSION = 3  # FVO_ABI_VERSION of include/fvo.h
+STAGE_ORB, STAGE_BF, STAGE_SGBM, STAGE_POSE, STAGE_BA, STAGE_MONO = 1, 2, 4, 8, 16, 32
 
 # name -> (restype, argtypes); mirrors include/fvo.h
 _P = ctypes.c_void_p
@@ -53,6 +53,11 @@ SIGNATURES = {
     "fvo_ba_windows": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, ctypes.c_double, _P, _I, _I,
                                       _P, _P, _P]),
     "fvo_ba_landmarks": (ctypes.c_int, [_P, _I, _P, _P, _P]),
+    "fvo_gather_matches": (ctypes.c_int, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P]),
+    "fvo_find_essential": (ctypes.c_int, [_P, _P, _P, _P, _I, _I, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                          ctypes.c_double, ctypes.c_double, _I, _P, _P, _P, _P]),
+    "fvo_recover_pose": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, ctypes.c_double, ctypes.c_double,
+                                        ctypes.c_double, ctypes.c_double, _P, _P, _P, _P, _P]),
     "fvo_test_retain_best": (ctypes.c_int, [_P, _P, _I, _I, _P, _P, _P]),
     "fvo_debug_buffer": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     "fvo_kernel_count": (ctypes.c_int, []),
@@ -288,6 +293,49 @@ class Context:
             xyz, cnt = out
         self._check(self.L.fvo_ba_landmarks(self.h, int(window), _ptr(xyz), _ptr(cnt), _stream(self.device)))
         return xyz, cnt
+
+    def gather_matches(self, kp0, kp1, matches, nmatch, out=None):
+        """mkpts0/mkpts1 of a BF match list (fvo_gather_matches): (p0 f32[B,cap,2], p1, n i32[B])."""
+        B, cap = matches.shape[0], matches.shape[1]
+        if out is None:
+            p0 = torch.empty((B, cap, 2), dtype=torch.float32, device=self.device)
+            p1 = torch.empty((B, cap, 2), dtype=torch.float32, device=self.device)
+            n = torch.empty((B,), dtype=torch.int32, device=self.device)
+        else:
+            p0, p1, n = out
+        self._check(self.L.fvo_gather_matches(self.h, _ptr(kp0), _ptr(kp1), _ptr(matches), _ptr(nmatch), B, cap,
+                                              _ptr(p0), _ptr(p1), _ptr(n), _stream(self.device)))
+        return p0, p1, n
+
+    def find_essential(self, p0, p1, n, focal, pp, prob=0.999, threshold=1.0, max_iters=1000, out=None):
+        """findEssentialMat(RANSAC) on [B] point sets: (E f64[B,3,3], mask u8[B,cap], status i32[B])."""
+        B, cap = p0.shape[0], p0.shape[1]
+        if out is None:
+            E = torch.empty((B, 3, 3), dtype=torch.float64, device=self.device)
+            mask = torch.empty((B, cap), dtype=torch.uint8, device=self.device)
+            st = torch.empty((B,), dtype=torch.int32, device=self.device)
+        else:
+            E, mask, st = out
+        self._check(self.L.fvo_find_essential(self.h, _ptr(p0.contiguous()), _ptr(p1.contiguous()), _ptr(n), B, cap,
+                                              float(focal), float(pp[0]), float(pp[1]), float(prob), float(threshold),
+                                              int(max_iters), _ptr(E), _ptr(mask), _ptr(st), _stream(self.device)))
+        return E, mask, st
+
+    def recover_pose(self, E, p0, p1, n, focal, pp, e_status=None, distance_thresh=50.0, out=None):
+        """recoverPose on [B] frames: (R f64[B,3,3], t f64[B,3], T f64[B,4,4], n_good i32[B])."""
+        B, cap = p0.shape[0], p0.shape[1]
+        if out is None:
+            R = torch.empty((B, 3, 3), dtype=torch.float64, device=self.device)
+            t = torch.empty((B, 3), dtype=torch.float64, device=self.device)
+            T = torch.empty((B, 4, 4), dtype=torch.float64, device=self.device)
+            g = torch.empty((B,), dtype=torch.int32, device=self.device)
+        else:
+            R, t, T, g = out
+        self._check(self.L.fvo_recover_pose(self.h, _ptr(E.contiguous()), _ptr(e_status), _ptr(p0.contiguous()),
+                                            _ptr(p1.contiguous()), _ptr(n), B, cap, float(focal), float(pp[0]),
+                                            float(pp[1]), float(distance_thresh), _ptr(R), _ptr(t), _ptr(T), _ptr(g),
+                                            _stream(self.device)))
+        return R, t, T, g
 
     def debug_buffer(self, which: int) -> torch.Tensor:
         """Host copy (u8 CPU tensor) of an internal workspace buffer (fvo_debug_buffer)."""

@@ -60,7 +60,8 @@ static void release(fvo_ctx* c) {
                   c->ncand,      c->nsel1,     c->nsel2,     c->koff,     c->scratch, c->rt.xofs,  c->rt.xc1,
                   c->rt.yofs,    c->rt.yc1,    c->umax,      c->bf_sidx,  c->bf_sdist, c->bf_tidx, c->sg_cost,
                   c->sg_L,       c->sg_V,      c->sg_raw,    c->sg_d2,    c->sg_d2c,  c->pnp_hyp,  c->pnp_good,
-                  c->pnp_sub,    c->pnp_subsets, c->pnp_models, c->pnp_state, c->ba_ws, c->keepbits};
+                  c->pnp_sub,    c->pnp_subsets, c->pnp_models, c->pnp_state, c->ba_ws, c->keepbits,
+                  c->em_x, c->em_subsets, c->em_models, c->em_good, c->em_nmod, c->em_state};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
 }
@@ -86,7 +87,8 @@ int fvo_create(int device, const fvo_config* cfg, fvo_ctx** out) {
     c->err = "image size must be at least 64x64";
     return bail(-1);
   }
-  if (!(st & FVO_STAGE_ORB) && (st & (FVO_STAGE_BF | FVO_STAGE_POSE | FVO_STAGE_BA)) && cfg->kp_capacity < 1) {
+  if (!(st & FVO_STAGE_ORB) && (st & (FVO_STAGE_BF | FVO_STAGE_POSE | FVO_STAGE_BA | FVO_STAGE_MONO)) &&
+      cfg->kp_capacity < 1) {
     c->err = "kp_capacity must be set when the ORB stage is not enabled";
     return bail(-1);
   }
@@ -94,7 +96,7 @@ int fvo_create(int device, const fvo_config* cfg, fvo_ctx** out) {
   int rc = 0;
   if (((st & FVO_STAGE_ORB) && (rc = orb_init(c))) || ((st & FVO_STAGE_BF) && (rc = bf_init(c))) ||
       ((st & FVO_STAGE_SGBM) && (rc = sgbm_init(c))) || ((st & FVO_STAGE_POSE) && (rc = pose_init(c))) ||
-      ((st & FVO_STAGE_BA) && (rc = ba_init(c))))
+      ((st & FVO_STAGE_BA) && (rc = ba_init(c))) || ((st & FVO_STAGE_MONO) && (rc = mono_init(c))))
     return bail(rc);
   *out = c;
   return 0;
@@ -208,6 +210,41 @@ int fvo_ba_landmarks(fvo_ctx* c, int32_t window, double* xyz, int32_t* count, fv
   return ba_export_run(c, window, xyz, count, (hipStream_t)stream);
 }
 
+int fvo_gather_matches(fvo_ctx* c, const float* kp0, const float* kp1, const int32_t* matches,
+                       const int32_t* n_matches, int32_t batch, int32_t cap, float* p0, float* p1, int32_t* n_points,
+                       fvo_stream stream) {
+  if (!c) return -1;
+  if (batch < 0 || batch > c->cfg.max_batch) return fvo_fail(c, "batch exceeds max_batch");
+  if (batch == 0) return 0;
+  if (!kp0 || !kp1 || !matches || !n_matches || !p0 || !p1 || !n_points) return fvo_fail(c, "null pointer argument");
+  if (cap < 1) return fvo_fail(c, "cap must be >= 1");
+  return gather_run(c, kp0, kp1, matches, n_matches, batch, cap, p0, p1, n_points, (hipStream_t)stream);
+}
+
+int fvo_find_essential(fvo_ctx* c, const float* p0, const float* p1, const int32_t* n_points, int32_t batch,
+                       int32_t cap, double focal, double cx, double cy, double prob, double threshold,
+                       int32_t max_iters, double* E, uint8_t* mask, int32_t* status, fvo_stream stream) {
+  if (check_batch(c, batch, FVO_STAGE_MONO)) return -1;
+  if (batch == 0) return 0;
+  if (!p0 || !p1 || !n_points || !E || !status) return fvo_fail(c, "null pointer argument");
+  if (cap < 1 || cap > c->kp_cap) return fvo_fail(c, "cap must be in [1, fvo_kp_capacity()]");
+  if (!(focal > 0.0)) return fvo_fail(c, "focal must be > 0");
+  return essential_run(c, p0, p1, n_points, batch, cap, focal, cx, cy, prob, threshold, max_iters, E, mask, status,
+                       (hipStream_t)stream);
+}
+
+int fvo_recover_pose(fvo_ctx* c, const double* E, const int32_t* e_status, const float* p0, const float* p1,
+                     const int32_t* n_points, int32_t batch, int32_t cap, double focal, double cx, double cy,
+                     double distance_thresh, double* R, double* t, double* T, int32_t* n_good, fvo_stream stream) {
+  if (check_batch(c, batch, FVO_STAGE_MONO)) return -1;
+  if (batch == 0) return 0;
+  if (!E || !p0 || !p1 || !n_points || !R || !t || !T || !n_good) return fvo_fail(c, "null pointer argument");
+  if (cap < 1 || cap > c->kp_cap) return fvo_fail(c, "cap must be in [1, fvo_kp_capacity()]");
+  if (!(focal > 0.0)) return fvo_fail(c, "focal must be > 0");
+  return recover_run(c, E, e_status, p0, p1, n_points, batch, cap, focal, cx, cy, distance_thresh, R, t, T, n_good,
+                     (hipStream_t)stream);
+}
+
 int fvo_kernel_count(void) { return KN_COUNT; }
 
 const char* fvo_kernel_name(int id) {
@@ -215,7 +252,7 @@ const char* fvo_kernel_name(int id) {
       "orb_copy_level0", "orb_resize", "orb_fast_score", "orb_nms_count", "orb_row_scan", "orb_nms_compact",
       "orb_select_fast", "orb_harris", "orb_select_harris", "orb_offsets", "orb_angle", "orb_blur", "orb_brief",
       "bf_argmin", "bf_finish", "sgbm_hsum", "sgbm_vert", "sgbm_horiz", "sgbm_median", "backproject",
-      "pnp_ransac", "ba_stereo", "ba_build", "ba_solve"};
+      "pnp_ransac", "ba_stereo", "ba_build", "ba_solve", "gather_matches", "essential_ransac", "recover_pose"};
   return (id >= 0 && id < KN_COUNT) ? names[id] : "";
 }
 

@@ -40,7 +40,7 @@ enum FvoKernel {
   KN_ORB_COPY, KN_ORB_RESIZE, KN_ORB_FAST, KN_ORB_NMS_COUNT, KN_ORB_ROW_SCAN, KN_ORB_COMPACT, KN_ORB_SELECT1,
   KN_ORB_HARRIS, KN_ORB_SELECT2, KN_ORB_OFFSETS, KN_ORB_ANGLE, KN_ORB_BLUR, KN_ORB_BRIEF, KN_BF_ARGMIN,
   KN_BF_FINISH, KN_SG_HSUM, KN_SG_VERT, KN_SG_HORIZ, KN_SG_MEDIAN, KN_BACKPROJECT, KN_PNP, KN_BA_STEREO,
-  KN_BA_BUILD, KN_BA_SOLVE, KN_COUNT
+  KN_BA_BUILD, KN_BA_SOLVE, KN_GATHER, KN_ESSENTIAL, KN_RECOVER, KN_COUNT
 };
 
 struct TimingRec {
@@ -98,6 +98,14 @@ struct fvo_ctx {
   // local BA workspace (per window w < max_batch; strides in ba_* counts)
   void* ba_ws = nullptr;          // one allocation, carved per window (ba.hip)
   int64_t ba_win_bytes = 0;
+  // mono (essential matrix) workspace
+  double* em_x = nullptr;         // [B][cap][4] normalised (x1, y1, x2, y2)
+  int16_t* em_subsets = nullptr;  // [B][max_iters][5]
+  double* em_models = nullptr;    // [B][max_iters][10][9] 5-point solutions
+  int32_t* em_good = nullptr;     // [B][max_iters][10] inlier counts
+  int8_t* em_nmod = nullptr;      // [B][max_iters] solutions per subset
+  void* em_state = nullptr;       // [B] EmState
+  int32_t em_max_iters = 0;
 };
 
 // Error helpers: set ctx->err and return negative status.
@@ -144,6 +152,16 @@ int backproject_run(fvo_ctx* ctx, const int16_t* disp, const float* kp0, const f
 int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts, int batch, int cap, const double* K,
             const double* dist, float reproj, double conf, int iters, double* rvec, double* tvec, double* T,
             int32_t* status, uint8_t* inliers, hipStream_t s);
+
+int mono_init(fvo_ctx* ctx);
+int gather_run(fvo_ctx* ctx, const float* kp0, const float* kp1, const int32_t* matches, const int32_t* nmatch,
+               int batch, int cap, float* p0, float* p1, int32_t* npts, hipStream_t s);
+int essential_run(fvo_ctx* ctx, const float* p0, const float* p1, const int32_t* npts, int batch, int cap,
+                  double focal, double cx, double cy, double prob, double threshold, int maxIters, double* E,
+                  uint8_t* mask, int32_t* status, hipStream_t s);
+int recover_run(fvo_ctx* ctx, const double* E, const int32_t* est, const float* p0, const float* p1,
+                const int32_t* npts, int batch, int cap, double focal, double cx, double cy, double dist, double* R,
+                double* t, double* T, int32_t* ngood, hipStream_t s);
 
 int ba_init(fvo_ctx* ctx);
 int ba_export_run(fvo_ctx* ctx, int window, double* xyz, int32_t* count, hipStream_t s);

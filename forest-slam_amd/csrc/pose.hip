@@ -19,6 +19,7 @@
 #include <cfloat>
 
 #include "fvo_internal.h"
+#include "ransac.h"
 
 namespace {
 
@@ -571,27 +572,8 @@ struct EPnPd {
   }
 };
 
-struct RNG {
-  uint64_t state;
-  __device__ unsigned next() {
-    state = (uint64_t)(unsigned)state * 4164903690u + (unsigned)(state >> 32);
-    return (unsigned)state;
-  }
-  __device__ int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a) + a); }
-};
-
-__device__ int update_num_iters(double p, double ep, int m, int maxIters) {
-  p = fmax(p, 0.);
-  p = fmin(p, 1.);
-  ep = fmax(ep, 0.);
-  ep = fmin(ep, 1.);
-  double num = fmax(1. - p, DBL_MIN);
-  double denom = 1. - pow(1. - ep, (double)m);
-  if (denom < DBL_MIN) return 0;
-  num = log(num);
-  denom = log(denom);
-  return denom >= 0 || -num >= maxIters * (-denom) ? maxIters : (int)rint(num / denom);
-}
+using fvo_rs::RNG;
+using fvo_rs::update_num_iters;
 
 __device__ __forceinline__ double wsum_d(double v) {
 #pragma unroll
@@ -836,22 +818,7 @@ __global__ void k_pnp_subsets(const int32_t* __restrict__ npts, int batch, int c
   st.n = n;
   state[b] = st;
   if (n < 6) return;
-  RNG rng{~0ull};
-  int16_t* o = sub + (int64_t)b * maxIters * 5;
-  for (int it = 0; it < maxIters; ++it) {
-    int idx[5];
-    for (int i = 0; i < 5; ++i) {
-      int j;
-      for (;;) {
-        j = rng.uniform(0, n);
-        bool dup = false;
-        for (int q = 0; q < i; ++q) dup |= idx[q] == j;
-        if (!dup) break;
-      }
-      idx[i] = j;
-      o[it * 5 + i] = (int16_t)j;
-    }
-  }
+  fvo_rs::draw_subsets(n, maxIters, sub + (int64_t)b * maxIters * 5);
 }
 
 // One lane per RANSAC iteration: EPnP on its subset (undistorted, float32-rounded

@@ -9,6 +9,9 @@ Face 1 mirrors the OpenCV calls of ros_ws/src/stereo_slam.py:
     StereoSGBM_create(...).compute(L, R)                        (:108-117)
     ok, rvec, tvec, inliers = solvePnPRansac(P, p, K, dist, ...)  (:294-295)
     R, _ = Rodrigues(rvec)                                      (:298)
+and of ros_ws/src/mono_slam.py:
+    E, mask = findEssentialMat(m0, m1, focal=, pp=, method=RANSAC, prob=0.999, threshold=1.0)  (:111)
+    _, R, t, _ = recoverPose(E, m0, m1, focal=, pp=)            (:112)
 Face 2 mirrors `feature_matcher({'image0': t0, 'image1': t1})` (:81, :210-229) with
 ORB + BF-cross-check underneath; matching_scores0 = 1 - distance/256.
 
@@ -29,6 +32,7 @@ STEREO_SGBM_MODE_SGBM = 0
 STEREO_SGBM_MODE_HH = 1
 STEREO_SGBM_MODE_SGBM_3WAY = 2
 SOLVEPNP_ITERATIVE = 0
+RANSAC = 8
 
 
 class error(RuntimeError):
@@ -261,6 +265,75 @@ def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec=Non
     idx = np.nonzero(inl[0, :n].cpu().numpy())[0].astype(np.int32).reshape(-1, 1)
     return True, rv, tv, idx
 
+
+
+_mono_cache = _CtxCache()
+
+
+def _mono_ctx(n):
+    cap = max(1024, -(-n // 1024) * 1024)
+    return cap, _mono_cache.get(cap, lambda: _lib.Context(64, 64, max_batch=1, stages=_lib.STAGE_MONO,
+                                                          kp_capacity=cap))
+
+
+def _pinhole(cameraMatrix, focal, pp, name):
+    if cameraMatrix is not None:
+        K = np.asarray(cameraMatrix, dtype=np.float64).reshape(3, 3)
+        if K[0, 0] != K[1, 1]:
+            raise NotImplementedError(f"{name}: only fx == fy camera matrices are implemented")
+        return float(K[0, 0]), (float(K[0, 2]), float(K[1, 2]))
+    return float(focal), (float(pp[0]), float(pp[1]))
+
+
+def _point_pairs(points1, points2, name):
+    p0 = np.ascontiguousarray(np.asarray(points1, dtype=np.float32).reshape(-1, 2))
+    p1 = np.ascontiguousarray(np.asarray(points2, dtype=np.float32).reshape(-1, 2))
+    if p0.shape[0] != p1.shape[0]:
+        raise error(f"{name}: point counts differ")
+    n = p0.shape[0]
+    cap, ctx = _mono_ctx(n)
+    dev = _device()
+    P0 = torch.zeros((1, cap, 2), dtype=torch.float32, device=dev)
+    P1 = torch.zeros((1, cap, 2), dtype=torch.float32, device=dev)
+    P0[0, :n] = torch.from_numpy(p0).to(dev)
+    P1[0, :n] = torch.from_numpy(p1).to(dev)
+    return n, ctx, P0, P1, torch.tensor([n], dtype=torch.int32, device=dev)
+
+
+def findEssentialMat(points1, points2, cameraMatrix=None, method=RANSAC, prob=0.999, threshold=1.0, maxIters=1000,
+                     mask=None, focal=1.0, pp=(0.0, 0.0)):
+    """cv2.findEssentialMat(points1, points2, focal=, pp=, method=RANSAC, prob=, threshold=)
+    (mono_slam.py:111) -> (E (3,3) f64, mask (n,1) u8), or (None, None) when RANSAC finds no
+    model / fewer than 5 points are given."""
+    if method != RANSAC:
+        raise NotImplementedError("findEssentialMat: only method=RANSAC is implemented")
+    f, c = _pinhole(cameraMatrix, focal, pp, "findEssentialMat")
+    n, ctx, P0, P1, cnt = _point_pairs(points1, points2, "findEssentialMat")
+    if maxIters > 1000:
+        raise NotImplementedError("findEssentialMat: maxIters > 1000")
+    E, m, st = ctx.find_essential(P0, P1, cnt, f, c, prob=float(prob), threshold=float(threshold),
+                                  max_iters=int(maxIters))
+    st = int(st[0].item())
+    if st == -2:
+        raise NotImplementedError("findEssentialMat: 5 points with several solutions (stacked E)")
+    if st != 1:
+        return None, None
+    return E[0].cpu().numpy(), m[0, :n].cpu().numpy().reshape(-1, 1)
+
+
+def recoverPose(E, points1, points2, cameraMatrix=None, R=None, t=None, focal=1.0, pp=(0.0, 0.0), mask=None):
+    """cv2.recoverPose(E, points1, points2, focal=, pp=) (mono_slam.py:112) ->
+    (n_good, R (3,3), t (3,1), mask); distanceThresh 50 as in that OpenCV overload."""
+    if mask is not None:
+        raise NotImplementedError("recoverPose: an input mask is not implemented (the reference passes none)")
+    E = np.asarray(E, dtype=np.float64)
+    if E.shape != (3, 3):
+        raise error("recoverPose: E must be 3x3")
+    f, c = _pinhole(cameraMatrix, focal, pp, "recoverPose")
+    n, ctx, P0, P1, cnt = _point_pairs(points1, points2, "recoverPose")
+    Et = torch.from_numpy(np.ascontiguousarray(E)).to(P0.device)[None]
+    Rm, tv, T, g = ctx.recover_pose(Et, P0, P1, cnt, f, c)
+    return int(g[0].item()), Rm[0].cpu().numpy(), tv[0].cpu().numpy().reshape(3, 1), None
 
 def Rodrigues(src):
     """cv2.Rodrigues for a rotation vector (3,1)/(1,3)/(3,) -> (R 3x3, jacobian 3x9), or a

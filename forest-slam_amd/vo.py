@@ -208,3 +208,107 @@ def run_sequence(frontend: StereoFrontEnd, L_all: torch.Tensor, R_all: torch.Ten
         stamps = np.arange(n, dtype=np.float64)
     rows = ev.tum_rows(np.asarray(stamps)[1:][valid], cum)
     return rows, T, st
+
+
+class MonoFrontEnd:
+    """Batched mono VO on the GPU — the ORB variant of ros_ws/src/mono_slam.py:97-118
+    (SURVEY.md §8 a16): per frame pair ORB on the current image, BF cross-check
+    previous -> current, mkpts gather (:106-108), findEssentialMat(RANSAC, 0.999, 1.0)
+    (:111), recoverPose (:112) and T = [R | t] (:114-117).  The chain (:118) is composed on
+    the host (``eval.chain``); translations are unit-norm (mono is scale-free).
+
+    ``step`` status per frame: 1 pose valid; 0 RANSAC found no model, -1 fewer than 5
+    matches, -2 five matches with several solutions — the cases where the reference's
+    cv2.recoverPose would raise; T is the identity there."""
+
+    def __init__(self, width: int, height: int, K: np.ndarray, batch: int, nfeatures: int = 500, device=None,
+                 prob: float = 0.999, threshold: float = 1.0, **params):
+        self.B = batch
+        self.K = np.asarray(K, np.float64)
+        self.focal = float(self.K[0, 0])
+        self.pp = (float(self.K[0, 2]), float(self.K[1, 2]))
+        self.prob, self.threshold = float(prob), float(threshold)
+        stages = _lib.STAGE_ORB | _lib.STAGE_BF | _lib.STAGE_MONO
+        self.ctx = _lib.Context(width, height, max_batch=batch, device=device, nfeatures=nfeatures, stages=stages,
+                                **params)
+        self.dev = self.ctx.device
+        self.cap = cap = self.ctx.kp_cap
+        B, dev = batch, self.dev
+        e = lambda shape, dt: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
+        self.kp = e((B, cap, _lib.KP_STRIDE), torch.float32)
+        self.desc = e((B, cap, _lib.DESC_BYTES), torch.uint8)
+        self.cnt = e((B,), torch.int32)
+        self.q_kp = e((B, cap, _lib.KP_STRIDE), torch.float32)
+        self.q_desc = e((B, cap, _lib.DESC_BYTES), torch.uint8)
+        self.q_cnt = e((B,), torch.int32)
+        self.matches = e((B, cap, 3), torch.int32)
+        self.nmatch = e((B,), torch.int32)
+        self.p0 = e((B, cap, 2), torch.float32)
+        self.p1 = e((B, cap, 2), torch.float32)
+        self.npts = e((B,), torch.int32)
+        self.E = e((B, 3, 3), torch.float64)
+        self.mask = e((B, cap), torch.uint8)
+        self.status = e((B,), torch.int32)
+        self.R = e((B, 3, 3), torch.float64)
+        self.t = e((B, 3), torch.float64)
+        self.T = e((B, 4, 4), torch.float64)
+        self.ngood = e((B,), torch.int32)
+        self.last_kp = e((cap, _lib.KP_STRIDE), torch.float32)
+        self.last_desc = e((cap, _lib.DESC_BYTES), torch.uint8)
+        self.last_cnt = e((1,), torch.int32)
+        self.has_prev = False
+
+    def prime(self, img0: torch.Tensor):
+        kp, desc, cnt = self.ctx.orb(img0.to(self.dev)[None])
+        self.last_kp.copy_(kp[0])
+        self.last_desc.copy_(desc[0])
+        self.last_cnt.copy_(cnt[:1])
+        self.has_prev = True
+
+    def step(self, imgs: torch.Tensor):
+        """imgs: u8 [n,H,W] device tensor of the next n <= B selected frames.  Returns
+        (T f64[n,4,4], status i32[n]) device tensors (async)."""
+        if not self.has_prev:
+            raise RuntimeError("call prime() with the first frame first")
+        n, ctx = imgs.shape[0], self.ctx
+        if n > self.B:
+            raise ValueError("more frames than the configured batch")
+        kp, desc, cnt = ctx.orb(imgs, out=(self.kp[:n], self.desc[:n], self.cnt[:n]))
+        self.q_kp[0].copy_(self.last_kp)
+        self.q_desc[0].copy_(self.last_desc)
+        self.q_cnt[0:1].copy_(self.last_cnt)
+        if n > 1:
+            self.q_kp[1:n].copy_(kp[:n - 1])
+            self.q_desc[1:n].copy_(desc[:n - 1])
+            self.q_cnt[1:n].copy_(cnt[:n - 1])
+        m, nm = ctx.bf_match(self.q_desc[:n], self.q_cnt[:n], desc, cnt, out=(self.matches[:n], self.nmatch[:n]))
+        p0, p1, npts = ctx.gather_matches(self.q_kp[:n], kp, m, nm, out=(self.p0[:n], self.p1[:n], self.npts[:n]))
+        E, _, st = ctx.find_essential(p0, p1, npts, self.focal, self.pp, self.prob, self.threshold,
+                                      out=(self.E[:n], self.mask[:n], self.status[:n]))
+        _, _, T, _ = ctx.recover_pose(E, p0, p1, npts, self.focal, self.pp, e_status=st,
+                                      out=(self.R[:n], self.t[:n], self.T[:n], self.ngood[:n]))
+        self.last_kp.copy_(kp[n - 1])
+        self.last_desc.copy_(desc[n - 1])
+        self.last_cnt.copy_(cnt[n - 1:n])
+        return T, st
+
+
+def run_mono_sequence(frontend: MonoFrontEnd, imgs: torch.Tensor, stamps=None, frame_interval: int = 1):
+    """mono_slam.py's loop over a sequence: frames with index % frame_interval == 0 form the
+    consecutive pairs (:97); returns (TUM rows, relative T, statuses)."""
+    from . import eval as ev
+    sel = np.arange(0, imgs.shape[0], frame_interval)
+    if stamps is None:
+        stamps = np.arange(imgs.shape[0], dtype=np.float64)
+    frontend.prime(imgs[sel[0]])
+    Ts, sts = [], []
+    for s in range(1, len(sel), frontend.B):
+        idx = sel[s:s + frontend.B]
+        T, st = frontend.step(imgs[torch.as_tensor(idx, device=imgs.device)])
+        Ts.append(T.cpu().numpy())
+        sts.append(st.cpu().numpy())
+    T = np.concatenate(Ts) if Ts else np.zeros((0, 4, 4))
+    st = np.concatenate(sts) if sts else np.zeros((0,), np.int32)
+    cum = ev.chain(T, np.ones(len(T), bool))
+    rows = ev.tum_rows(np.asarray(stamps)[sel[1:]], cum)
+    return rows, T, st

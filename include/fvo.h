@@ -16,6 +16,12 @@
  *                              confidence=0.99, iterationsCount=1000, SOLVEPNP_ITERATIVE)
  *                              + cv2.Rodrigues + T assembly, stereo_slam.py:292-303
  *   fvo_ba_window           <- (new) windowed bundle adjustment, no reference counterpart
+ *   fvo_gather_matches      <- mkpts0 = kpts0[valid], mkpts1 = kpts1[matches[valid]]
+ *                              mono_slam.py:106-108 (stereo_slam.py:235-238 for the BF DMatch list)
+ *   fvo_find_essential      <- cv2.findEssentialMat(mkpts0, mkpts1, focal=K0[0,0], pp=(K0[0,2], K0[1,2]),
+ *                              method=cv2.RANSAC, prob=0.999, threshold=1.0)   mono_slam.py:111
+ *   fvo_recover_pose        <- cv2.recoverPose(E, mkpts0, mkpts1, focal=, pp=) + the [R|t] matrix
+ *                              mono_slam.py:112-117
  *
  * Conventions
  *  - All array pointers are DEVICE pointers owned by the caller (e.g. torch tensors'
@@ -39,7 +45,7 @@
 extern "C" {
 #endif
 
-#define FVO_ABI_VERSION 2
+#define FVO_ABI_VERSION 3
 
 typedef struct fvo_ctx fvo_ctx;
 typedef void* fvo_stream; /* hipStream_t */
@@ -86,7 +92,8 @@ typedef struct fvo_config {
 #define FVO_STAGE_SGBM 4
 #define FVO_STAGE_POSE 8
 #define FVO_STAGE_BA 16
-#define FVO_STAGE_ALL 31
+#define FVO_STAGE_MONO 32
+#define FVO_STAGE_ALL 63
 
 /* Fill `cfg` with the reference's parameters for a width x height image. */
 void fvo_config_default(fvo_config* cfg, int32_t width, int32_t height);
@@ -175,6 +182,33 @@ int fvo_ba_windows(fvo_ctx* ctx, const float* keypoints, const int32_t* n_keypoi
  * keyframe map a rank shares with the others): xyz [ba_max_landmarks][3] f64
  * in the window's first-camera frame, count [1] i32.  Device-side, no host sync. */
 int fvo_ba_landmarks(fvo_ctx* ctx, int32_t window, double* xyz, int32_t* count, fvo_stream stream);
+
+/* Matched keypoint coordinates of `batch` frame pairs (mono_slam.py:106-108):
+ * p0[i] = kp0[matches[i].queryIdx].xy, p1[i] = kp1[matches[i].trainIdx].xy, f32 [batch][cap][2];
+ * n_points [batch] = n_matches clamped to [0, cap]. */
+int fvo_gather_matches(fvo_ctx* ctx, const float* kp0, const float* kp1, const int32_t* matches,
+                       const int32_t* n_matches, int32_t batch, int32_t cap, float* p0, float* p1, int32_t* n_points,
+                       fvo_stream stream);
+
+/* cv2.findEssentialMat(p0, p1, focal, pp, cv2.RANSAC, prob, threshold, max_iters) on `batch`
+ * frame pairs (stage FVO_STAGE_MONO; mono_slam.py:111).  5-point solver inside OpenCV's
+ * RANSAC (RNG(-1) subsets, adaptive iterations, max_iters <= 1000).
+ * E:      [batch][9] f64 row-major unit-norm essential matrix (zeros when status != 1).
+ * mask:   [batch][cap] u8 inlier mask of E (may be NULL).
+ * status: [batch] i32: 1 ok, 0 RANSAC found no model, -1 fewer than 5 points, -2 exactly 5
+ *         points with several solutions (OpenCV returns a stacked 3k x 3 E that recoverPose rejects). */
+int fvo_find_essential(fvo_ctx* ctx, const float* p0, const float* p1, const int32_t* n_points, int32_t batch,
+                       int32_t cap, double focal, double cx, double cy, double prob, double threshold,
+                       int32_t max_iters, double* E, uint8_t* mask, int32_t* status, fvo_stream stream);
+
+/* cv2.recoverPose(E, p0, p1, focal=, pp=) (distanceThresh 50 for that overload) on `batch`
+ * frame pairs, all points (the reference passes no mask, mono_slam.py:112), + T = [R|t].
+ * e_status: fvo_find_essential status (may be NULL); frames with status != 1 get R = I, t = 0,
+ *           T = I and n_good = -1 (the reference's cv2 call would raise there).
+ * R [batch][9], t [batch][3], T [batch][16] f64; n_good [batch] i32 = cheirality inliers. */
+int fvo_recover_pose(fvo_ctx* ctx, const double* E, const int32_t* e_status, const float* p0, const float* p1,
+                     const int32_t* n_points, int32_t batch, int32_t cap, double focal, double cx, double cy,
+                     double distance_thresh, double* R, double* t, double* T, int32_t* n_good, fvo_stream stream);
 
 /* Test hook: KeyPointsFilter::retainBest on `n` float responses (device memory) with the
  * product's selection kernel.  idx_out [n] receives the surviving original indices in

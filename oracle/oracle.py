@@ -52,6 +52,14 @@ def lib():
         L.ref_fast_atan2.argtypes = [ctypes.c_float, ctypes.c_float]
         L.ref_bf_match.restype = ctypes.c_int
         L.ref_solve_pnp_ransac.restype = ctypes.c_int
+        L.ref_find_essential.restype = ctypes.c_int
+        L.ref_find_essential.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                         ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int, _f64p,
+                                         _u8p, _i32p, _i32p]
+        L.ref_recover_pose.restype = ctypes.c_int
+        L.ref_recover_pose.argtypes = [_f64p, _f32p, _f32p, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_double, _f64p, _f64p]
+        L.ref_five_point.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -213,6 +221,44 @@ def solve_pnp_ransac(P3: np.ndarray, p2: np.ndarray, K: np.ndarray, dist: np.nda
                                     ctypes.c_float(reproj), ctypes.c_double(confidence), _p(rv, _f64p),
                                     _p(tv, _f64p), _p(mask, _u8p), _p(ni, _i32p), _p(bg, _i32p))
     return bool(ok), rv, tv, np.nonzero(mask[:n])[0].astype(np.int32), int(ni[0]), int(bg[0])
+
+
+def find_essential(p1: np.ndarray, p2: np.ndarray, focal: float, pp, prob: float = 0.999, threshold: float = 1.0,
+                   max_iters: int = 1000):
+    """cv2.findEssentialMat(p1, p2, focal=, pp=, RANSAC, prob, threshold) (mono_slam.py:111).
+    Returns (status, E 3x3, inlier mask u8[n], ransac_iters, ransac_inliers); status 1 ok,
+    0 RANSAC failed, -1 fewer than 5 points, -2 five points with several solutions."""
+    p1 = np.ascontiguousarray(p1, dtype=np.float32).reshape(-1, 2)
+    p2 = np.ascontiguousarray(p2, dtype=np.float32).reshape(-1, 2)
+    n = len(p1)
+    E = np.zeros(9)
+    mask = np.zeros(max(n, 1), np.uint8)
+    ni = np.zeros(1, np.int32)
+    bg = np.zeros(1, np.int32)
+    st = lib().ref_find_essential(_p(p1, _f32p), _p(p2, _f32p), n, focal, float(pp[0]), float(pp[1]), prob,
+                                  threshold, max_iters, _p(E, _f64p), _p(mask, _u8p), _p(ni, _i32p), _p(bg, _i32p))
+    return int(st), E.reshape(3, 3), mask[:n], int(ni[0]), int(bg[0])
+
+
+def recover_pose(E: np.ndarray, p1: np.ndarray, p2: np.ndarray, focal: float, pp, dist: float = 50.0):
+    """cv2.recoverPose(E, p1, p2, focal=, pp=) (mono_slam.py:112) -> (good, R 3x3, t 3)."""
+    E = np.ascontiguousarray(E, dtype=np.float64).reshape(9)
+    p1 = np.ascontiguousarray(p1, dtype=np.float32).reshape(-1, 2)
+    p2 = np.ascontiguousarray(p2, dtype=np.float32).reshape(-1, 2)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    g = lib().ref_recover_pose(_p(E, _f64p), _p(p1, _f32p), _p(p2, _f32p), len(p1), focal, float(pp[0]),
+                               float(pp[1]), dist, _p(R, _f64p), _p(t, _f64p))
+    return int(g), R.reshape(3, 3), t
+
+
+def five_point(x1: np.ndarray, x2: np.ndarray) -> np.ndarray:
+    """EMEstimatorCallback::runKernel on 5 normalised correspondences -> models [k,3,3]."""
+    x1 = np.ascontiguousarray(x1, dtype=np.float64).reshape(5, 2)
+    x2 = np.ascontiguousarray(x2, dtype=np.float64).reshape(5, 2)
+    out = np.zeros(90)
+    k = lib().ref_five_point(_p(x1, _f64p), _p(x2, _f64p), _p(out, _f64p))
+    return out[:9 * k].reshape(k, 3, 3)
 
 
 def rodrigues(rvec: np.ndarray) -> np.ndarray:

@@ -17,7 +17,7 @@ def find(d, pat):
 def ours(name):
     return any(k in name for k in ("k_sg_", "k_bf_", "k_pnp", "k_backproject", "k_brief", "k_blur", "k_angle",
                                    "k_harris", "k_select", "k_nms", "k_fast", "k_resize", "k_copy_level0",
-                                   "k_row_scan", "k_offsets"))
+                                   "k_row_scan", "k_offsets", "k_ba_", "k_em_", "k_ing_", "k_gather"))
 
 
 def short(name):

@@ -18,7 +18,8 @@ def _declared():
 def test_header_declares_reference_entry_points():
     names = _declared()
     for n in ["fvo_orb_detect_compute", "fvo_bf_match", "fvo_sgbm", "fvo_backproject", "fvo_pnp_ransac",
-              "fvo_create", "fvo_destroy", "fvo_last_error", "fvo_config_default"]:
+              "fvo_create", "fvo_destroy", "fvo_last_error", "fvo_config_default", "fvo_gather_matches",
+              "fvo_find_essential", "fvo_recover_pose"]:
         assert n in names
 
 
@@ -28,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(path)
     missing = [n for n in _declared() if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.fvo_abi_version() == 2
+    assert lib.fvo_abi_version() == 3
 
 
 def test_binding_signatures_cover_header():
@@ -46,7 +47,7 @@ def test_config_default_matches_reference_constants():
     assert abs(cfg.scale_factor - 1.2) < 1e-6
     assert (cfg.num_disparities, cfg.min_disparity, cfg.block_size, cfg.P1, cfg.P2) == (96, 0, 7, 392, 1568)
     assert cfg.sgbm_stripes == 4
-    assert cfg.stages == 31  # FVO_STAGE_ALL
+    assert cfg.stages == 63  # FVO_STAGE_ALL
     assert (cfg.ba_window, cfg.ba_max_landmarks, cfg.ba_max_obs) == (10, 4096, 32768)
 
 

@@ -52,6 +52,12 @@ def test_unsupported_parameters_are_refused():
         cv2.StereoSGBM_create(numDisparities=96, blockSize=5, mode=cv2.STEREO_SGBM_MODE_SGBM_3WAY)
     with pytest.raises(NotImplementedError):
         cv2.solvePnPRansac(np.zeros((8, 3)), np.zeros((8, 2)), np.eye(3), None, useExtrinsicGuess=True)
+    with pytest.raises(NotImplementedError):
+        cv2.findEssentialMat(np.zeros((8, 2)), np.zeros((8, 2)), focal=500.0, pp=(0, 0), method=4)
+    with pytest.raises(NotImplementedError):
+        cv2.findEssentialMat(np.zeros((8, 2)), np.zeros((8, 2)), np.diag([500.0, 501.0, 1.0]))
+    with pytest.raises(NotImplementedError):
+        cv2.recoverPose(np.eye(3), np.zeros((8, 2)), np.zeros((8, 2)), focal=500.0, mask=np.ones((8, 1), np.uint8))
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-GPU failure path")
@@ -169,3 +175,36 @@ def test_bf_shim_edge_cases(oracle_mod):
     d1 = rng.integers(0, 256, (1800, 32), dtype=np.uint8)
     got = np.array([[m.queryIdx, m.trainIdx, m.distance] for m in bf.match(d0, d1)])
     assert np.array_equal(got, oracle_mod.bf_match(d0, d1))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_reference_mono_lines_through_shims(oracle_mod):
+    """mono_slam.py:111-117 verbatim over the shims, on ORB+BF matches of two synthetic
+    frames, against the oracle."""
+    import forest_slam_amd.synth as synth
+    cv2 = _cv2()
+    seq = synth.StereoSequence(seed=12, n_frames=3, W=960, H=600, device="cpu", start=120)
+    I0, I1 = seq.frame(0)[0].numpy(), seq.frame(2)[0].numpy()
+    K0 = seq.K
+    orb = cv2.ORB_create()
+    bf = cv2.BFMatcher(cv2.NORM_HAMMING, crossCheck=True)
+    k0, d0 = orb.detectAndCompute(I0, None)
+    k1, d1 = orb.detectAndCompute(I1, None)
+    matches = bf.match(d0, d1)
+    mkpts0 = np.float32([k0[m.queryIdx].pt for m in matches])
+    mkpts1 = np.float32([k1[m.trainIdx].pt for m in matches])
+    # --- mono_slam.py:111-117
+    E, mask = cv2.findEssentialMat(mkpts0, mkpts1, focal=K0[0,0], pp=(K0[0,2], K0[1,2]), method=cv2.RANSAC, prob=0.999, threshold=1.0)
+    _, rotation, translation, _ = cv2.recoverPose(E, mkpts0, mkpts1, focal=K0[0,0], pp=(K0[0,2], K0[1,2]))
+    translation = translation.reshape(3)
+    relative_est_tf_mat = np.eye(4)
+    relative_est_tf_mat[:3, 3] = translation
+    relative_est_tf_mat[:3, :3] = rotation
+    # --- oracle
+    st, rE, rmask, _, _ = oracle_mod.find_essential(mkpts0, mkpts1, K0[0, 0], (K0[0, 2], K0[1, 2]))
+    assert st == 1
+    assert np.abs(E - rE).max() < 1e-9 and np.array_equal(mask.reshape(-1), rmask)
+    g, rR, rt = oracle_mod.recover_pose(rE, mkpts0, mkpts1, K0[0, 0], (K0[0, 2], K0[1, 2]))
+    assert np.abs(relative_est_tf_mat[:3, :3] - rR).max() < 1e-9
+    assert np.abs(relative_est_tf_mat[:3, 3] - rt).max() < 1e-9
