@@ -8,6 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -58,6 +59,7 @@ SIGNATURES = {
                                           ctypes.c_double, ctypes.c_double, _I, _P, _P, _P, _P]),
     "fvo_recover_pose": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, ctypes.c_double, ctypes.c_double,
                                         ctypes.c_double, ctypes.c_double, _P, _P, _P, _P, _P]),
+    "fvo_undistort_gray": (ctypes.c_int, [_P, _P, _I, _L, _I, _P, _P, _P, _L, _I, _P]),
     "fvo_test_retain_best": (ctypes.c_int, [_P, _P, _I, _I, _P, _P, _P]),
     "fvo_debug_buffer": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     "fvo_kernel_count": (ctypes.c_int, []),
@@ -293,6 +295,25 @@ class Context:
             xyz, cnt = out
         self._check(self.L.fvo_ba_landmarks(self.h, int(window), _ptr(xyz), _ptr(cnt), _stream(self.device)))
         return xyz, cnt
+
+    def undistort_gray(self, bgr, K, dist, out=None):
+        """cv2.undistort + cvtColor(BGR2GRAY): bgr u8 [B,H,W,3] (or [H,W,3]) -> gray u8 [B,H,W]."""
+        if bgr.dim() == 3:
+            bgr = bgr[None]
+        if bgr.dtype != torch.uint8 or bgr.shape[-1] != 3:
+            raise TypeError("bgr must be uint8 [B,H,W,3]")
+        bgr = bgr.contiguous()
+        B, H, W, _ = bgr.shape
+        if (H, W) != (self.height, self.width):
+            raise ValueError(f"context is {self.width}x{self.height}, got {W}x{H}")
+        if out is None:
+            out = torch.empty((B, H, W), dtype=torch.uint8, device=self.device)
+        Kh = (ctypes.c_double * 9)(*[float(v) for v in np.asarray(K, np.float64).reshape(-1)])
+        d = [float(v) for v in np.asarray(dist, np.float64).reshape(-1)[:5]]
+        dh = (ctypes.c_double * 5)(*(d + [0.0] * (5 - len(d))))
+        self._check(self.L.fvo_undistort_gray(self.h, _ptr(bgr), B, H * W * 3, W * 3, Kh, dh, _ptr(out), H * W, W,
+                                              _stream(self.device)))
+        return out
 
     def gather_matches(self, kp0, kp1, matches, nmatch, out=None):
         """mkpts0/mkpts1 of a BF match list (fvo_gather_matches): (p0 f32[B,cap,2], p1, n i32[B])."""

@@ -245,6 +245,19 @@ int fvo_recover_pose(fvo_ctx* c, const double* E, const int32_t* e_status, const
                      (hipStream_t)stream);
 }
 
+int fvo_undistort_gray(fvo_ctx* c, const uint8_t* bgr, int32_t batch, int64_t src_stride, int32_t src_pitch,
+                       const double* K, const double* dist, uint8_t* gray, int64_t dst_stride, int32_t dst_pitch,
+                       fvo_stream stream) {
+  if (!c) return -1;
+  if (batch < 0 || batch > c->cfg.max_batch) return fvo_fail(c, "batch exceeds max_batch");
+  if (batch == 0) return 0;
+  if (!bgr || !K || !dist || !gray) return fvo_fail(c, "null pointer argument");
+  const int W = c->cfg.width, H = c->cfg.height;
+  if (src_pitch < 3 * W || src_stride < (int64_t)src_pitch * H || dst_pitch < W || dst_stride < (int64_t)dst_pitch * H)
+    return fvo_fail(c, "bad pitch/stride");
+  return ingest_run(c, bgr, batch, src_stride, src_pitch, K, dist, gray, dst_stride, dst_pitch, (hipStream_t)stream);
+}
+
 int fvo_kernel_count(void) { return KN_COUNT; }
 
 const char* fvo_kernel_name(int id) {
@@ -252,7 +265,7 @@ const char* fvo_kernel_name(int id) {
       "orb_copy_level0", "orb_resize", "orb_fast_score", "orb_nms_count", "orb_row_scan", "orb_nms_compact",
       "orb_select_fast", "orb_harris", "orb_select_harris", "orb_offsets", "orb_angle", "orb_blur", "orb_brief",
       "bf_argmin", "bf_finish", "sgbm_hsum", "sgbm_vert", "sgbm_horiz", "sgbm_median", "backproject",
-      "pnp_ransac", "ba_stereo", "ba_build", "ba_solve", "gather_matches", "essential_ransac", "recover_pose"};
+      "pnp_ransac", "ba_stereo", "ba_build", "ba_solve", "gather_matches", "essential_ransac", "recover_pose", "ingest_undistort_gray"};
   return (id >= 0 && id < KN_COUNT) ? names[id] : "";
 }
 

@@ -40,7 +40,7 @@ enum FvoKernel {
   KN_ORB_COPY, KN_ORB_RESIZE, KN_ORB_FAST, KN_ORB_NMS_COUNT, KN_ORB_ROW_SCAN, KN_ORB_COMPACT, KN_ORB_SELECT1,
   KN_ORB_HARRIS, KN_ORB_SELECT2, KN_ORB_OFFSETS, KN_ORB_ANGLE, KN_ORB_BLUR, KN_ORB_BRIEF, KN_BF_ARGMIN,
   KN_BF_FINISH, KN_SG_HSUM, KN_SG_VERT, KN_SG_HORIZ, KN_SG_MEDIAN, KN_BACKPROJECT, KN_PNP, KN_BA_STEREO,
-  KN_BA_BUILD, KN_BA_SOLVE, KN_GATHER, KN_ESSENTIAL, KN_RECOVER, KN_COUNT
+  KN_BA_BUILD, KN_BA_SOLVE, KN_GATHER, KN_ESSENTIAL, KN_RECOVER, KN_INGEST, KN_COUNT
 };
 
 struct TimingRec {
@@ -153,6 +153,8 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
             const double* dist, float reproj, double conf, int iters, double* rvec, double* tvec, double* T,
             int32_t* status, uint8_t* inliers, hipStream_t s);
 
+int ingest_run(fvo_ctx* ctx, const uint8_t* bgr, int batch, int64_t sstride, int spitch, const double* K,
+               const double* dist, uint8_t* gray, int64_t dstride, int dpitch, hipStream_t s);
 int mono_init(fvo_ctx* ctx);
 int gather_run(fvo_ctx* ctx, const float* kp0, const float* kp1, const int32_t* matches, const int32_t* nmatch,
                int batch, int cap, float* p0, float* p1, int32_t* npts, hipStream_t s);

@@ -22,6 +22,8 @@
  *                              method=cv2.RANSAC, prob=0.999, threshold=1.0)   mono_slam.py:111
  *   fvo_recover_pose        <- cv2.recoverPose(E, mkpts0, mkpts1, focal=, pp=) + the [R|t] matrix
  *                              mono_slam.py:112-117
+ *   fvo_undistort_gray      <- cv2.cvtColor(cv2.undistort(img, K, dist), cv2.COLOR_BGR2GRAY)
+ *                              stereo_slam.py:184-186, :196-198; mono_slam.py:92-93
  *
  * Conventions
  *  - All array pointers are DEVICE pointers owned by the caller (e.g. torch tensors'
@@ -209,6 +211,16 @@ int fvo_find_essential(fvo_ctx* ctx, const float* p0, const float* p1, const int
 int fvo_recover_pose(fvo_ctx* ctx, const double* E, const int32_t* e_status, const float* p0, const float* p1,
                      const int32_t* n_points, int32_t batch, int32_t cap, double focal, double cx, double cy,
                      double distance_thresh, double* R, double* t, double* T, int32_t* n_good, fvo_stream stream);
+
+/* Image ingest of `batch` BGR8 camera images of one camera (any stage; no workspace):
+ * cv2.undistort(img, K, dist) (new camera matrix = K, INTER_LINEAR remap, BORDER_CONSTANT 0)
+ * followed by cv2.cvtColor(., COLOR_BGR2GRAY).  Image size = the context's width x height.
+ * bgr:  [batch] images, image b at bgr + b*src_stride, rows src_pitch (>= 3*width) bytes apart.
+ * K:    host double[9] row-major; dist: host double[5] (k1 k2 p1 p2 k3).
+ * gray: [batch] u8 images at gray + b*dst_stride, rows dst_pitch bytes apart. */
+int fvo_undistort_gray(fvo_ctx* ctx, const uint8_t* bgr, int32_t batch, int64_t src_stride, int32_t src_pitch,
+                       const double* K, const double* dist, uint8_t* gray, int64_t dst_stride, int32_t dst_pitch,
+                       fvo_stream stream);
 
 /* Test hook: KeyPointsFilter::retainBest on `n` float responses (device memory) with the
  * product's selection kernel.  idx_out [n] receives the surviving original indices in

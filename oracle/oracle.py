@@ -261,6 +261,27 @@ def five_point(x1: np.ndarray, x2: np.ndarray) -> np.ndarray:
     return out[:9 * k].reshape(k, 3, 3)
 
 
+def undistort_gray(bgr: np.ndarray, K: np.ndarray, dist) -> np.ndarray:
+    """cv2.cvtColor(cv2.undistort(bgr, K, dist), cv2.COLOR_BGR2GRAY) (stereo_slam.py:184-186)."""
+    bgr = np.ascontiguousarray(bgr, dtype=np.uint8)
+    H, W = bgr.shape[:2]
+    K = np.ascontiguousarray(K, dtype=np.float64).reshape(9)
+    d = np.ascontiguousarray(np.resize(np.asarray(dist, np.float64), 5))
+    out = np.zeros((H, W), np.uint8)
+    lib().ref_undistort_gray(_p(bgr, _u8p), H, W, W * 3, _p(K, _f64p), _p(d, _f64p), _p(out, _u8p))
+    return out
+
+
+def undistort_map(H: int, W: int, K: np.ndarray, dist):
+    """(map xy i16[H,W,2], fractional index u16[H,W]) of initUndistortRectifyMap(CV_16SC2)."""
+    K = np.ascontiguousarray(K, dtype=np.float64).reshape(9)
+    d = np.ascontiguousarray(np.resize(np.asarray(dist, np.float64), 5))
+    mxy = np.zeros((H, W, 2), np.int16)
+    fr = np.zeros((H, W), np.uint16)
+    lib().ref_undistort_map(H, W, _p(K, _f64p), _p(d, _f64p), _p(mxy, _i16p), _p(fr, ctypes.POINTER(ctypes.c_uint16)))
+    return mxy, fr
+
+
 def rodrigues(rvec: np.ndarray) -> np.ndarray:
     rvec = np.ascontiguousarray(rvec, dtype=np.float64).reshape(3)
     R = np.zeros(9)
