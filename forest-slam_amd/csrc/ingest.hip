@@ -40,11 +40,16 @@ __device__ __forceinline__ int round_sat(double v) {
   return v >= 2147483647.0 ? 2147483647 : (v <= -2147483648.0 ? (-2147483647 - 1) : (int)rint(v));
 }
 
+// PIX output pixels per thread.  kPinhole: K has the camera-matrix zero pattern
+// (K[1] = K[3] = K[6] = K[7] = 0, K[8] = 1), so ir[6] = ir[7] = 0 (exact zeros of the closed
+// form) and _w, hence w = 1/_w, is constant along a row: hoisted (bit-identical to the
+// per-pixel evaluation).  The k4..k6 denominator is exactly 1 and x/1.0 == x, so it is dropped.
+template <int PIX, bool kPinhole>
 __global__ __launch_bounds__(256) void k_ing_undistort_gray(const uint8_t* __restrict__ src, int64_t sstride,
                                                             int spitch, uint8_t* __restrict__ dst, int64_t dstride,
                                                             int dpitch, int W, int H, int stripe0, Lens L) {
   const int row = blockIdx.y, b = blockIdx.z;
-  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * PIX;
   if (c0 >= W) return;
   const uint8_t* S = src + b * sstride;
   const int y0 = (row / stripe0) * stripe0, i = row - y0;
@@ -56,16 +61,20 @@ __global__ __launch_bounds__(256) void k_ing_undistort_gray(const uint8_t* __res
   inv3(Ar, ir);
   const double fx = L.K[0], fy = L.K[4], u0 = L.K[2], v0 = L.K[5];
   const double bx = i * ir[1] + ir[2], by = i * ir[4] + ir[5], bw = i * ir[7] + ir[8];
-  uint32_t packed = 0;
+  const double w_row = kPinhole ? 1. / (bw + 0 * ir[6]) : 0.0;
+  uint32_t packed[PIX / 4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int k = 0; k < PIX / 4; ++k) packed[k] = 0;
+#pragma unroll
+  for (int q = 0; q < PIX; ++q) {
     const int col = c0 + q;
     if (col >= W) break;
-    double _x = bx + col * ir[0], _y = by + col * ir[3], _w = bw + col * ir[6];
-    double w = 1. / _w, x = _x * w, y = _y * w;
+    double _x = bx + col * ir[0], _y = by + col * ir[3];
+    double w = kPinhole ? w_row : 1. / (bw + col * ir[6]);
+    double x = _x * w, y = _y * w;
     double x2 = x * x, y2 = y * y;
     double r2 = x2 + y2, _2xy = 2 * x * y;
-    double kr = (1 + ((L.k3 * r2 + L.k2) * r2 + L.k1) * r2) / (1 + ((0.0 * r2 + 0.0) * r2 + 0.0) * r2);
+    double kr = (1 + ((L.k3 * r2 + L.k2) * r2 + L.k1) * r2);
     double xd = (x * kr + L.p1 * _2xy + L.p2 * (r2 + 2 * x2) + 0.0 * r2 + 0.0 * r2 * r2);
     double yd = (y * kr + L.p1 * (r2 + 2 * y2) + L.p2 * _2xy + 0.0 * r2 + 0.0 * r2 * r2);
     const int iu = round_sat((fx * xd + u0) * 32.0), iv = round_sat((fy * yd + v0) * 32.0);
@@ -87,13 +96,14 @@ __global__ __launch_bounds__(256) void k_ing_undistort_gray(const uint8_t* __res
       }
     }
     const uint32_t g = (uint32_t)((ch[0] * 1868 + ch[1] * 9617 + ch[2] * 4899 + (1 << 13)) >> 14);
-    packed |= g << (8 * q);
+    packed[q / 4] |= g << (8 * (q % 4));
   }
   uint8_t* D = dst + b * dstride + (int64_t)row * dpitch + c0;
-  if (c0 + 4 <= W && (((uintptr_t)D) & 3) == 0) {
-    *reinterpret_cast<uint32_t*>(D) = packed;
+  if (c0 + PIX <= W && (((uintptr_t)D) & 3) == 0) {
+#pragma unroll
+    for (int k = 0; k < PIX / 4; ++k) reinterpret_cast<uint32_t*>(D)[k] = packed[k];
   } else {
-    for (int q = 0; q < 4 && c0 + q < W; ++q) D[q] = (uint8_t)(packed >> (8 * q));
+    for (int q = 0; q < PIX && c0 + q < W; ++q) D[q] = (uint8_t)(packed[q / 4] >> (8 * (q % 4)));
   }
 }
 
@@ -107,9 +117,17 @@ int ingest_run(fvo_ctx* ctx, const uint8_t* bgr, int batch, int64_t sstride, int
   L.k1 = dist[0]; L.k2 = dist[1]; L.p1 = dist[2]; L.p2 = dist[3]; L.k3 = dist[4];
   int stripe0 = 4096 / (W > 1 ? W : 1);
   stripe0 = stripe0 < 1 ? 1 : (stripe0 > H ? H : stripe0);
-  dim3 grid((W + 1023) / 1024, H, batch);
-  FVO_TIMED(ctx, KN_INGEST, s, hipLaunchKernelGGL(k_ing_undistort_gray, grid, dim3(256), 0, s, bgr, sstride, spitch,
-                                                  gray, dstride, dpitch, W, H, stripe0, L));
+  constexpr int PIX = 8;
+  dim3 grid((W + 256 * PIX - 1) / (256 * PIX), H, batch);
+  const bool pinhole = K[1] == 0.0 && K[3] == 0.0 && K[6] == 0.0 && K[7] == 0.0 && K[8] == 1.0;
+  FVO_TIMED(ctx, KN_INGEST, s, {
+    if (pinhole)
+      hipLaunchKernelGGL((k_ing_undistort_gray<PIX, true>), grid, dim3(256), 0, s, bgr, sstride, spitch, gray, dstride,
+                         dpitch, W, H, stripe0, L);
+    else
+      hipLaunchKernelGGL((k_ing_undistort_gray<PIX, false>), grid, dim3(256), 0, s, bgr, sstride, spitch, gray,
+                         dstride, dpitch, W, H, stripe0, L);
+  });
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }

@@ -1,0 +1,181 @@
+"""ROS bag v2.0 I/O and the bag-driven pipelines.
+
+CPU: writer/reader round trips (uncompressed and bz2 chunks, timestamp ordering, padded
+image rows), the stereo_slam.py message-selection semantics (index % frame_interval over
+both camera topics), and gt_localisation.py restated: a bag holding the GT poses behind the
+reference's own 1018_00_Ground_Truth.txt reproduces that file.  GPU: run_stereo_bag (ingest
++ ORB/BF/SGBM/PnP) on a synthetic bag equals the oracle's pipeline on the same bytes."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, gpu_available
+
+
+def _rb():
+    from forest_slam_amd import rosbag
+    return rosbag
+
+
+def _write_small(path, compression="none"):
+    rb = _rb()
+    rng = np.random.default_rng(0)
+    imgs, poses = [], []
+    with rb.BagWriter(path, chunk_msgs=3, compression=compression) as w:
+        for i in range(5):
+            t = rb.Time(100 + i, 5000 * i)
+            img = rng.integers(0, 256, (6, 7, 3), dtype=np.uint8)
+            imgs.append((t, img))
+            w.write("/cam", rb.image_message(img, t, seq=i, frame_id="cam"), t)
+            p = rb.PoseStamped(rb.Header(i, t, "map"), rb.Pose(rb.Point(*rng.normal(size=3)),
+                                                               rb.Quaternion(*rng.normal(size=4))))
+            poses.append((t, p))
+            w.write("/pose", p, rb.Time(t.secs, t.nsecs + 1))
+    return imgs, poses
+
+
+@pytest.mark.parametrize("compression", ["none", "bz2"])
+def test_bag_round_trip(tmp_path, compression):
+    rb = _rb()
+    path = str(tmp_path / "a.bag")
+    imgs, poses = _write_small(path, compression)
+    bag = rb.Bag(path)
+    assert bag.get_message_count() == 10 and bag.get_message_count("/cam") == 5
+    msgs = list(bag.read_messages())
+    assert [m[0] for m in msgs] == ["/cam", "/pose"] * 5  # timestamp order across topics
+    got_imgs = [(t, rb.imgmsg_to_array(m)) for topic, m, t in bag.read_messages(topics=["/cam"])]
+    for (t0, a), (t1, b) in zip(imgs, got_imgs):
+        assert t0 == t1 and np.array_equal(a, b)
+    got_poses = [m for _, m, _ in bag.read_messages(topics="/pose")]
+    for (_, p), q in zip(poses, got_poses):
+        assert p == q
+    types = {c.topic: c.type for c in bag.connections.values()}
+    assert types == {"/cam": rb.IMAGE_TYPE, "/pose": rb.POSE_TYPE}
+
+
+def test_out_of_order_writes_are_read_in_time_order(tmp_path):
+    rb = _rb()
+    path = str(tmp_path / "b.bag")
+    with rb.BagWriter(path, chunk_msgs=2) as w:
+        for s in [5, 1, 4, 2, 3]:
+            w.write("/x", rb.image_message(np.full((2, 2), s, np.uint8), rb.Time(s, 0), encoding="mono8"), rb.Time(s, 0))
+    vals = [int(rb.imgmsg_to_array(m)[0, 0]) for _, m, _ in rb.Bag(path).read_messages()]
+    assert vals == [1, 2, 3, 4, 5]
+
+
+def test_imgmsg_honours_row_step():
+    rb = _rb()
+    a = np.arange(4 * 5 * 3, dtype=np.uint8).reshape(4, 5, 3)
+    padded = np.zeros((4, 20), np.uint8)
+    padded[:, :15] = a.reshape(4, 15)
+    m = rb.Image(rb.Header(), 4, 5, "bgr8", 0, 20, padded.tobytes())
+    assert np.array_equal(rb.imgmsg_to_array(rb.decode_image(rb.encode_image(m))), a)
+    with pytest.raises(NotImplementedError):
+        rb.imgmsg_to_array(rb.Image(rb.Header(), 1, 1, "16UC1", 0, 2, b"\0\0"))
+
+
+def test_stereo_pair_selection_follows_the_reference_loop(tmp_path):
+    rb = _rb()
+    from forest_slam_amd import pipeline as pl
+    path = str(tmp_path / "c.bag")
+    with rb.BagWriter(path) as w:
+        for i in range(6):
+            for topic, dt in ((pl.LEFT, 0), (pl.RIGHT, 1000)):
+                t = rb.Time(10 + i, dt)
+                w.write(topic, rb.image_message(np.full((2, 2, 3), i, np.uint8), t), t)
+    bag = rb.Bag(path)
+    # indices: L0 R1 L2 R3 ...: every right message for interval 1; none for even intervals
+    sel = pl.select_stereo_pairs(bag, 1)
+    assert [int(rb.imgmsg_to_array(l)[0, 0, 0]) for _, l, _ in sel] == list(range(6))
+    assert all(r.header.stamp == t for t, _, r in sel)
+    assert pl.select_stereo_pairs(bag, 2) == []
+    assert [int(rb.imgmsg_to_array(r)[0, 0, 0]) for _, _, r in pl.select_stereo_pairs(bag, 3)] == [1, 4]
+
+
+def test_gt_from_bag_reproduces_reference_ground_truth(tmp_path):
+    """gt_localisation.py on a bag whose /gt_poses are the poses behind the reference's own
+    1018_00_Ground_Truth.txt (inverted through T_rgb0_vlp16) -> the same file (%f)."""
+    rb = _rb()
+    from forest_slam_amd import eval as ev
+    from forest_slam_amd import pipeline as pl
+    ref = np.loadtxt(os.path.join(GOLDEN, "1018_00_Ground_Truth.txt"))[:200]
+    path = str(tmp_path / "gt.bag")
+    Tinv = np.linalg.inv(pl.T_RGB0_VLP16)
+    with rb.BagWriter(path) as w:
+        stamps = np.r_[ref[0, 0] - 0.1, ref[:, 0]]
+        for k, t in enumerate(stamps):
+            row = ref[max(k - 1, 0)]
+            M = pl.quaternion_matrix(row[4:8])
+            M[:3, 3] = row[1:4]
+            P = Tinv @ M
+            q = ev.quaternion_from_matrix(P)
+            # nearest-stamp lookup: pose messages stamped 1 ms after each image
+            tt = rb.Time.from_sec(t + 0.001)
+            w.write(pl.GT, rb.PoseStamped(rb.Header(k, tt, "map"), rb.Pose(rb.Point(*P[:3, 3]), rb.Quaternion(*q))), tt)
+            ti = rb.Time.from_sec(t)
+            w.write(pl.LEFT, rb.image_message(np.zeros((2, 2, 3), np.uint8), ti), ti)
+    rows = pl.gt_from_bag(path)
+    assert rows.shape == ref.shape
+    assert np.abs(rows[:, 0] - ref[:, 0]).max() < 2e-6
+    # positions: the file's %f rounding; quaternions: the sign of q is the ROS convention's
+    assert np.abs(rows[:, 1:4] - ref[:, 1:4]).max() < 2e-6
+    dq = np.minimum(np.abs(rows[:, 4:] - ref[:, 4:]).max(1), np.abs(rows[:, 4:] + ref[:, 4:]).max(1))
+    assert dq.max() < 2e-6
+
+
+def test_quaternion_matrix_round_trip():
+    from forest_slam_amd import eval as ev
+    from forest_slam_amd import pipeline as pl
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        M = pl.quaternion_matrix(q)
+        assert abs(np.linalg.det(M[:3, :3]) - 1) < 1e-12
+        q2 = ev.quaternion_from_matrix(M)
+        assert min(np.abs(q2 - q).max(), np.abs(q2 + q).max()) < 1e-12
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_run_stereo_bag_matches_oracle_pipeline(tmp_path, oracle_mod):
+    rb = _rb()
+    import forest_slam_amd.synth as synth
+    from forest_slam_amd import eval as ev
+    from forest_slam_amd import pipeline as pl
+    W, H = 320, 200
+    seq = synth.StereoSequence(seed=4, n_frames=6, W=W, H=H, device="cpu", start=110)
+    K = seq.K
+    path = str(tmp_path / "s.bag")
+    frames = []
+    with rb.BagWriter(path) as w:
+        for i in range(6):
+            L, R = (x.numpy() for x in seq.frame(i))
+            bl = np.repeat(L[..., None], 3, axis=2)
+            br = np.repeat(R[..., None], 3, axis=2)
+            frames.append((bl, br))
+            t = rb.Time(1000 + i, 0)
+            w.write(pl.LEFT, rb.image_message(bl, t), t)
+            w.write(pl.RIGHT, rb.image_message(br, rb.Time(1000 + i, 500)), rb.Time(1000 + i, 500))
+    rows, T, st = pl.run_stereo_bag(path, batch=2, nfeatures=300, device="cuda:0", K_left=K, dist_left=pl.DIST_L,
+                                    K_right=K, dist_right=pl.DIST_R, baseline=synth.BASELINE)
+    # oracle: the same bytes through the restated ingest and stereo_slam.py:232-306
+    grays = [(oracle_mod.undistort_gray(bl, K, pl.DIST_L), oracle_mod.undistort_gray(br, K, pl.DIST_R))
+             for bl, br in frames]
+    Ts, valid = [], []
+    for i in range(1, 6):
+        out = oracle_mod.frame_pose(grays[i - 1][0], grays[i - 1][1], grays[i][0], K, pl.DIST_L, synth.BASELINE,
+                                    nfeatures=300)
+        valid.append(out["T"] is not None)
+        Ts.append(out["T"] if out["T"] is not None else np.eye(4))
+    assert np.array_equal(st != -1, np.array(valid))
+    for i in range(5):
+        if valid[i]:
+            assert np.abs(T[i] - Ts[i]).max() < 1e-4, i
+    cum = ev.chain(np.array(Ts), np.array(valid))
+    ref_rows = ev.tum_rows(np.array([1000 + i + 0.5e-6 for i in range(1, 6)])[np.array(valid)], cum)
+    assert np.abs(rows[:, 0] - ref_rows[:, 0]).max() < 1e-6
+    assert np.abs(rows[:, 1:4] - ref_rows[:, 1:4]).max() < 1e-3
