@@ -293,7 +293,8 @@ int fvo_timing_read(fvo_ctx* c, double* ms, int32_t* launches) {
 
 // Debug/test hook: device pointer + size of an internal workspace buffer of the last call.
 // which: 0 pyramid, 1 blurred pyramid, 2 FAST score map (all [max_batch][total_px] u8),
-//        3 per-level candidate counts, 4 after retainBest(2n), 5 after retainBest(n) (i32 [B][L]).
+//        3 per-level candidate counts, 4 after retainBest(2n), 5 after retainBest(n) (i32 [B][L]),
+//        6 PnP RANSAC inlier count per iteration (i32 [B][1000]), 7 PnP hypotheses (f64 [B][1000][6]).
 int fvo_debug_buffer(fvo_ctx* c, int which, void** ptr, int64_t* bytes) {
   if (!c || !ptr || !bytes) return -1;
   const int64_t B = c->cfg.max_batch;
@@ -304,6 +305,8 @@ int fvo_debug_buffer(fvo_ctx* c, int which, void** ptr, int64_t* bytes) {
     case 3: *ptr = c->ncand; *bytes = B * c->g.nlevels * 4; return 0;
     case 4: *ptr = c->nsel1; *bytes = B * c->g.nlevels * 4; return 0;
     case 5: *ptr = c->nsel2; *bytes = B * c->g.nlevels * 4; return 0;
+    case 6: *ptr = c->pnp_good; *bytes = B * c->pnp_max_iters * 4; return 0;
+    case 7: *ptr = c->pnp_models; *bytes = B * c->pnp_max_iters * 6 * 8; return 0;
     default: return fvo_fail(c, "unknown debug buffer");
   }
 }

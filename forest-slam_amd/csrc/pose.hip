@@ -478,8 +478,11 @@ struct EPnPd {
         M1[3 * j] = as[j] * fu; M1[3 * j + 1] = 0.0; M1[3 * j + 2] = as[j] * (uc - u);
         M2[3 * j] = 0.0; M2[3 * j + 1] = as[j] * fv; M2[3 * j + 2] = as[j] * (vc - v);
       }
+      // rows of M in order (M1 then M2), each accumulated on its own: the oracle's summation order
       for (int a = 0; a < 12; ++a)
-        for (int bb = 0; bb < 12; ++bb) MtM[a * 12 + bb] += M1[a] * M1[bb] + M2[a] * M2[bb];
+        for (int bb = 0; bb < 12; ++bb) MtM[a * 12 + bb] += M1[a] * M1[bb];
+      for (int a = 0; a < 12; ++a)
+        for (int bb = 0; bb < 12; ++bb) MtM[a * 12 + bb] += M2[a] * M2[bb];
     }
     double W[12], U[144], V[144];
     dsvd<12, 12>(MtM, W, U, V);

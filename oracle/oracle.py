@@ -282,6 +282,19 @@ def undistort_map(H: int, W: int, K: np.ndarray, dist):
     return mxy, fr
 
 
+def pnp_hypotheses(P3, p2, K, dist, iters=1000, reproj=1.0):
+    """Debug: (models f64[iters,6] (rvec, tvec), inlier counts i32[iters]) of the RANSAC subsets."""
+    P3 = np.ascontiguousarray(P3, dtype=np.float64)
+    p2 = np.ascontiguousarray(p2, dtype=np.float32)
+    K = np.ascontiguousarray(K, dtype=np.float64)
+    dist = np.ascontiguousarray(np.resize(np.asarray(dist, np.float64), 5))
+    models = np.zeros((iters, 6))
+    good = np.zeros(iters, np.int32)
+    lib().ref_pnp_hypotheses(_p(P3, _f64p), _p(p2, _f32p), len(P3), _p(K, _f64p), _p(dist, _f64p), iters,
+                             ctypes.c_float(reproj), _p(models, _f64p), _p(good, _i32p))
+    return models, good
+
+
 def rodrigues(rvec: np.ndarray) -> np.ndarray:
     rvec = np.ascontiguousarray(rvec, dtype=np.float64).reshape(3)
     R = np.zeros(9)

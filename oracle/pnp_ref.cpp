@@ -812,6 +812,39 @@ int ref_solve_pnp_ransac(const double* P3d, const float* p2, int n, const double
   return 1;
 }
 
+// Debug: the RANSAC hypotheses of the first `iters` iterations (EPnP model per subset and its
+// inlier count), without the acceptance rule -- for stage-by-stage comparison with the GPU.
+int ref_pnp_hypotheses(const double* P3d, const float* p2, int n, const double* Kmat, const double* dist, int iters,
+                       float reproj, double* models, int32_t* good) {
+  pnp::Cam K{Kmat[0], Kmat[4], Kmat[2], Kmat[5], {dist[0], dist[1], dist[2], dist[3], dist[4]}};
+  std::vector<float> P3(3 * n);
+  for (int i = 0; i < 3 * n; ++i) P3[i] = (float)P3d[i];
+  if (n < 6) return 0;
+  std::vector<uint8_t> mask(n);
+  pnp::RNG rng(~0ull);
+  float ms1[15], ms2[10];
+  for (int it = 0; it < iters; ++it) {
+    int idx[5];
+    for (int i = 0; i < 5; ++i) {
+      int j;
+      for (;;) {
+        j = rng.uniform(0, n);
+        bool dup = false;
+        for (int k = 0; k < i; ++k) dup |= idx[k] == j;
+        if (!dup) break;
+      }
+      idx[i] = j;
+      for (int k = 0; k < 3; ++k) ms1[3 * i + k] = P3[3 * j + k];
+      for (int k = 0; k < 2; ++k) ms2[2 * i + k] = p2[2 * j + k];
+    }
+    double rv[3], tv[3];
+    pnp::solve_epnp(K, ms1, ms2, 5, rv, tv);
+    good[it] = pnp::find_inliers(K, P3.data(), p2, n, rv, tv, (float)((double)reproj * reproj), mask.data());
+    for (int i = 0; i < 3; ++i) { models[it * 6 + i] = rv[i]; models[it * 6 + 3 + i] = tv[i]; }
+  }
+  return iters;
+}
+
 void ref_rodrigues(const double* rvec, double* R) { pnp::rodrigues_r2R(rvec, R, nullptr); }
 void ref_rodrigues_jac(const double* rvec, double* R, double* J) { pnp::rodrigues_r2R(rvec, R, J); }
 void ref_rodrigues_inv(const double* R, double* rvec) { pnp::rodrigues_R2r(R, rvec); }
