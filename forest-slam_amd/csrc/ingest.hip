@@ -40,7 +40,7 @@ __device__ __forceinline__ int round_sat(double v) {
   return v >= 2147483647.0 ? 2147483647 : (v <= -2147483648.0 ? (-2147483647 - 1) : (int)rint(v));
 }
 
-// PIX output pixels per thread.  kPinhole: K has the camera-matrix zero pattern
+// PIX output pixels per thread, 4 rows x 64 threads per block.  kPinhole: K has the camera-matrix zero pattern
 // (K[1] = K[3] = K[6] = K[7] = 0, K[8] = 1), so ir[6] = ir[7] = 0 (exact zeros of the closed
 // form) and _w, hence w = 1/_w, is constant along a row: hoisted (bit-identical to the
 // per-pixel evaluation).  The k4..k6 denominator is exactly 1 and x/1.0 == x, so it is dropped.
@@ -48,9 +48,10 @@ template <int PIX, bool kPinhole>
 __global__ __launch_bounds__(256) void k_ing_undistort_gray(const uint8_t* __restrict__ src, int64_t sstride,
                                                             int spitch, uint8_t* __restrict__ dst, int64_t dstride,
                                                             int dpitch, int W, int H, int stripe0, Lens L) {
-  const int row = blockIdx.y, b = blockIdx.z;
-  const int c0 = (blockIdx.x * 256 + threadIdx.x) * PIX;
-  if (c0 >= W) return;
+  // block = 4 rows x 64 threads, each thread PIX consecutive pixels of its row
+  const int row = blockIdx.y * 4 + (threadIdx.x >> 6), b = blockIdx.z;
+  const int c0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * PIX;
+  if (c0 >= W || row >= H) return;
   const uint8_t* S = src + b * sstride;
   const int y0 = (row / stripe0) * stripe0, i = row - y0;
   double Ar[9];
@@ -117,8 +118,8 @@ int ingest_run(fvo_ctx* ctx, const uint8_t* bgr, int batch, int64_t sstride, int
   L.k1 = dist[0]; L.k2 = dist[1]; L.p1 = dist[2]; L.p2 = dist[3]; L.k3 = dist[4];
   int stripe0 = 4096 / (W > 1 ? W : 1);
   stripe0 = stripe0 < 1 ? 1 : (stripe0 > H ? H : stripe0);
-  constexpr int PIX = 8;
-  dim3 grid((W + 256 * PIX - 1) / (256 * PIX), H, batch);
+  constexpr int PIX = 4;
+  dim3 grid((W + 64 * PIX - 1) / (64 * PIX), (H + 3) / 4, batch);
   const bool pinhole = K[1] == 0.0 && K[3] == 0.0 && K[6] == 0.0 && K[7] == 0.0 && K[8] == 1.0;
   FVO_TIMED(ctx, KN_INGEST, s, {
     if (pinhole)

@@ -86,6 +86,9 @@ class StereoFrontEnd:
             self.T_ba = e((B, 4, 4), torch.float64)
             self.ba_stats = e((B, 6), torch.float64)
             self.valid_from = Kw - 2
+        # SGBM (HBM-bound) runs on its own stream, concurrent with ORB + BF on the caller's
+        # stream (latency/VALU-bound); the caller's stream joins it before back-projection.
+        self.s_sgbm = torch.cuda.Stream(dev)
         self.has_prev = False
 
     def prime(self, L0: torch.Tensor, R0: torch.Tensor):
@@ -115,6 +118,18 @@ class StereoFrontEnd:
         if n > B:
             raise ValueError("more frames than the configured batch")
         ctx = self.ctx
+        main = torch.cuda.current_stream(self.dev)
+        # previous stereo pairs -> SGBM on the side stream (needs only images)
+        self.s_sgbm.wait_stream(main)
+        L.record_stream(self.s_sgbm)
+        R.record_stream(self.s_sgbm)
+        with torch.cuda.stream(self.s_sgbm):
+            self.prevL[0].copy_(self.lastL)
+            self.prevR[0].copy_(self.lastR)
+            if n > 1:
+                self.prevL[1:n].copy_(L[:n - 1])
+                self.prevR[1:n].copy_(R[:n - 1])
+            disp = ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n])
         self.imgs[:n].copy_(L)
         self.imgs[n:2 * n].copy_(R)
         kp, desc, cnt = ctx.orb(self.imgs[:2 * n], out=(self.kp[:2 * n], self.desc[:2 * n], self.cnt[:2 * n]))
@@ -132,15 +147,11 @@ class StereoFrontEnd:
         nb = 2 * n if self.match_right else n
         m, nm = ctx.bf_match(self.q_desc[:nb], self.q_cnt[:nb], desc[:nb], cnt[:nb],
                              out=(self.matches[:nb], self.nmatch[:nb]))
-        # previous stereo pairs for SGBM and previous-left keypoints for back-projection
-        self.prevL[0].copy_(self.lastL)
-        self.prevR[0].copy_(self.lastR)
+        # previous-left keypoints for back-projection
         self.q_kp[0].copy_(self.last_kp)
         if n > 1:
-            self.prevL[1:n].copy_(L[:n - 1])
-            self.prevR[1:n].copy_(R[:n - 1])
             self.q_kp[1:n].copy_(kp[:n - 1])
-        disp = ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n])
+        main.wait_stream(self.s_sgbm)
         P3, p2, npts = ctx.backproject(disp, self.q_kp[:n], kp[:n], m[:n], nm[:n], self.K, self.baseline,
                                        out=(self.P3[:n], self.p2[:n], self.npts[:n]))
         rv, tv, T, st, _ = ctx.pnp_ransac(P3, p2, npts, self.K, self.dist,
