@@ -114,6 +114,7 @@ def main():
     ap.add_argument("--ate-frames", type=int, default=200, help="frames of the ATE run (0 = skip)")
     ap.add_argument("--ba-window", type=int, default=10, help="local BA window K (0 = PnP only)")
     ap.add_argument("--cpu-frames", type=int, default=4, help="CPU baseline sample (0 = skip)")
+    ap.add_argument("--overlap-sgbm", type=int, default=1, help="SGBM of step k+1 on a side stream during step k")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,7 +141,7 @@ def main():
     L_all, R_all = seq.frames(range(B + 1))
     torch.cuda.synchronize()
     fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=B, nfeatures=args.nfeatures, device=dev,
-                           ba_window=args.ba_window)
+                           ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm))
     fe.prime(L_all[0], R_all[0])
     Lb, Rb = L_all[1:].contiguous(), R_all[1:].contiguous()
 

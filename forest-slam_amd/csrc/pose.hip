@@ -298,6 +298,75 @@ __device__ void dundistort(const Cam& K, double u, double v, double* xy) {
   xy[1] = y;
 }
 
+// dsvd<12,12> specialised for EPnP: only U is consumed (the rows ut[8..11] of U^T, i.e. the
+// singular vectors of the four smallest singular values), so V is not accumulated; u lives
+// in LDS (one column of a [144][64] array per lane: conflict-free, and no scratch).  The
+// operations on u, the norms, the stable descending order and the scaling are exactly those
+// of dsvd (and of the oracle's svd()).
+template <int S>  // u[k] lives at u[k * S] (S = 64: a lane's column of an LDS array [144][64])
+__device__ __forceinline__ void dsvd12_null4(double* __restrict__ u, double (*out)[12]) {
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0;
+    for (int p = 0; p < 11; ++p)
+      for (int q = p + 1; q < 12; ++q) {
+        double a = 0, bb = 0, g = 0;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          double up = u[(i * 12 + p) * S], uq = u[(i * 12 + q) * S];
+          a += up * up;
+          bb += uq * uq;
+          g += up * uq;
+        }
+        if (!(g == 0.0 || fabs(g) <= 1e-300)) {
+          double rel = fabs(g) / sqrt(a * bb);
+          off = fmax(off, rel);
+          if (!(rel < 1e-15)) {
+            double zeta = (bb - a) / (2.0 * g);
+            double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+            double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+              double up = u[(i * 12 + p) * S], uq = u[(i * 12 + q) * S];
+              u[(i * 12 + p) * S] = c * up - sn * uq;
+              u[(i * 12 + q) * S] = sn * up + c * uq;
+            }
+          }
+        }
+      }
+    if (off < 1e-15) break;
+  }
+  double w[12];
+  int ord[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) s += u[(i * 12 + j) * S] * u[(i * 12 + j) * S];
+    w[j] = sqrt(s);
+    ord[j] = j;
+  }
+  for (int i = 1; i < 12; ++i) {  // stable insertion sort, descending (as dsvd)
+    int k = ord[i], j = i;
+    while (j > 0 && w[ord[j - 1]] < w[k]) { ord[j] = ord[j - 1]; --j; }
+    ord[j] = k;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = ord[8 + r];
+    double wj = 0.0;
+#pragma unroll
+    for (int c = 0; c < 12; ++c) wj = (c == j) ? w[c] : wj;
+    const double inv = wj > 0 ? 1.0 / wj : 0.0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      double v = 0.0;
+#pragma unroll
+      for (int c = 0; c < 12; ++c) v = (c == j) ? u[(i * 12 + c) * S] : v;
+      out[r][i] = v * inv;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ EPnP (5 points)
 __device__ __forceinline__ double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 __device__ __forceinline__ double dist2(const double* a, const double* b) {
@@ -347,10 +416,11 @@ struct EPnPd {
       a[0] = 1.0f - a[1] - a[2] - a[3];
     }
   }
-  __device__ void compute_ccs(const double* betas, const double* ut) {
+  // nv[r] = ut row 8 + r (EPnP's v_{3-r}); rows 11..8 are the four null-space directions
+  __device__ void compute_ccs(const double* betas, const double (*nv)[12]) {
     for (int i = 0; i < 4; ++i) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
     for (int i = 0; i < 4; ++i) {
-      const double* v = ut + 12 * (11 - i);
+      const double* v = nv[3 - i];
       for (int j = 0; j < 4; ++j)
         for (int k = 0; k < 3; ++k) ccs[j][k] += betas[i] * v[3 * j + k];
     }
@@ -361,8 +431,8 @@ struct EPnPd {
       for (int j = 0; j < 3; ++j) pcs[3 * i + j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
     }
   }
-  __device__ double compute_R_and_t(const double* ut, const double* betas, double* R, double* t) {
-    compute_ccs(betas, ut);
+  __device__ double compute_R_and_t(const double (*nv)[12], const double* betas, double* R, double* t) {
+    compute_ccs(betas, nv);
     compute_pcs();
     if (pcs[2] < 0.0) {
       for (int i = 0; i < 4; ++i)
@@ -465,11 +535,11 @@ struct EPnPd {
       for (int i = 0; i < 4; ++i) betas[i] += x[i];
     }
   }
-  __device__ void compute_pose(double* R, double* t) {
+  // MtM: this lane's slice of an LDS [144][64] array (element k at MtM[k * 64]).
+  __device__ void compute_pose(double* R, double* t, double* __restrict__ MtM) {
     choose_control_points();
     barycentric();
-    double MtM[144];
-    for (int i = 0; i < 144; ++i) MtM[i] = 0.0;
+    for (int i = 0; i < 144; ++i) MtM[i * 64] = 0.0;
     for (int i = 0; i < NP; ++i) {
       const double* as = &alphas[4 * i];
       double u = us[2 * i], v = us[2 * i + 1];
@@ -480,18 +550,15 @@ struct EPnPd {
       }
       // rows of M in order (M1 then M2), each accumulated on its own: the oracle's summation order
       for (int a = 0; a < 12; ++a)
-        for (int bb = 0; bb < 12; ++bb) MtM[a * 12 + bb] += M1[a] * M1[bb];
+        for (int bb = 0; bb < 12; ++bb) MtM[(a * 12 + bb) * 64] += M1[a] * M1[bb];
       for (int a = 0; a < 12; ++a)
-        for (int bb = 0; bb < 12; ++bb) MtM[a * 12 + bb] += M2[a] * M2[bb];
+        for (int bb = 0; bb < 12; ++bb) MtM[(a * 12 + bb) * 64] += M2[a] * M2[bb];
     }
-    double W[12], U[144], V[144];
-    dsvd<12, 12>(MtM, W, U, V);
-    double* ut = V;  // reuse: rows = singular vectors (ut[i*12+j] = U[j*12+i])
-    for (int i = 0; i < 12; ++i)
-      for (int j = 0; j < 12; ++j) ut[i * 12 + j] = U[j * 12 + i];
+    double nv[4][12];  // U^T rows 8..11 (singular vectors of the 4 smallest singular values)
+    dsvd12_null4<64>(MtM, nv);
     double L[60], rho[6];
     {
-      const double* vv[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
+      const double* vv[4] = {nv[3], nv[2], nv[1], nv[0]};
       double dv[4][6][3];
       for (int i = 0; i < 4; ++i) {
         int a = 0, bb = 1;
@@ -563,7 +630,7 @@ struct EPnPd {
       }
       gauss_newton(L, rho, betas);
       double Rn[9], tn[3];
-      double e = compute_R_and_t(ut, betas, Rn, tn);
+      double e = compute_R_and_t(nv, betas, Rn, tn);
       if (N == 1 || e < best_err) {
         best_err = e;
         for (int i = 0; i < 9; ++i) Rb[i] = Rn[i];
@@ -832,7 +899,9 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ P3all,
                                                 int cap, Cam K, float thr2, int maxIters, int it_lo,
                                                 const int16_t* __restrict__ sub, const PnpState* __restrict__ state,
                                                 double* __restrict__ model, int32_t* __restrict__ good) {
-  extern __shared__ __attribute__((aligned(16))) float spts[];  // [n][5] x,y,z,u,v
+  extern __shared__ __attribute__((aligned(16))) double smem[];  // [144][64] EPnP MtM, then [n][5] points
+  double* su = smem;
+  float* spts = reinterpret_cast<float*>(smem + 144 * 64);  // x,y,z,u,v
   const int b = blockIdx.y;
   const int it = it_lo + blockIdx.x * 64 + threadIdx.x;
   const PnpState st = state[b];
@@ -862,7 +931,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ P3all,
     e.us[2 * i + 1] = fy * K.fy + K.cy;
   }
   double R[9], t[3], r[3], dR[27];
-  e.compute_pose(R, t);
+  e.compute_pose(R, t, su + threadIdx.x);
   rod_R2r(R, r);
   double* mo = model + ((int64_t)b * maxIters + it) * 6;
   for (int i = 0; i < 3; ++i) { mo[i] = r[i]; mo[3 + i] = t[i]; }
@@ -999,7 +1068,8 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
   const float thr2 = (float)((double)reproj * reproj);
   const int maxIters = iters;
   PnpState* st = (PnpState*)ctx->pnp_state;
-  const size_t shm = (size_t)cap * 5 * sizeof(float);
+  const size_t shm = 144 * 64 * sizeof(double) + (size_t)cap * 5 * sizeof(float);
+  if (shm > 160 * 1024) return fvo_fail(ctx, "pnp: point capacity exceeds LDS (cap <= 3328)");
   if (shm > 64 * 1024)
     FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_pnp_hyp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   const int first = std::min(maxIters, 128);

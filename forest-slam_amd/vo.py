@@ -29,7 +29,7 @@ from . import _lib
 class StereoFrontEnd:
     def __init__(self, width: int, height: int, K: np.ndarray, dist: np.ndarray, baseline: float, batch: int,
                  nfeatures: int = 500, match_right: bool = True, device=None, ba_window: int = 10,
-                 ba_iters: int = 10, **params):
+                 ba_iters: int = 10, overlap_sgbm: bool = False, **params):
         self.B = batch
         self.K = np.asarray(K, np.float64)
         self.dist = np.resize(np.asarray(dist, np.float64), 5)
@@ -59,7 +59,8 @@ class StereoFrontEnd:
         self.nmatch = e((2 * B,), torch.int32)
         self.prevL = e((B, height, width), torch.uint8)
         self.prevR = e((B, height, width), torch.uint8)
-        self.disp = e((B, height, width), torch.int16)
+        self.disp_buf = [e((B, height, width), torch.int16), e((B, height, width), torch.int16)]
+        self.disp = self.disp_buf[0]
         self.P3 = e((B, cap, 3), torch.float32)
         self.p2 = e((B, cap, 2), torch.float32)
         self.npts = e((B,), torch.int32)
@@ -69,8 +70,6 @@ class StereoFrontEnd:
         self.status = e((B,), torch.int32)
         self.inl = e((B, cap), torch.uint8)
         self.imgs = e((2 * B, height, width), torch.uint8)
-        self.lastL = e((height, width), torch.uint8)
-        self.lastR = e((height, width), torch.uint8)
         self.last_kp = e((cap, _lib.KP_STRIDE), torch.float32)
         self.last_desc = e((2, cap, _lib.DESC_BYTES), torch.uint8)
         self.last_cnt = e((2,), torch.int32)
@@ -86,17 +85,25 @@ class StereoFrontEnd:
             self.T_ba = e((B, 4, 4), torch.float64)
             self.ba_stats = e((B, 6), torch.float64)
             self.valid_from = Kw - 2
-        # SGBM (HBM-bound) runs on its own stream, concurrent with ORB + BF on the caller's
-        # stream (latency/VALU-bound); the caller's stream joins it before back-projection.
-        self.s_sgbm = torch.cuda.Stream(dev)
+        # overlap_sgbm: SGBM (HBM-bound) runs on its own stream with double-buffered
+        # disparities, so the SGBM of step k+1 overlaps the PnP / BA of step k; the caller's
+        # stream joins it before back-projection.  The step inputs must then be complete
+        # when step() is called (resident in HBM, or pass inputs_ready).  Default: SGBM runs
+        # in order on the caller's stream.
+        self.overlap_sgbm = bool(overlap_sgbm)
+        self.s_sgbm = torch.cuda.Stream(dev) if self.overlap_sgbm else None
+        self.sg_lastL = e((height, width), torch.uint8)
+        self.sg_lastR = e((height, width), torch.uint8)
+        self.main_done = [None, None]
+        self.k = 0
         self.has_prev = False
 
     def prime(self, L0: torch.Tensor, R0: torch.Tensor):
         """Feed the first stereo pair of a sequence (no pose is produced for it)."""
         imgs = torch.stack([L0, R0]).to(self.dev)
         kp, desc, cnt = self.ctx.orb(imgs)
-        self.lastL.copy_(imgs[0])
-        self.lastR.copy_(imgs[1])
+        self.sg_lastL.copy_(imgs[0])
+        self.sg_lastR.copy_(imgs[1])
         self.last_kp.copy_(kp[0])
         self.last_desc.copy_(desc[:2])
         self.last_cnt.copy_(cnt[:2])
@@ -107,7 +114,7 @@ class StereoFrontEnd:
             self.valid_from = Kw - 2
         self.has_prev = True
 
-    def step(self, L: torch.Tensor, R: torch.Tensor):
+    def step(self, L: torch.Tensor, R: torch.Tensor, inputs_ready=None):
         """L, R: u8 [n,H,W] device tensors, n <= B consecutive frames after the primed/last
         pair.  Returns (T f64[n,4,4], status i32[n]) device tensors (async): the BA-refined
         relative transforms when local BA is enabled, else the PnP ones (``self.T``)."""
@@ -119,16 +126,24 @@ class StereoFrontEnd:
             raise ValueError("more frames than the configured batch")
         ctx = self.ctx
         main = torch.cuda.current_stream(self.dev)
-        # previous stereo pairs -> SGBM on the side stream (needs only images)
-        self.s_sgbm.wait_stream(main)
-        L.record_stream(self.s_sgbm)
-        R.record_stream(self.s_sgbm)
-        with torch.cuda.stream(self.s_sgbm):
-            self.prevL[0].copy_(self.lastL)
-            self.prevR[0].copy_(self.lastR)
+        slot = self.k % 2
+        self.disp = self.disp_buf[slot]
+        sg = self.s_sgbm if self.overlap_sgbm else main
+        if self.overlap_sgbm:
+            if inputs_ready is not None:
+                sg.wait_event(inputs_ready)
+            if self.main_done[slot] is not None:  # main's reads of this disparity buffer (step k-2)
+                sg.wait_event(self.main_done[slot])
+            L.record_stream(sg)
+            R.record_stream(sg)
+        with torch.cuda.stream(sg):  # previous stereo pairs -> SGBM (needs only images)
+            self.prevL[0].copy_(self.sg_lastL)
+            self.prevR[0].copy_(self.sg_lastR)
             if n > 1:
                 self.prevL[1:n].copy_(L[:n - 1])
                 self.prevR[1:n].copy_(R[:n - 1])
+            self.sg_lastL.copy_(L[n - 1])
+            self.sg_lastR.copy_(R[n - 1])
             disp = ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n])
         self.imgs[:n].copy_(L)
         self.imgs[n:2 * n].copy_(R)
@@ -151,7 +166,8 @@ class StereoFrontEnd:
         self.q_kp[0].copy_(self.last_kp)
         if n > 1:
             self.q_kp[1:n].copy_(kp[:n - 1])
-        main.wait_stream(self.s_sgbm)
+        if self.overlap_sgbm:
+            main.wait_stream(self.s_sgbm)
         P3, p2, npts = ctx.backproject(disp, self.q_kp[:n], kp[:n], m[:n], nm[:n], self.K, self.baseline,
                                        out=(self.P3[:n], self.p2[:n], self.npts[:n]))
         rv, tv, T, st, _ = ctx.pnp_ransac(P3, p2, npts, self.K, self.dist,
@@ -160,13 +176,14 @@ class StereoFrontEnd:
         out = T
         if self.ba_window:
             out = self._local_ba(n, kp, cnt, m, nm, disp, T)
-        self.lastL.copy_(L[n - 1])
-        self.lastR.copy_(R[n - 1])
         self.last_kp.copy_(kp[n - 1])
         self.last_desc[0].copy_(desc[n - 1])
         self.last_desc[1].copy_(desc[2 * n - 1])
         self.last_cnt[0:1].copy_(cnt[n - 1:n])
         self.last_cnt[1:2].copy_(cnt[2 * n - 1:2 * n])
+        if self.overlap_sgbm:
+            self.main_done[slot] = main.record_event()
+        self.k += 1
         return out, st
 
     def _local_ba(self, n, kp, cnt, m, nm, disp, T):

@@ -233,3 +233,21 @@ def test_contexts_of_different_sizes_coexist(oracle_mod):
         (res,), _ = _orb_gpu(ctx, [img])
         kp, d = oracle_mod.orb_detect_compute(img, 300)
         assert np.array_equal(res[0][:, :6], kp) and np.array_equal(res[1], d)
+
+
+def test_overlapped_sgbm_stream_matches_serial(frames):
+    """StereoFrontEnd(overlap_sgbm=True) (SGBM of step k+1 on a side stream, double-buffered
+    disparities) gives bit-identical transforms and statuses to the in-order schedule."""
+    from forest_slam_amd import synth, vo
+    Ls = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
+    Rs = torch.from_numpy(np.stack([f[1] for f in frames])).cuda()
+    outs = []
+    for ov in (False, True):
+        fe = vo.StereoFrontEnd(960, 600, synth.K0, synth.DIST_L, synth.BASELINE, batch=1, nfeatures=500,
+                               ba_window=3, overlap_sgbm=ov)
+        fe.prime(Ls[0], Rs[0])
+        res = [fe.step(Ls[i:i + 1], Rs[i:i + 1]) for i in (1, 2, 1, 2)]
+        torch.cuda.synchronize()
+        outs.append([(T.cpu().numpy().copy(), st.cpu().numpy().copy()) for T, st in res])
+    for (Ta, sa), (Tb, sb) in zip(*outs):
+        assert np.array_equal(sa, sb) and np.array_equal(Ta, Tb)
