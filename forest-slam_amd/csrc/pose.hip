@@ -899,33 +899,26 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ P3all,
                                                 int cap, Cam K, float thr2, int maxIters, int it_lo,
                                                 const int16_t* __restrict__ sub, const PnpState* __restrict__ state,
                                                 double* __restrict__ model, int32_t* __restrict__ good) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];  // [144][64] EPnP MtM, then [n][5] points
+  extern __shared__ __attribute__((aligned(16))) double smem[];  // [144][64] EPnP MtM (one column per lane)
   double* su = smem;
-  float* spts = reinterpret_cast<float*>(smem + 144 * 64);  // x,y,z,u,v
   const int b = blockIdx.y;
   const int it = it_lo + blockIdx.x * 64 + threadIdx.x;
   const PnpState st = state[b];
   const int n = st.n;
   if (n < 6 || it_lo + (int)blockIdx.x * 64 >= min(st.niters, maxIters)) return;
-  const float* P3 = P3all + (int64_t)b * cap * 3;
-  const float* p2 = p2all + (int64_t)b * cap * 2;
-  for (int i = threadIdx.x; i < n; i += 64) {
-    spts[i * 5 + 0] = P3[3 * i];
-    spts[i * 5 + 1] = P3[3 * i + 1];
-    spts[i * 5 + 2] = P3[3 * i + 2];
-    spts[i * 5 + 3] = p2[2 * i];
-    spts[i * 5 + 4] = p2[2 * i + 1];
-  }
-  __syncthreads();
   if (it >= maxIters) return;
+  // points are read from global memory: the scoring loop's addresses are wave-uniform
+  // (scalar loads), so they take no LDS and leave room for two waves per CU
+  const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
+  const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
   const int16_t* sb = sub + ((int64_t)b * maxIters + it) * 5;
   EPnPd<5> e;
   e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
   for (int i = 0; i < 5; ++i) {
     int j = sb[i];
-    for (int c = 0; c < 3; ++c) e.pws[3 * i + c] = (double)spts[j * 5 + c];
+    for (int c = 0; c < 3; ++c) e.pws[3 * i + c] = (double)P3[j * 3 + c];
     double xy[2];
-    dundistort(K, (double)spts[j * 5 + 3], (double)spts[j * 5 + 4], xy);
+    dundistort(K, (double)p2[j * 2], (double)p2[j * 2 + 1], xy);
     float fx = (float)xy[0], fy = (float)xy[1];
     e.us[2 * i] = fx * K.fx + K.cx;
     e.us[2 * i + 1] = fy * K.fy + K.cy;
@@ -938,10 +931,9 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ P3all,
   rod_r2R(r, R, dR);
   int g = 0;
   for (int i = 0; i < n; ++i) {
-    const float* q = spts + i * 5;
-    double M[3] = {(double)q[0], (double)q[1], (double)q[2]}, uv[2];
+    double M[3] = {(double)P3[3 * i], (double)P3[3 * i + 1], (double)P3[3 * i + 2]}, uv[2];
     dproject(K, R, dR, t, M, uv, nullptr);
-    float du = q[3] - (float)uv[0], dv = q[4] - (float)uv[1];
+    float du = p2[2 * i] - (float)uv[0], dv = p2[2 * i + 1] - (float)uv[1];
     g += (du * du + dv * dv) <= thr2;
   }
   good[(int64_t)b * maxIters + it] = g;
@@ -1068,8 +1060,7 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
   const float thr2 = (float)((double)reproj * reproj);
   const int maxIters = iters;
   PnpState* st = (PnpState*)ctx->pnp_state;
-  const size_t shm = 144 * 64 * sizeof(double) + (size_t)cap * 5 * sizeof(float);
-  if (shm > 160 * 1024) return fvo_fail(ctx, "pnp: point capacity exceeds LDS (cap <= 3328)");
+  const size_t shm = 144 * 64 * sizeof(double);
   if (shm > 64 * 1024)
     FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_pnp_hyp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   const int first = std::min(maxIters, 128);
