@@ -554,51 +554,83 @@ __global__ __launch_bounds__(kBlock) void k_ba_solve(void* ws, BaDims dm) {
   const int nch = (L + dm.LPC - 1) / dm.LPC;
   const double lam = S->lam;
   double* rhs = sS + np * np;
-  for (int idx = tid; idx < np * np; idx += kBlock) {
-    const int a = idx / np, b = idx % np;
-    if (a > b) continue;
-    const int fa = a / 6 + 1, fb = b / 6 + 1;
-    double hv = 0.0;
-    if (fa == fb) {
-      const int i = a % 6, j = b % 6;
-      const int q = i * 6 - i * (i - 1) / 2 + (j - i);
-      hv = S->Hpp[fa][q];
-      if (i == j) hv += lam * hv + 1e-6;
+  // S = H_pp + lam diag + 1e-6 I - sum_c G_c (upper triangle computed, mirrored); 16 x 16
+  // thread grid over (a, b), no integer division
+  const int ta = tid >> 4, tb = tid & 15;
+  for (int a = ta; a < np; a += 16) {
+    const int fa = a / 6 + 1, ia = a - 6 * (fa - 1);
+    for (int b = a + tb; b < np; b += 16) {
+      const int fb = b / 6 + 1;
+      double hv = 0.0;
+      if (fa == fb) {
+        const int i = ia, j = b - 6 * (fb - 1);
+        const int q = i * 6 - i * (i - 1) / 2 + (j - i);
+        hv = S->Hpp[fa][q];
+        if (i == j) hv += lam * hv + 1e-6;
+      }
+      double gs = 0.0;  // chunk order kept; the loads are issued 8 ahead of the adds
+      const double* gp = v.Gp + a * NR + b;
+#pragma unroll 8
+      for (int c = 0; c < nch; ++c) gs += gp[(int64_t)c * NR * NR];
+      sS[a * np + b] = hv - gs;
+      sS[b * np + a] = hv - gs;
     }
-    double gs = 0.0;
-    for (int c = 0; c < nch; ++c) gs += v.Gp[(int64_t)c * NR * NR + a * NR + b];
-    sS[a * np + b] = hv - gs;
-    sS[b * np + a] = hv - gs;
   }
   for (int a = tid; a < np; a += kBlock) {
     double gs = 0.0;
-    for (int c = 0; c < nch; ++c) gs += v.Gp[(int64_t)c * NR * NR + a * NR + NR - 1];
+    const double* gp = v.Gp + a * NR + NR - 1;
+#pragma unroll 8
+    for (int c = 0; c < nch; ++c) gs += gp[(int64_t)c * NR * NR];
     rhs[a] = -S->Hpp[a / 6 + 1][21 + a % 6] + gs;
   }
+  double* sdiag = rhs + np;  // sqrt of the pivots
   if (tid == 0) s_fail = 0;
   __syncthreads();
-  for (int k = 0; k < np; ++k) {
+  // Right-looking Cholesky, one barrier per column: phase k applies column k to the trailing
+  // matrix and finishes column k+1 at the same time -- every thread that owns an element
+  // (i, k+1) recomputes the updated pivot d = S[k+1][k+1] - S[k+1][k]^2 itself (identical
+  // arithmetic in every thread), so the pivot's square root and the column scaling need no
+  // extra barrier.  The pivot entries themselves stay untouched (sdiag holds the roots).
+  if (tid == 0) {
+    const double d = sS[0];
+    if (!(d > 0.0)) s_fail = 1;
+    sdiag[0] = sqrt(d);
+  }
+  __syncthreads();
+  if (s_fail) {
+    if (tid == 0) S->fail = 1;
+    return;
+  }
+  for (int i = 1 + tid; i < np; i += kBlock) sS[i * np] /= sdiag[0];
+  __syncthreads();
+  for (int k = 0; k + 1 < np; ++k) {
+    const int k1 = k + 1;
+    const double lk1 = sS[k1 * np + k];
+    const double dk1 = sS[k1 * np + k1] - lk1 * lk1;
+    const double rk1 = sqrt(dk1);
     if (tid == 0) {
-      const double d = sS[k * np + k];
-      if (!(d > 0.0)) s_fail = 1;
-      else sS[k * np + k] = sqrt(d);
+      if (!(dk1 > 0.0)) s_fail = 1;
+      sdiag[k1] = rk1;
+    }
+    for (int i = k1 + ta; i < np; i += 16) {
+      const double lik = sS[i * np + k];
+      for (int j = k1 + tb; j <= i; j += 16) {
+        if (j == k1) {
+          if (i > k1) sS[i * np + k1] = (sS[i * np + k1] - lik * lk1) / rk1;
+        } else {
+          sS[i * np + j] -= lik * sS[j * np + k];
+        }
+      }
     }
     __syncthreads();
     if (s_fail) break;
-    const double dk = sS[k * np + k];
-    for (int i = k + 1 + tid; i < np; i += kBlock) sS[i * np + k] /= dk;
-    __syncthreads();
-    const int m = np - k - 1;
-    for (int idx = tid; idx < m * m; idx += kBlock) {
-      const int i = k + 1 + idx / m, j = k + 1 + idx % m;
-      if (j <= i) sS[i * np + j] -= sS[i * np + k] * sS[j * np + k];
-    }
-    __syncthreads();
   }
   if (s_fail) {
     if (tid == 0) S->fail = 1;
     return;
   }
+  for (int i = tid; i < np; i += kBlock) sS[i * np + i] = sdiag[i];
+  __syncthreads();
   if (wid == 0) {  // L y = rhs, L^T x = y (wave 0)
     for (int i = 0; i < np; ++i) {
       double p = 0;
@@ -794,7 +826,7 @@ BaDims make_dims(const fvo_ctx* ctx) {
 size_t lin_shm(const BaDims& d) { return (size_t)8 * 3 * d.LPC * (d.NR + 2); }
 size_t solve_shm(int K) {
   const int np = 6 * (K - 1);
-  return (size_t)8 * (np * np + np);
+  return (size_t)8 * (np * np + 2 * np);  // S, rhs, pivot roots
 }
 
 }  // namespace

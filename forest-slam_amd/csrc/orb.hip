@@ -36,8 +36,10 @@ struct OrbDev {
   long long cand_off[FVO_MAX_LEVELS + 1];
   float scale[FVO_MAX_LEVELS];
   int nfeat[FVO_MAX_LEVELS];
-  int tile0[FVO_MAX_LEVELS + 1];  // first 64x16 tile of each level (per image)
+  int tile0[FVO_MAX_LEVELS + 1];  // first 64x32 FAST tile of each level (per image)
   int ntx[FVO_MAX_LEVELS];        // tiles per row of each level
+  int btile0[FVO_MAX_LEVELS + 1]; // first 256x32 blur tile of each level (per image)
+  int bntx[FVO_MAX_LEVELS];       // blur tiles per row of each level
 };
 __constant__ int c_umax[20];
 __constant__ signed char c_pattern[256 * 4];
@@ -103,7 +105,7 @@ __constant__ int c_cdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2
 // strict 3x3 NMS + border filter of the tile is evaluated from the LDS score tile.  Output:
 // the full score map (debug / tests), one keep bit per pixel (a 64-bit word per tile row)
 // and per-row keep counts.
-constexpr int kTW = 64, kTH = 16;
+constexpr int kTW = 64, kTH = 32;
 constexpr int kFW = kTW + 2, kFH = kTH + 2;     // FAST region (NMS halo)
 constexpr int kIW = kTW + 8, kIH = kTH + 8;     // image patch (FAST radius 3 + halo)
 
@@ -645,41 +647,59 @@ __device__ __forceinline__ int reflect101(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
+// GaussianBlur 7x7 sigma 2 (8-bit fixed point, BORDER_REFLECT_101 per level).  Block = a
+// 256 x 32 output tile: the (32+6) x (256+6) input patch is staged in LDS once, then each
+// thread owns one column and streams down the 38 input rows, computing the horizontal 7-tap
+// sum from LDS and the vertical 7-tap sum from a 7-entry register window (the row loop is
+// unrolled, so the window is static registers).  Read amplification 1.2x, one byte store
+// per pixel (64 B per wave instruction).
+constexpr int kBW = 256, kBH = 32;
+
+__device__ __forceinline__ int btile_level(const OrbDev& G, int t) {
+  int l = 0;
+#pragma unroll
+  for (int k = 1; k < FVO_MAX_LEVELS; ++k)
+    if (k < G.nlevels && t >= G.btile0[k]) l = k;
+  return l;
+}
+
 __global__ __launch_bounds__(256) void k_blur(const OrbDev G, const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur, int64_t total) {
-  constexpr int BW = kTW + 6, BH = kTH + 6;
-  __shared__ uint8_t s_img[BH][BW];
-  __shared__ int s_rs[BH][kTW];
+  constexpr int RW = kBW + 6, RH = kBH + 6;
+  __shared__ uint8_t s_img[RH][RW + 2];
   const int b = blockIdx.y, t = blockIdx.x;
-  const int l = tile_level(G, t);
-  const int lt = t - G.tile0[l];
-  const int tx = lt % G.ntx[l], ty = lt / G.ntx[l];
-  const int x0 = tx * kTW, y0 = ty * kTH;
+  const int l = btile_level(G, t);
+  const int lt = t - G.btile0[l];
+  const int tx = lt % G.bntx[l], ty = lt / G.bntx[l];
+  const int x0 = tx * kBW, y0 = ty * kBH;
   const int w = G.w[l], h = G.h[l];
   const uint8_t* im = pyr + b * total + G.off[l];
-  for (int i = threadIdx.x; i < BH * BW; i += 256) {
-    const int r = i / BW, c = i % BW;
-    const int y = reflect101(min(y0 - 3 + r, h - 1 + (h - 1)), h), x = reflect101(min(x0 - 3 + c, 2 * (w - 1)), w);
-    s_img[r][c] = im[(int64_t)y * w + x];
+  for (int r = 0; r < RH; ++r) {
+    const int y = reflect101(min(y0 - 3 + r, 2 * (h - 1)), h);
+    const uint8_t* row = im + (int64_t)y * w;
+    for (int c = threadIdx.x; c < RW; c += 256) s_img[r][c] = row[reflect101(min(x0 - 3 + c, 2 * (w - 1)), w)];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < BH * kTW; i += 256) {
-    const int r = i / kTW, c = i % kTW;
-    int rs = 0;
+  const int c = threadIdx.x, x = x0 + c;
+  uint8_t* out = blur + b * total + G.off[l] + x;
+  const bool xin = x < w;
+  int win[7] = {0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 7; ++k) rs += c_gk[k] * s_img[r][c + k];
-    s_rs[r][c] = rs;
-  }
-  __syncthreads();
-  const int c = threadIdx.x & 63, x = x0 + c;
-  for (int rr = threadIdx.x >> 6; rr < kTH; rr += 4) {
-    const int y = y0 + rr;
-    if (y >= h || x >= w) continue;
-    int s = 0;
+  for (int r = 0; r < RH; ++r) {
+    int hs = 0;
 #pragma unroll
-    for (int j = 0; j < 7; ++j) s += c_gk[j] * s_rs[rr + j][c];
-    const int q = (s + 32767 + ((s >> 16) & 1)) >> 16;  // round half to even
-    blur[b * total + G.off[l] + (int64_t)y * w + x] = (uint8_t)min(q, 255);
+    for (int k = 0; k < 7; ++k) hs += c_gk[k] * s_img[r][c + k];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) win[j] = win[j + 1];
+    win[6] = hs;
+    if (r >= 6) {
+      const int y = y0 + r - 6;
+      int sv = 0;
+#pragma unroll
+      for (int j = 0; j < 7; ++j) sv += c_gk[j] * win[j];
+      const int q = (sv + 32767 + ((sv >> 16) & 1)) >> 16;  // round half to even
+      if (xin && y < h) out[(int64_t)y * w] = (uint8_t)min(q, 255);
+    }
   }
 }
 
@@ -848,7 +868,7 @@ OrbDev make_dev(const OrbGeom& g) {
   OrbDev G{};
   G.nlevels = g.nlevels;
   G.total_rows = g.total_rows;
-  int t = 0;
+  int t = 0, bt = 0;
   for (int l = 0; l < g.nlevels; ++l) {
     G.row0[l] = g.row0[l];
     G.w[l] = g.w[l];
@@ -860,7 +880,11 @@ OrbDev make_dev(const OrbGeom& g) {
     G.ntx[l] = (g.w[l] + kTW - 1) / kTW;
     G.tile0[l] = t;
     t += G.ntx[l] * ((g.h[l] + kTH - 1) / kTH);
+    G.bntx[l] = (g.w[l] + kBW - 1) / kBW;
+    G.btile0[l] = bt;
+    bt += G.bntx[l] * ((g.h[l] + kBH - 1) / kBH);
   }
+  G.btile0[g.nlevels] = bt;
   G.row0[g.nlevels] = g.row0[g.nlevels];
   G.off[g.nlevels] = g.off[g.nlevels];
   G.cand_off[g.nlevels] = g.cand_off[g.nlevels];
@@ -901,7 +925,7 @@ int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride
   FVO_TIMED(ctx, KN_ORB_OFFSETS, s, hipLaunchKernelGGL(k_offsets, dim3((batch + 63) / 64), dim3(64), 0, s, ctx->nsel2, ctx->koff, counts, batch, L, cap));
   FVO_TIMED(ctx, KN_ORB_ANGLE, s, hipLaunchKernelGGL(k_angle, dim3(16, L, batch), dim3(256), 0, s, G, ctx->pyr, ctx->hel, ctx->nsel2, ctx->koff, kp,
                      total, g.cand_total, L, cap, c.patch_size));
-  FVO_TIMED(ctx, KN_ORB_BLUR, s, hipLaunchKernelGGL(k_blur, dim3(ntiles, batch), dim3(256), 0, s, G, ctx->pyr, ctx->blur, total));
+  FVO_TIMED(ctx, KN_ORB_BLUR, s, hipLaunchKernelGGL(k_blur, dim3(G.btile0[L], batch), dim3(256), 0, s, G, ctx->pyr, ctx->blur, total));
   FVO_TIMED(ctx, KN_ORB_BRIEF, s, hipLaunchKernelGGL(k_brief, dim3(64, batch), dim3(256), 0, s, G, ctx->blur, kp, counts, desc, total, cap));
   FVO_LAUNCH_CHECK(ctx);
   return 0;

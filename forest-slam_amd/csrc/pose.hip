@@ -149,6 +149,65 @@ __device__ void dsvd(const double* A, double* W, double* U, double* V) {
   }
 }
 
+// dsvd with caller-provided work arrays (e.g. LDS for the single-lane 12x12 DLT SVD of the
+// refinement: no scratch).  Same operations as dsvd.
+template <int M, int N>
+__device__ void dsvd_ws(const double* A, double* W, double* U, double* V, double* u, double* v) {
+  double w[N];
+  for (int i = 0; i < M * N; ++i) u[i] = A[i];
+  for (int i = 0; i < N * N; ++i) v[i] = (i % (N + 1) == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0;
+    for (int p = 0; p < N - 1; ++p)
+      for (int q = p + 1; q < N; ++q) {
+        double a = 0, bb = 0, g = 0;
+        for (int i = 0; i < M; ++i) {
+          double up = u[i * N + p], uq = u[i * N + q];
+          a += up * up;
+          bb += uq * uq;
+          g += up * uq;
+        }
+        if (g == 0.0 || fabs(g) <= 1e-300) continue;
+        double rel = fabs(g) / sqrt(a * bb);
+        off = fmax(off, rel);
+        if (rel < 1e-15) continue;
+        double zeta = (bb - a) / (2.0 * g);
+        double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+        for (int i = 0; i < M; ++i) {
+          double up = u[i * N + p], uq = u[i * N + q];
+          u[i * N + p] = c * up - s * uq;
+          u[i * N + q] = s * up + c * uq;
+        }
+        for (int i = 0; i < N; ++i) {
+          double vp = v[i * N + p], vq = v[i * N + q];
+          v[i * N + p] = c * vp - s * vq;
+          v[i * N + q] = s * vp + c * vq;
+        }
+      }
+    if (off < 1e-15) break;
+  }
+  int ord[N];
+  for (int j = 0; j < N; ++j) {
+    double s = 0;
+    for (int i = 0; i < M; ++i) s += u[i * N + j] * u[i * N + j];
+    w[j] = sqrt(s);
+    ord[j] = j;
+  }
+  for (int i = 1; i < N; ++i) {
+    int k = ord[i], j = i;
+    while (j > 0 && w[ord[j - 1]] < w[k]) { ord[j] = ord[j - 1]; --j; }
+    ord[j] = k;
+  }
+  for (int jj = 0; jj < N; ++jj) {
+    int j = ord[jj];
+    W[jj] = w[j];
+    double inv = w[j] > 0 ? 1.0 / w[j] : 0.0;
+    for (int i = 0; i < M; ++i) U[i * N + jj] = u[i * N + j] * inv;
+    for (int i = 0; i < N; ++i) V[i * N + jj] = v[i * N + j];
+  }
+}
+
 template <int M, int N>
 __device__ void dsolve(const double* A, const double* b, double* x) {
   double W[N], U[M * N], V[N * N], tmp[N];
@@ -653,6 +712,7 @@ __device__ __forceinline__ double wsum_d(double v) {
 
 // ------------------------------------------------------------------ RANSAC + refine
 struct PnpShared {
+  double dlt[5][144];  // DLT 12x12 SVD: input, work u / v, outputs U / V (lane 0 only)
   int sub[kChunk][5];
   int good[kChunk];
   double model[kChunk][6];
@@ -736,11 +796,14 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
   if (lane == 0) {
     double R[9];
     if (!planar) {
-      double LL[144], LW[12], LU[144], LV[144];
+      double* LL = sh.dlt[0];
+      double* LU = sh.dlt[3];
+      double* LV = sh.dlt[4];
+      double LW[12];
       int k = 0;
       for (int a = 0; a < 12; ++a)
         for (int b = a; b < 12; ++b) { LL[a * 12 + b] = LLp[k]; LL[b * 12 + a] = LLp[k]; ++k; }
-      dsvd<12, 12>(LL, LW, LU, LV);
+      dsvd_ws<12, 12>(LL, LW, LU, LV, sh.dlt[1], sh.dlt[2]);
       double RRt[12];
       for (int i = 0; i < 12; ++i) RRt[i] = LV[i * 12 + 11];
       double RR[9] = {RRt[0], RRt[1], RRt[2], RRt[4], RRt[5], RRt[6], RRt[8], RRt[9], RRt[10]};
@@ -762,11 +825,14 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
       for (int i = 0; i < 3; ++i) param[3 + i] = tt[i] * nR / sc;
       rod_R2r(R, param);
     } else {
-      double AtA[81], W9[9], U9[81], V9[81], H[9], t[3];
+      double* AtA = sh.dlt[0];
+      double* U9 = sh.dlt[3];
+      double* V9 = sh.dlt[4];
+      double W9[9], H[9], t[3];
       int k = 0;
       for (int a = 0; a < 9; ++a)
         for (int b = a; b < 9; ++b) { AtA[a * 9 + b] = LLp[k]; AtA[b * 9 + a] = LLp[k]; ++k; }
-      dsvd<9, 9>(AtA, W9, U9, V9);
+      dsvd_ws<9, 9>(AtA, W9, U9, V9, sh.dlt[1], sh.dlt[2]);
       for (int i = 0; i < 9; ++i) H[i] = V9[i * 9 + 8];
       if (fabs(H[8]) >= 1e-300) {
         for (int i = 0; i < 9; ++i) H[i] /= H[8];
