@@ -83,8 +83,9 @@ struct fvo_ctx {
   uint16_t* sg_L = nullptr;     // cost C [B][width1][D/8][H]x8
   uint16_t* sg_V = nullptr;     // top-down pass V [B][width1][D/8][H]x8
   int16_t* sg_raw = nullptr;    // [B][W][H] pre-median disparity (transposed)
-  int16_t* sg_d2 = nullptr;     // [B][W][H] right-view disparity (pseudo LR check)
-  int16_t* sg_d2c = nullptr;    // [B][W][H] right-view best cost
+  uint32_t* sg_d2 = nullptr;    // [B][W][H] right-view key (cost << 16 | 0xFFFF - x1), pseudo LR check
+  hipStream_t sg_s2 = nullptr;  // second stream for chunked (pipelined) SGBM batches
+  hipEvent_t sg_fork = nullptr, sg_join = nullptr;
   // pose workspace
   double* pnp_hyp = nullptr;      // [B][cap][2] normalised inlier points (refinement)
   int32_t* pnp_sub = nullptr;     // [B][cap] inlier indices

@@ -2,22 +2,26 @@
 // get_disparity_map (ros_ws/src/stereo_slam.py:108-117): numDisparities 96, minDisparity 0,
 // blockSize 7, P1 392, P2 1568, 3-way aggregation, 4 fixed stripes, then medianBlur(3).
 //
-// Volumes per pair, all [row][x1][d] u16 (x1 = x - max(maxD,0) in [0,width1), d in [0,D)):
-//   hsum (k_sg_hsum -> k_sg_vert), C and V (k_sg_vert -> k_sg_horiz), LV = L + V (the
-//   left->right pass, written over hsum).  raw / d2 / d2c are [x][row] int16.
+// Volumes per pair, u16 [HG][x1][16][d] (row groups of 16 rows interleaved per column, so
+// the 16 rows a wave of k_sg_horiz scans read 3 KB contiguous per column step; x1 = x -
+// max(maxD,0) in [0,width1), d in [0,D)): C and V (k_sg_costvert -> k_sg_horiz), LV = L + V
+// (the left->right pass).  raw is [x][row] int16, the right-view keys [x][row] u32.
 // Kernels
-//   k_sg_hsum<D>   thread per (d, 64-column segment): BT pixel cost of both channels in one
-//                  u16x2 word from LDS-staged row planes, 7-wide sliding window along x1
-//   k_sg_vert<D>   quad of lanes per column (D/4 disparities per lane): 7-row vertical box
-//                  sum as a running sum (clamped to the stripe's first row and to H-1, the
-//                  overlap rule of OpenCV's 4 stripes) fused with the top->down path
-//   k_sg_horiz<D>  quad of lanes per row: left->right path (stores LV), right->left path
+//   k_sg_costvert<D,CB>  block of CB column quads (D/4 disparities per lane) marching down a
+//                  stripe: BT pixel cost of both channels in one u16x2 word from LDS-staged
+//                  rows, 7x7 box sum (7-column sum from LDS, 7-row running sum over a VGPR
+//                  shift register, rows clamped to the stripe's first row and to H-1 -- the
+//                  overlap rule of OpenCV's 4 stripes), fused with the top->down path
+//   k_sg_horiz<D,PF> quad of lanes per row: left->right path (stores LV), right->left path
 //                  fused with S = LV + R, first-minimum WTA, integer parabolic sub-pixel,
-//                  right-view disparity and the pseudo left-right check
+//                  right-view disparity (atomicMin keys) and the pseudo left-right check
 //   k_sg_median    3x3 median (replicated border) -> int16 disparity*16
 // Path states are packed u16x2 VGPRs (v_pk_add/sub/min_u16, v_alignbit for d-1 / d+1);
 // neighbours across the quad come from DPP quad permutes.  Integer arithmetic only;
 // bit-identical to oracle/sgbm_ref.cpp.
+#include <algorithm>
+#include <cstdlib>
+
 #include "fvo_internal.h"
 
 namespace {
@@ -31,6 +35,7 @@ __device__ __forceinline__ u16x2 splat(uint32_t s) { return as_v((s & 0xFFFFu) |
 
 struct SgParams {
   int W, H, D, minD, minX1, width1, P1, P2, ftzero, disp12, ss, ov, nstripes;
+  int HG;  // row groups of 16 (volume layout)
 };
 
 // SGM recurrence for one packed pair k of a lane's disparity run, in place.  `old_km1`
@@ -97,145 +102,6 @@ __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q
 }
 
 
-// ------------------------------------------------------------------ pixel cost + hsum
-// Block = one row segment of 2*kSeg columns x all D disparities; thread (seg, d) slides a
-// 7-wide window along its kSeg columns, so each pixel cost is computed once per window.
-// The BT terms of both channels (x-Sobel, intensity) ride in one u16x2 word:
-// c = min(max(u - v1, v0 - u)^+, max(v - u1, u0 - v)^+) with saturating packed subtracts.
-constexpr int kSeg = 64;
-
-template <int D>
-__global__ __launch_bounds__(2 * D) void k_sg_hsum(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
-                                                   int64_t stride, int pitch, SgParams p,
-                                                   uint16_t* __restrict__ hsum) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t sw[];
-  const int W = p.W;
-  // [0] Lu [1] Lmin [2] Lmax [3] Ru [4] Rmin [5] Rmax, each [W] u16x2 (Sobel, intensity)
-  const int y = blockIdx.y, b = blockIdx.z;
-  const uint8_t* L = Limg + b * stride;
-  const uint8_t* R = Rimg + b * stride;
-  const int ym = y > 0 ? y - 1 : y, yp = y < p.H - 1 ? y + 1 : y;
-  const int ft = p.ftzero;
-  auto clip = [ft](int v) { return min(max(v, -ft), ft) + ft; };
-  auto chan = [&](const uint8_t* img, int x) -> uint32_t {  // (Sobel, intensity) of column x
-    if (x < 1 || x >= W - 1) return (uint32_t)clip(0) * 0x10001u;  // both channels read ftzero
-    const uint8_t* r0 = img + (int64_t)ym * pitch;
-    const uint8_t* r1 = img + (int64_t)y * pitch;
-    const uint8_t* r2 = img + (int64_t)yp * pitch;
-    int s = (r1[x + 1] - r1[x - 1]) * 2 + r0[x + 1] - r0[x - 1] + r2[x + 1] - r2[x - 1];
-    return (uint32_t)clip(s) | ((uint32_t)r1[x] << 16);
-  };
-  for (int x = threadIdx.x; x < W; x += blockDim.x) {
-#pragma unroll
-    for (int side = 0; side < 2; ++side) {
-      const uint8_t* img = side ? R : L;
-      u16x2 u = as_v(chan(img, x));
-      u16x2 ul = x > 0 ? as_v(chan(img, x - 1)) : u, ur = x < W - 1 ? as_v(chan(img, x + 1)) : u;
-      u16x2 hl = (u + ul) >> 1, hr = (u + ur) >> 1;  // (a + b) / 2 of non-negatives
-      if (x == 0) hl = u;
-      if (x == W - 1) hr = u;
-      sw[(3 * side) * W + x] = as_u(u);
-      sw[(3 * side + 1) * W + x] = as_u(vmin(vmin(hl, hr), u));
-      sw[(3 * side + 2) * W + x] = as_u(__builtin_elementwise_max(__builtin_elementwise_max(hl, hr), u));
-    }
-  }
-  __syncthreads();
-  const int d = threadIdx.x % D, seg = threadIdx.x / D;
-  const int x1b = blockIdx.x * (2 * kSeg) + seg * kSeg;
-  if (x1b >= p.width1) return;
-  const uint32_t *Lu = sw, *L0 = sw + W, *L1 = sw + 2 * W, *Ru = sw + 3 * W, *R0 = sw + 4 * W, *R1 = sw + 5 * W;
-  const int dofs = p.minX1 - d - p.minD;  // xr = x1 + dofs >= 0
-  auto pc = [&](int x1) -> int {
-    x1 = min(max(x1, 0), p.width1 - 1);
-    const int x = x1 + p.minX1, xr = x1 + dofs;
-    u16x2 u = as_v(Lu[x]), u0 = as_v(L0[x]), u1 = as_v(L1[x]);
-    u16x2 v = as_v(Ru[xr]), v0 = as_v(R0[xr]), v1 = as_v(R1[xr]);
-    u16x2 c0 = __builtin_elementwise_max(__builtin_elementwise_sub_sat(u, v1), __builtin_elementwise_sub_sat(v0, u));
-    u16x2 c1 = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, u1), __builtin_elementwise_sub_sat(u0, v));
-    uint32_t m = as_u(vmin(c0, c1));
-    return (int)(m & 0xFFFFu) + (int)(m >> 18);
-  };
-  int ring[7];
-  int s = 0;
-#pragma unroll
-  for (int k = 0; k < 7; ++k) { ring[k] = pc(x1b - 3 + k); s += ring[k]; }
-  uint16_t* out = hsum + ((int64_t)b * p.H + y) * p.width1 * D + d;
-#pragma unroll
-  for (int i = 0; i < kSeg; ++i) {
-    if (i > 0) {
-      int nv = pc(x1b + i + 3);
-      s += nv - ring[(i - 1) % 7];
-      ring[(i - 1) % 7] = nv;
-    }
-    if (x1b + i < p.width1) out[(int64_t)(x1b + i) * D] = (uint16_t)s;
-  }
-}
-
-// ------------------------------------------------------------------ vertical sum + top->down
-// Quad per column x1 (lane q holds disparities [q*D/4, (q+1)*D/4)), 16 columns per wave,
-// one block per (16 columns, stripe, pair).  The 7-row vertical box sum is a running sum
-// over the hsum rows, with rows clamped to the stripe's first processed row and to H-1
-// (OpenCV's stripe overlap rule); the top->down path restarts at each stripe's first row.
-template <int D>
-__global__ __launch_bounds__(64) void k_sg_vert(const uint16_t* __restrict__ hsum, uint16_t* __restrict__ Cvol,
-                                                uint16_t* __restrict__ Vvol, SgParams p) {
-  constexpr int DQ = D / 4, PQ = DQ / 2, NV4 = DQ / 8;
-  const int q = threadIdx.x & 3;
-  const int x1 = blockIdx.x * 16 + (threadIdx.x >> 2);
-  const int s = blockIdx.y, b = blockIdx.z;
-  if (x1 >= p.width1) return;  // whole quads leave together
-  const int64_t plane = (int64_t)p.width1 * D;
-  const int H = p.H;
-  const int start = max(min(s * p.ss - p.ov, H), 0);
-  const int end = min((s + 1) * p.ss, H);
-  const int first_out = min(s * p.ss, H);
-  if (start >= end) return;
-  const int64_t colofs = (int64_t)b * H * plane + (int64_t)x1 * D + q * DQ;
-  auto row = [&](int r) { return hsum + colofs + (int64_t)r * plane; };
-  uint32_t crun[PQ], st[PQ], a[PQ], o[PQ], an[PQ], on[PQ];
-  load_run<NV4>(row(start), crun);
-#pragma unroll
-  for (int k = 0; k < PQ; ++k) {
-    u16x2 v = as_v(crun[k]);
-    crun[k] = as_u(v + v + v + v);  // rows start-3..start clamp to start
-  }
-  for (int r = start + 1; r <= start + 3; ++r) {
-    load_run<NV4>(row(min(r, H - 1)), a);
-#pragma unroll
-    for (int k = 0; k < PQ; ++k) crun[k] = as_u(as_v(crun[k]) + as_v(a[k]));
-  }
-#pragma unroll
-  for (int k = 0; k < PQ; ++k) st[k] = 0;
-  if (start + 1 < end) {
-    load_run<NV4>(row(min(start + 4, H - 1)), an);
-    load_run<NV4>(row(start), on);
-  }
-  uint32_t minPrev = 0;
-  const u16x2 P1 = splat(p.P1);
-  for (int y = start; y < end; ++y) {
-    if (y > start) {  // window [y-3, y+3] clamped to [start, H-1]
-#pragma unroll
-      for (int k = 0; k < PQ; ++k) { a[k] = an[k]; o[k] = on[k]; }
-      if (y + 1 < end) {
-        load_run<NV4>(row(min(y + 4, H - 1)), an);
-        load_run<NV4>(row(max(y - 3, start)), on);
-      }
-#pragma unroll
-      for (int k = 0; k < PQ; ++k) crun[k] = as_u(as_v(crun[k]) - as_v(o[k]) + as_v(a[k]));
-    }
-    minPrev = hstep<PQ>(st, crun, q, P1, minPrev, p.P2);
-    if (y >= first_out) {
-      uint4* cp = reinterpret_cast<uint4*>(Cvol + colofs + (int64_t)y * plane);
-      uint4* vp = reinterpret_cast<uint4*>(Vvol + colofs + (int64_t)y * plane);
-#pragma unroll
-      for (int i = 0; i < NV4; ++i) {
-        cp[i] = make_uint4(crun[4 * i], crun[4 * i + 1], crun[4 * i + 2], crun[4 * i + 3]);
-        vp[i] = make_uint4(st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3]);
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------------------ fused cost + vertical pass
 // One block (4 waves) per (64 columns, stripe, pair); quad of lanes per column as in
 // k_sg_vert.  Per new hsum row (the row entering the 7-row window) the block stages the 3
@@ -245,25 +111,24 @@ __global__ __launch_bounds__(64) void k_sg_vert(const uint16_t* __restrict__ hsu
 // 8 hsum rows are a shift register in VGPRs, so the hsum volume never goes to HBM.  The next
 // row's image bytes are fetched before the current row is processed.  Same integer
 // arithmetic as k_sg_hsum + k_sg_vert (order-independent sums).
-constexpr int kCB = 64;           // columns per block
-constexpr int kCX = kCB + 6;      // pixel-cost columns (7-wide box apron)
-
-template <int D>
-__global__ __launch_bounds__(256) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
+template <int D, int CB>
+__global__ __launch_bounds__(4 * CB) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
                                                     int64_t stride, int pitch, SgParams p, uint16_t* __restrict__ Cvol,
                                                     uint16_t* __restrict__ Vvol) {
   constexpr int DQ = D / 4, PQ = DQ / 2, NV4 = DQ / 8;
+  constexpr int NT = 4 * CB;                // threads: a quad per column
+  constexpr int kCX = CB + 6;               // pixel-cost columns (7-wide box apron)
   constexpr int NRC = kCX + D - 1;          // right-image core pixels
   constexpr int NLI = kCX + 4, NRI = NRC + 4;  // staged pixels per image row (core + 2 each side)
   constexpr int NIMG = 3 * (NLI + NRI);     // staged bytes per hsum row
-  constexpr int PER = (NIMG + 255) / 256;   // staged bytes per thread
+  constexpr int PER = (NIMG + NT - 1) / NT;  // staged bytes per thread
   __shared__ uint8_t sImg[3][NLI + NRI];
   __shared__ uint32_t sCh[kCX + 2 + NRC + 2];                       // (Sobel, intensity), L then R
   __shared__ uint32_t sW[3][kCX + NRC];                            // u, BT min, BT max, L then R
   __shared__ __attribute__((aligned(16))) uint16_t sPC[kCX][D];    // pixel cost
   const int tid = threadIdx.x, lane = tid & 63, q = lane & 3;
   const int col = (tid >> 6) * 16 + (lane >> 2);  // 0..63
-  const int c0 = blockIdx.x * kCB;
+  const int c0 = blockIdx.x * CB;
   const int s = blockIdx.y, b = blockIdx.z;
   const int H = p.H, W = p.W;
   const int start = max(min(s * p.ss - p.ov, H), 0);
@@ -273,7 +138,7 @@ __global__ __launch_bounds__(256) void k_sg_costvert(const uint8_t* __restrict__
   const uint8_t* Lb = Limg + b * stride;
   const uint8_t* Rb = Rimg + b * stride;
   const int xl0 = max(c0 - 3, 0) + p.minX1;                    // first left core pixel
-  const int xl1 = min(c0 + kCB + 2, p.width1 - 1) + p.minX1;   // last left core pixel
+  const int xl1 = min(c0 + CB + 2, p.width1 - 1) + p.minX1;   // last left core pixel
   const int nl = xl1 - xl0 + 1;                                // <= kCX
   const int xr0 = xl0 - (D - 1) - p.minD;                      // first right core pixel (>= 1)
   const int nr = nl + D - 1;                                   // <= NRC
@@ -286,7 +151,7 @@ __global__ __launch_bounds__(256) void k_sg_costvert(const uint8_t* __restrict__
     const int rows[3] = {r > 0 ? r - 1 : r, r, r < H - 1 ? r + 1 : r};
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const int i = tid + 256 * k;
+      const int i = tid + NT * k;
       uint8_t v = 0;
       if (i < NIMG) {
         const int rr = i / (NLI + NRI), j = i % (NLI + NRI);
@@ -300,12 +165,12 @@ __global__ __launch_bounds__(256) void k_sg_costvert(const uint8_t* __restrict__
   auto hs_row = [&](uint32_t* acc) {
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const int i = tid + 256 * k;
+      const int i = tid + NT * k;
       if (i < NIMG) (&sImg[0][0])[i] = pre[k];
     }
     __syncthreads();
     // channel words at core-1 .. core+1 of both images; borders (x < 1, x >= W-1) read ftzero
-    for (int j = tid; j < (nl + 2) + (nr + 2); j += 256) {
+    for (int j = tid; j < (nl + 2) + (nr + 2); j += NT) {
       const bool left = j < nl + 2;
       const int k = left ? j : j - (nl + 2);
       const int x = (left ? xl0 : xr0) - 1 + k;
@@ -322,7 +187,7 @@ __global__ __launch_bounds__(256) void k_sg_costvert(const uint8_t* __restrict__
     }
     __syncthreads();
     // BT words: u, min(u, (u+ul)/2, (u+ur)/2), max(...); at x = 0 / W-1 the half is u itself
-    for (int j = tid; j < nl + nr; j += 256) {
+    for (int j = tid; j < nl + nr; j += NT) {
       const bool left = j < nl;
       const int k = left ? j : j - nl;
       const int x = left ? xl0 + k : xr0 + k;
@@ -338,7 +203,7 @@ __global__ __launch_bounds__(256) void k_sg_costvert(const uint8_t* __restrict__
     }
     __syncthreads();
     // pixel costs of the kCX (clamped) columns x D disparities, 8 disparities per task
-    for (int task = tid; task < kCX * (D / 8); task += 256) {
+    for (int task = tid; task < kCX * (D / 8); task += NT) {
       const int i = task / (D / 8), d0 = (task % (D / 8)) * 8;
       const int x1c = min(max(c0 - 3 + i, 0), p.width1 - 1);
       const int kl = x1c + p.minX1 - xl0;
@@ -371,7 +236,8 @@ __global__ __launch_bounds__(256) void k_sg_costvert(const uint8_t* __restrict__
         acc[4 * k + 3] = as_u(as_v(acc[4 * k + 3]) + as_v(w4.w));
       }
     }
-    __syncthreads();  // sImg / sPC are rewritten by the next row
+    // no trailing barrier: the next row's first LDS write (sImg) comes after every thread
+    // has passed this row's later barriers, i.e. finished reading sImg / sCh / sW / sPC
   };
 
   // window shift register: win[k] = hsum(clamp(y - 3 + k)), k = 0..6, for the output row y
@@ -406,7 +272,7 @@ __global__ __launch_bounds__(256) void k_sg_costvert(const uint8_t* __restrict__
   const u16x2 P1 = splat(p.P1);
   const int x1 = c0 + col;
   const int64_t plane = (int64_t)p.width1 * D;
-  const int64_t colofs = (int64_t)b * H * plane + (int64_t)x1 * D + q * DQ;
+  const int64_t colofs = (int64_t)b * p.HG * 16 * plane + (int64_t)x1 * 16 * D + q * DQ;
   for (int y = start; y < end; ++y) {
     if (y > start) {  // window [y-3, y+3] clamped to [start, H-1]: out clamp(y-4), in clamp(y+3)
       uint32_t nw[PQ];
@@ -428,8 +294,9 @@ __global__ __launch_bounds__(256) void k_sg_costvert(const uint8_t* __restrict__
     }
     minPrev = hstep<PQ>(st, crun, q, P1, minPrev, p.P2);
     if (y >= first_out && x1 < p.width1) {
-      uint4* cp = reinterpret_cast<uint4*>(Cvol + colofs + (int64_t)y * plane);
-      uint4* vp = reinterpret_cast<uint4*>(Vvol + colofs + (int64_t)y * plane);
+      const int64_t yo = (int64_t)(y >> 4) * 16 * plane + (y & 15) * D;
+      uint4* cp = reinterpret_cast<uint4*>(Cvol + colofs + yo);
+      uint4* vp = reinterpret_cast<uint4*>(Vvol + colofs + yo);
 #pragma unroll
       for (int i = 0; i < NV4; ++i) {
         cp[i] = make_uint4(crun[4 * i], crun[4 * i + 1], crun[4 * i + 2], crun[4 * i + 3]);
@@ -440,124 +307,160 @@ __global__ __launch_bounds__(256) void k_sg_costvert(const uint8_t* __restrict__
 }
 
 // ------------------------------------------------------------------ horizontal paths + WTA
-// raw / d2 / d2c are stored transposed, [x][row], so the rows of a wave are contiguous.
-template <int D>
+// Quad of lanes per row (16 rows per wave).  raw is stored transposed, [x][row], so the rows
+// of a wave are contiguous.  The right-view disparity of the pseudo left-right check is one
+// 32-bit key per right-image column, (cost << 16) | (0xFFFF - x1), lowered by a
+// fire-and-forget atomicMin: the smallest cost wins and, among equal costs, the largest x1 --
+// the first one the right->left scan visits -- which is the serial rule "replace iff
+// disp2cost > cost" of sgbm_ref.cpp; d + minD = x1 + minX1 - x2 is recovered from x1.  The
+// scan therefore never waits on a load of its own (the old read-modify-write of the right-view
+// cost drained every outstanding load once per column), and the volume loads of both passes
+// run PF columns ahead.
+template <int D, int PF>
 __global__ __launch_bounds__(64) void k_sg_horiz(const uint16_t* __restrict__ Cvol, const uint16_t* __restrict__ Vvol,
                                                  uint16_t* __restrict__ LVvol, int16_t* __restrict__ rawT,
-                                                 int16_t* __restrict__ d2T, int16_t* __restrict__ d2cT, SgParams p) {
+                                                 uint32_t* __restrict__ keyT, SgParams p) {
   constexpr int DQ = D / 4, PQ = DQ / 2, NV4 = DQ / 8;
   const int q = threadIdx.x & 3;
   const int y = blockIdx.x * 16 + (threadIdx.x >> 2);
   const int b = blockIdx.y;
-  const int H = p.H, W = p.W;
+  const int H = p.H, W = p.W, n1 = p.width1;
   if (y >= H) return;  // whole quads leave together
-  const int64_t rowofs = ((int64_t)b * H + y) * p.width1 * D + q * DQ;
+  constexpr int64_t XS = 16 * D;  // x1 stride: the 16 rows of a group are interleaved per column
+  const int64_t rowofs = ((int64_t)b * p.HG + (y >> 4)) * n1 * XS + (y & 15) * D + q * DQ;
+  const uint16_t* Crow = Cvol + rowofs;
+  const uint16_t* Vrow = Vvol + rowofs;
+  uint16_t* LVrow = LVvol + rowofs;
   const u16x2 P1 = splat(p.P1);
   const int INVALID = (p.minD - 1) * 16;
   const int64_t colT = (int64_t)b * W * H + y;  // + x*H
   for (int x = q; x < W; x += 4) {
     rawT[colT + (int64_t)x * H] = (int16_t)INVALID;
-    d2T[colT + (int64_t)x * H] = (int16_t)INVALID;
-    d2cT[colT + (int64_t)x * H] = (int16_t)0x7FFF;
+    keyT[colT + (int64_t)x * H] = 0xFFFFFFFFu;
   }
+  uint32_t st[PQ], cb[PF][PQ], vb[PF][PQ];
   // ---- left -> right: LV = L + V
-  uint32_t st[PQ], c[PQ], v[PQ], cn[PQ], vn[PQ];
 #pragma unroll
   for (int k = 0; k < PQ; ++k) st[k] = 0;
   uint32_t minPrev = 0;
-  load_run<NV4>(Cvol + rowofs, cn);
-  load_run<NV4>(Vvol + rowofs, vn);
-  for (int x1 = 0; x1 < p.width1; ++x1) {
 #pragma unroll
-    for (int k = 0; k < PQ; ++k) { c[k] = cn[k]; v[k] = vn[k]; }
-    if (x1 + 1 < p.width1) {
-      load_run<NV4>(Cvol + rowofs + (int64_t)(x1 + 1) * D, cn);
-      load_run<NV4>(Vvol + rowofs + (int64_t)(x1 + 1) * D, vn);
+  for (int j = 0; j < PF; ++j)
+    if (j < n1) {
+      load_run<NV4>(Crow + (int64_t)j * XS, cb[j]);
+      load_run<NV4>(Vrow + (int64_t)j * XS, vb[j]);
     }
-    minPrev = hstep<PQ>(st, c, q, P1, minPrev, p.P2);
-    uint4* lp = reinterpret_cast<uint4*>(LVvol + rowofs + (int64_t)x1 * D);
+  for (int x0 = 0; x0 < n1; x0 += PF) {
 #pragma unroll
-    for (int i = 0; i < NV4; ++i)
-      lp[i] = make_uint4(as_u(as_v(st[4 * i]) + as_v(v[4 * i])), as_u(as_v(st[4 * i + 1]) + as_v(v[4 * i + 1])),
-                         as_u(as_v(st[4 * i + 2]) + as_v(v[4 * i + 2])), as_u(as_v(st[4 * i + 3]) + as_v(v[4 * i + 3])));
+    for (int j = 0; j < PF; ++j) {
+      const int x1 = x0 + j;
+      if (x1 < n1) {
+        uint32_t c[PQ], v[PQ];
+#pragma unroll
+        for (int k = 0; k < PQ; ++k) { c[k] = cb[j][k]; v[k] = vb[j][k]; }
+        if (x1 + PF < n1) {
+          load_run<NV4>(Crow + (int64_t)(x1 + PF) * XS, cb[j]);
+          load_run<NV4>(Vrow + (int64_t)(x1 + PF) * XS, vb[j]);
+        }
+        minPrev = hstep<PQ>(st, c, q, P1, minPrev, p.P2);
+        uint4* lp = reinterpret_cast<uint4*>(LVrow + (int64_t)x1 * XS);
+#pragma unroll
+        for (int i = 0; i < NV4; ++i)
+          lp[i] = make_uint4(as_u(as_v(st[4 * i]) + as_v(v[4 * i])), as_u(as_v(st[4 * i + 1]) + as_v(v[4 * i + 1])),
+                             as_u(as_v(st[4 * i + 2]) + as_v(v[4 * i + 2])), as_u(as_v(st[4 * i + 3]) + as_v(v[4 * i + 3])));
+      }
+    }
   }
-  __syncthreads();  // init stores above vs. the quad leader's read-modify-writes below
-  // ---- right -> left, S = LV + R, first-minimum WTA, sub-pixel, right-view disparity
+  // the initialisation stores above have completed before the quad leaders' atomics / stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // ---- right -> left, S = LV + R, first-minimum WTA, sub-pixel, right-view key
 #pragma unroll
   for (int k = 0; k < PQ; ++k) st[k] = 0;
   minPrev = 0;
-  load_run<NV4>(Cvol + rowofs + (int64_t)(p.width1 - 1) * D, cn);
-  load_run<NV4>(LVvol + rowofs + (int64_t)(p.width1 - 1) * D, vn);
-  for (int x1 = p.width1 - 1; x1 >= 0; --x1) {
 #pragma unroll
-    for (int k = 0; k < PQ; ++k) { c[k] = cn[k]; v[k] = vn[k]; }
-    if (x1 > 0) {
-      load_run<NV4>(Cvol + rowofs + (int64_t)(x1 - 1) * D, cn);
-      load_run<NV4>(LVvol + rowofs + (int64_t)(x1 - 1) * D, vn);
+  for (int j = 0; j < PF; ++j)
+    if (j < n1) {
+      load_run<NV4>(Crow + (int64_t)(n1 - 1 - j) * XS, cb[j]);
+      load_run<NV4>(LVrow + (int64_t)(n1 - 1 - j) * XS, vb[j]);
     }
-    minPrev = hstep<PQ>(st, c, q, P1, minPrev, p.P2);
-    // local first-minimum over this lane's run, with its S neighbours
-    int best = 0x7FFFFFFF, bd = 0, sm1 = 0, sp1 = 0, prevv = 0;
-    bool cap = false;
-    uint32_t sFirst = 0, sLast = 0;
+  for (int i0 = 0; i0 < n1; i0 += PF) {
 #pragma unroll
-    for (int k = 0; k < PQ; ++k) {
-      uint32_t S = as_u(as_v(v[k]) + as_v(st[k]));
-      if (k == 0) sFirst = S & 0xFFFFu;
-      if (k == PQ - 1) sLast = S >> 16;
+    for (int j = 0; j < PF; ++j) {
+      const int i = i0 + j, x1 = n1 - 1 - i;
+      if (i < n1) {
+        uint32_t c[PQ], v[PQ];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        int sv = h ? (int)(S >> 16) : (int)(S & 0xFFFFu);
-        if (cap) { sp1 = sv; cap = false; }
-        if (sv < best) { best = sv; bd = 2 * k + h; sm1 = prevv; cap = true; }
-        prevv = sv;
-      }
-    }
-    const int fromPrev = (int)qperm<kQPrev>(sLast), fromNext = (int)qperm<kQNext>(sFirst);
-    if (bd == 0) sm1 = fromPrev;
-    if (bd == DQ - 1) sp1 = fromNext;
-    bd += q * DQ;
-    // quad reduction: smaller cost wins, ties go to the smaller disparity
+        for (int k = 0; k < PQ; ++k) { c[k] = cb[j][k]; v[k] = vb[j][k]; }
+        if (i + PF < n1) {
+          load_run<NV4>(Crow + (int64_t)(x1 - PF) * XS, cb[j]);
+          load_run<NV4>(LVrow + (int64_t)(x1 - PF) * XS, vb[j]);
+        }
+        minPrev = hstep<PQ>(st, c, q, P1, minPrev, p.P2);
+        // local first-minimum over this lane's run, with its S neighbours
+        int best = 0x7FFFFFFF, bd = 0, sm1 = 0, sp1 = 0, prevv = 0;
+        bool cap = false;
+        uint32_t sFirst = 0, sLast = 0;
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      int ob, od, om, op;
-      if (r == 0) {
-        ob = (int)qperm<kQX1>(best); od = (int)qperm<kQX1>(bd); om = (int)qperm<kQX1>(sm1); op = (int)qperm<kQX1>(sp1);
-      } else {
-        ob = (int)qperm<kQX2>(best); od = (int)qperm<kQX2>(bd); om = (int)qperm<kQX2>(sm1); op = (int)qperm<kQX2>(sp1);
-      }
-      if (ob < best || (ob == best && od < bd)) { best = ob; bd = od; sm1 = om; sp1 = op; }
-    }
-    if (q == 0) {
-      const int d = bd;
-      const int x2 = x1 + p.minX1 - d - p.minD;
-      if (x2 >= 0 && x2 < W) {
-        int64_t i2 = colT + (int64_t)x2 * H;
-        if ((int)d2cT[i2] > best) {
-          d2cT[i2] = (int16_t)best;
-          d2T[i2] = (int16_t)(d + p.minD);
+        for (int k = 0; k < PQ; ++k) {
+          uint32_t S = as_u(as_v(v[k]) + as_v(st[k]));
+          if (k == 0) sFirst = S & 0xFFFFu;
+          if (k == PQ - 1) sLast = S >> 16;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            int sv = h ? (int)(S >> 16) : (int)(S & 0xFFFFu);
+            if (cap) { sp1 = sv; cap = false; }
+            if (sv < best) { best = sv; bd = 2 * k + h; sm1 = prevv; cap = true; }
+            prevv = sv;
+          }
+        }
+        const int fromPrev = (int)qperm<kQPrev>(sLast), fromNext = (int)qperm<kQNext>(sFirst);
+        if (bd == 0) sm1 = fromPrev;
+        if (bd == DQ - 1) sp1 = fromNext;
+        bd += q * DQ;
+        // quad reduction: smaller cost wins, ties go to the smaller disparity
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          int ob, od, om, op;
+          if (r == 0) {
+            ob = (int)qperm<kQX1>(best); od = (int)qperm<kQX1>(bd); om = (int)qperm<kQX1>(sm1); op = (int)qperm<kQX1>(sp1);
+          } else {
+            ob = (int)qperm<kQX2>(best); od = (int)qperm<kQX2>(bd); om = (int)qperm<kQX2>(sm1); op = (int)qperm<kQX2>(sp1);
+          }
+          if (ob < best || (ob == best && od < bd)) { best = ob; bd = od; sm1 = om; sp1 = op; }
+        }
+        if (q == 0) {
+          const int d = bd;
+          const int x2 = x1 + p.minX1 - d - p.minD;
+          if (x2 >= 0 && x2 < W && best < 0x7FFF)  // disp2cost starts at SHRT_MAX
+            atomicMin(&keyT[colT + (int64_t)x2 * H], ((uint32_t)best << 16) | (uint32_t)(0xFFFF - x1));
+          int dd;
+          if (0 < d && d < D - 1) {
+            int denom2 = max(sm1 + sp1 - 2 * best, 1);
+            dd = d * 16 + ((sm1 - sp1) * 16 + denom2) / (denom2 * 2);
+          } else {
+            dd = d * 16;
+          }
+          rawT[colT + (int64_t)(x1 + p.minX1) * H] = (int16_t)(dd + p.minD * 16);
         }
       }
-      int dd;
-      if (0 < d && d < D - 1) {
-        int denom2 = max(sm1 + sp1 - 2 * best, 1);
-        dd = d * 16 + ((sm1 - sp1) * 16 + denom2) / (denom2 * 2);
-      } else {
-        dd = d * 16;
-      }
-      rawT[colT + (int64_t)(x1 + p.minX1) * H] = (int16_t)(dd + p.minD * 16);
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // ---- pseudo left-right consistency check, columns split over the quad
-  for (int x = p.minX1 + q; x < p.minX1 + p.width1; x += 4) {
-    int64_t ix = colT + (int64_t)x * H;
-    int d1 = rawT[ix];
+  // ---- pseudo left-right consistency check, columns split over the quad; the keys are read
+  // from L2 (the atomics were performed there)
+  auto disp2 = [&](int x2) -> int {
+    const uint32_t k = __hip_atomic_load(keyT + colT + (int64_t)x2 * H, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return k == 0xFFFFFFFFu ? INVALID : (int)(0xFFFFu - (k & 0xFFFFu)) + p.minX1 - x2;
+  };
+  for (int x = p.minX1 + q; x < p.minX1 + n1; x += 4) {
+    const int64_t ix = colT + (int64_t)x * H;
+    const int d1 = rawT[ix];
     if (d1 == INVALID) continue;
-    int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
-    int _x = x - _d, x_ = x - d_;
+    const int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
+    const int _x = x - _d, x_ = x - d_;
     if (0 <= x_ && x_ < W && 0 <= _x && _x < W) {
-      int a = d2T[colT + (int64_t)x_ * H], cc = d2T[colT + (int64_t)_x * H];
+      const int a = disp2(x_), cc = disp2(_x);
       if (a >= p.minD && abs(a - d_) > p.disp12 && cc >= p.minD && abs(cc - _d) > p.disp12) rawT[ix] = (int16_t)INVALID;
     }
   }
@@ -604,22 +507,61 @@ SgParams make_params(const fvo_config& c) {
   p.nstripes = c.sgbm_stripes;
   p.ss = (int)std::ceil(c.height / (double)p.nstripes);
   p.ov = (c.block_size / 2 + 1) + (int)std::ceil(0.1 * p.ss);
+  p.HG = (c.height + 15) / 16;
   return p;
+}
+
+// Experiment / tuning knobs (read per launch): FVO_SG_CB columns per cost block (16/32/64),
+// FVO_SG_PF horizontal-pass prefetch depth (1/2/4), FVO_SG_CHUNKS batch chunks alternated
+// over the caller's stream and a second stream (cost pass of one chunk overlaps the
+// HBM-bound horizontal pass of the other).  All variants are bit-identical.
+int env_int(const char* name, int def) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : def;
+}
+
+template <int D>
+void launch_chunk(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_t* R, int nb, int64_t stride,
+                  int pitch, uint16_t* C, uint16_t* V, uint16_t* LV, int16_t* raw, uint32_t* key, int16_t* disp,
+                  int cb, int pf, hipStream_t s) {
+  const dim3 gcv((p.width1 + cb - 1) / cb, p.nstripes, nb);
+  FVO_TIMED(ctx, KN_SG_VERT, s, {
+    if (cb == 16) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 16>), gcv, dim3(64), 0, s, L, R, stride, pitch, p, C, V);
+    else if (cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, C, V);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 64>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, C, V);
+  });
+  const dim3 ghz((p.H + 15) / 16, nb);
+  FVO_TIMED(ctx, KN_SG_HORIZ, s, {
+    if (pf == 1) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_horiz<D, 1>), ghz, dim3(64), 0, s, C, V, LV, raw, key, p);
+    else if (pf == 4) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_horiz<D, 4>), ghz, dim3(64), 0, s, C, V, LV, raw, key, p);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_horiz<D, 2>), ghz, dim3(64), 0, s, C, V, LV, raw, key, p);
+  });
+  FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.H + 255) / 256, p.W, nb), dim3(256), 0, s,
+                                                     raw, disp, p.W, p.H));
 }
 
 template <int D>
 void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_t* R, int batch, int64_t stride,
                  int pitch, int16_t* disp, hipStream_t s) {
-  uint16_t* C = ctx->sg_L;
-  uint16_t* V = ctx->sg_V;
-  uint16_t* LV = ctx->sg_cost;
-  FVO_TIMED(ctx, KN_SG_VERT, s,
-            hipLaunchKernelGGL(k_sg_costvert<D>, dim3((p.width1 + kCB - 1) / kCB, p.nstripes, batch), dim3(256), 0, s,
-                               L, R, stride, pitch, p, C, V));
-  FVO_TIMED(ctx, KN_SG_HORIZ, s, hipLaunchKernelGGL(k_sg_horiz<D>, dim3((p.H + 15) / 16, batch), dim3(64), 0, s, C, V,
-                                                    LV, ctx->sg_raw, ctx->sg_d2, ctx->sg_d2c, p));
-  FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.H + 255) / 256, p.W, batch), dim3(256), 0, s,
-                                                     ctx->sg_raw, disp, p.W, p.H));
+  const int cb = env_int("FVO_SG_CB", 64), pf = env_int("FVO_SG_PF", 1);
+  const int nch = std::max(1, std::min(env_int("FVO_SG_CHUNKS", 1), batch));
+  const int64_t vol = (int64_t)p.HG * 16 * p.width1 * D, img = (int64_t)p.H * p.W;
+  if (nch > 1) {
+    (void)hipEventRecord(ctx->sg_fork, s);
+    (void)hipStreamWaitEvent(ctx->sg_s2, ctx->sg_fork, 0);
+  }
+  for (int k = 0; k < nch; ++k) {
+    const int b0 = (int)((int64_t)batch * k / nch), b1 = (int)((int64_t)batch * (k + 1) / nch);
+    if (b1 <= b0) continue;
+    hipStream_t sk = (k & 1) ? ctx->sg_s2 : s;
+    launch_chunk<D>(ctx, p, L + b0 * stride, R + b0 * stride, b1 - b0, stride, pitch, ctx->sg_L + b0 * vol,
+                    ctx->sg_V + b0 * vol, ctx->sg_cost + b0 * vol, ctx->sg_raw + b0 * img, ctx->sg_d2 + b0 * img,
+                    disp + b0 * img, cb, pf, sk);
+  }
+  if (nch > 1) {
+    (void)hipEventRecord(ctx->sg_join, ctx->sg_s2);
+    (void)hipStreamWaitEvent(s, ctx->sg_join, 0);
+  }
 }
 
 }  // namespace
@@ -635,11 +577,15 @@ int sgbm_init(fvo_ctx* ctx) {
   if (p.width1 <= 0) return fvo_fail(ctx, "SGBM: image narrower than numDisparities");
   const int64_t B = c.max_batch, plane = (int64_t)p.width1 * p.D;
   int rc;
-  // sg_cost: hsum, then reused for L; sg_L: C; sg_V: V  (each B * H * plane u16)
-  if ((rc = fvo_alloc(ctx, &ctx->sg_cost, B * p.H * plane)) || (rc = fvo_alloc(ctx, &ctx->sg_L, B * p.H * plane)) ||
-      (rc = fvo_alloc(ctx, &ctx->sg_V, B * p.H * plane)) || (rc = fvo_alloc(ctx, &ctx->sg_raw, B * p.H * p.W)) ||
-      (rc = fvo_alloc(ctx, &ctx->sg_d2, B * p.H * p.W)) || (rc = fvo_alloc(ctx, &ctx->sg_d2c, B * p.H * p.W)))
+  // sg_L: C, sg_V: V, sg_cost: LV = L + V; each [B][HG][width1][16][D] u16
+  const int64_t vol = (int64_t)p.HG * 16 * plane;
+  if ((rc = fvo_alloc(ctx, &ctx->sg_cost, B * vol)) || (rc = fvo_alloc(ctx, &ctx->sg_L, B * vol)) ||
+      (rc = fvo_alloc(ctx, &ctx->sg_V, B * vol)) || (rc = fvo_alloc(ctx, &ctx->sg_raw, B * p.H * p.W)) ||
+      (rc = fvo_alloc(ctx, &ctx->sg_d2, B * p.H * p.W)))
     return rc;
+  FVO_HIP(ctx, hipStreamCreateWithFlags(&ctx->sg_s2, hipStreamNonBlocking));
+  FVO_HIP(ctx, hipEventCreateWithFlags(&ctx->sg_fork, hipEventDisableTiming));
+  FVO_HIP(ctx, hipEventCreateWithFlags(&ctx->sg_join, hipEventDisableTiming));
   return 0;
 }
 

@@ -251,3 +251,27 @@ def test_overlapped_sgbm_stream_matches_serial(frames):
         outs.append([(T.cpu().numpy().copy(), st.cpu().numpy().copy()) for T, st in res])
     for (Ta, sa), (Tb, sb) in zip(*outs):
         assert np.array_equal(sa, sb) and np.array_equal(Ta, Tb)
+
+
+@pytest.fixture(scope="module")
+def sgbm_ref(oracle_mod, frames):
+    return [oracle_mod.sgbm(L, R) for L, R in frames]
+
+
+@pytest.mark.parametrize("cb,pf,chunks", [(64, 1, 1), (32, 2, 2), (16, 4, 3), (64, 4, 2)])
+def test_sgbm_variants_bit_exact(frames, sgbm_ref, monkeypatch, cb, pf, chunks):
+    """Every SGBM launch variant (columns per cost block, horizontal prefetch depth, batch
+    chunks pipelined over two streams) is bit-identical to the oracle."""
+    from forest_slam_amd import _lib
+    monkeypatch.setenv("FVO_SG_CB", str(cb))
+    monkeypatch.setenv("FVO_SG_PF", str(pf))
+    monkeypatch.setenv("FVO_SG_CHUNKS", str(chunks))
+    ctx = _lib.Context(960, 600, max_batch=len(frames))
+    L = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
+    R = torch.from_numpy(np.stack([f[1] for f in frames])).cuda()
+    d = ctx.sgbm(L, R)
+    torch.cuda.synchronize()
+    d = d.cpu().numpy()
+    for i, want in enumerate(sgbm_ref):
+        bad = np.argwhere(d[i] != want)
+        assert len(bad) == 0, f"pair {i}: {len(bad)} px differ, first {bad[:5]}"

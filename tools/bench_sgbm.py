@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""SGBM alone on the GPU: B=64 synthetic 960x600 pairs, per-kernel times (HIP events) and
+the whole-call time, for the launch variant selected by FVO_SG_CB / FVO_SG_PF /
+FVO_SG_CHUNKS.  Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    from forest_slam_amd import _lib, synth
+    B, W, H = int(os.environ.get("B", "64")), 960, 600
+    seq = synth.StereoSequence(seed=0, n_frames=B, W=W, H=H, device="cuda")
+    L, R = seq.frames(range(B))
+    ctx = _lib.Context(W, H, max_batch=B, stages=_lib.STAGE_SGBM)
+    out = torch.empty((B, H, W), dtype=torch.int16, device="cuda")
+    for _ in range(2):
+        ctx.sgbm(L, R, out=out)
+    torch.cuda.synchronize()
+    n = 5
+    t0 = time.perf_counter()
+    for _ in range(n):
+        ctx.sgbm(L, R, out=out)
+    torch.cuda.synchronize()
+    call_ms = (time.perf_counter() - t0) / n * 1e3
+    ctx.timing_enable(None)
+    for _ in range(n):
+        ctx.sgbm(L, R, out=out)
+    torch.cuda.synchronize()
+    st = {k: round(v[0] / n, 4) for k, v in ctx.timing_read().items()}
+    ctx.timing_enable([])
+    var = {k: os.environ.get(k, "") for k in ("FVO_SG_CB", "FVO_SG_PF", "FVO_SG_CHUNKS")}
+    print(json.dumps({"variant": var, "call_ms": round(call_ms, 3), "kernels_ms": st}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
