@@ -79,9 +79,9 @@ struct fvo_ctx {
   int32_t* bf_sdist = nullptr;
   int32_t* bf_tidx = nullptr;
   // SGBM workspace
-  uint16_t* sg_cost = nullptr;  // hsum [B][H][width1][D], then the left->right pass L [B][width1][D/8][H]x8
-  uint16_t* sg_L = nullptr;     // cost C [B][width1][D/8][H]x8
-  uint16_t* sg_V = nullptr;     // top-down pass V [B][width1][D/8][H]x8
+  uint16_t* sg_cost = nullptr;  // LV = left->right pass + V, [B][HG][width1][16][D] (16-row groups)
+  uint16_t* sg_L = nullptr;     // cost C, same layout
+  uint16_t* sg_V = nullptr;     // top-down pass V, same layout
   int16_t* sg_raw = nullptr;    // [B][W][H] pre-median disparity (transposed)
   uint32_t* sg_d2 = nullptr;    // [B][W][H] right-view key (cost << 16 | 0xFFFF - x1), pseudo LR check
   hipStream_t sg_s2 = nullptr;  // second stream for chunked (pipelined) SGBM batches
@@ -89,7 +89,7 @@ struct fvo_ctx {
   // pose workspace
   double* pnp_hyp = nullptr;      // [B][cap][2] normalised inlier points (refinement)
   int32_t* pnp_sub = nullptr;     // [B][cap] inlier indices
-  int16_t* pnp_subsets = nullptr; // [B][max_iters][5] RANSAC subsets
+  int16_t* pnp_subsets = nullptr; // [cap+1][max_iters][5] RANSAC subsets per point count
   double* pnp_models = nullptr;   // [B][max_iters][6] hypotheses (rvec, tvec)
   int32_t* pnp_good = nullptr;    // [B][max_iters] inlier counts
   void* pnp_state = nullptr;      // [B] PnpState

@@ -208,6 +208,37 @@ __device__ void dsvd_ws(const double* A, double* W, double* U, double* V, double
   }
 }
 
+// SPD 6x6 solve by Cholesky for the LM step (JtJ with the (1 + lambda) diagonal).  Returns
+// false when a pivot is not clearly positive (pivot^2 below 1e-12 of the largest diagonal
+// entry): the caller then takes OpenCV's DECOMP_SVD path (dsolve), which also handles the
+// rank-deficient case.  On well-conditioned systems both give the same step to rounding.
+__device__ bool chol_solve6(const double* A, const double* b, double* x) {
+  double L[6][6], y[6], dmax = 0.0;
+  for (int i = 0; i < 6; ++i) dmax = fmax(dmax, A[i * 6 + i]);
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j <= i; ++j) {
+      double s = A[i * 6 + j];
+      for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
+      if (i == j) {
+        if (!(s > 1e-12 * dmax)) return false;
+        L[i][i] = sqrt(s);
+      } else {
+        L[i][j] = s / L[j][j];
+      }
+    }
+  for (int i = 0; i < 6; ++i) {
+    double s = b[i];
+    for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
+    y[i] = s / L[i][i];
+  }
+  for (int i = 5; i >= 0; --i) {
+    double s = y[i];
+    for (int k = i + 1; k < 6; ++k) s -= L[k][i] * x[k];
+    x[i] = s / L[i][i];
+  }
+  return true;
+}
+
 template <int M, int N>
 __device__ void dsolve(const double* A, const double* b, double* x) {
   double W[N], U[M * N], V[N * N], tmp[N];
@@ -899,7 +930,7 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
       double A[36], x[6];
       for (int i = 0; i < 36; ++i) A[i] = JtJ[i];
       for (int i = 0; i < 6; ++i) A[i * 6 + i] *= 1. + lambda;
-      dsolve<6, 6>(A, JtErr, x);
+      if (!chol_solve6(A, JtErr, x)) dsolve<6, 6>(A, JtErr, x);
       for (int i = 0; i < 6; ++i) sh.param[i] = prev[i] - x[i];
     }
     __syncthreads();
@@ -939,10 +970,18 @@ struct PnpState {
 };
 
 // Subsets of every potential RANSAC iteration, drawn exactly as getSubset() with
-// RNG(-1): 5 distinct indices from rng.uniform(0, n) with rejection of repeats.  The
-// draws depend only on n, so they can be generated before any hypothesis is scored.
+// RNG(-1): 5 distinct indices from rng.uniform(0, n) with rejection of repeats.  The draws
+// depend only on the point count n (solvePnPRansac seeds a fresh RNG(-1) per call), so the
+// table of every n in [6, cap] is drawn once when the context is created (one thread per n)
+// and a frame's hypotheses read row n of it.
+__global__ void k_pnp_table(int cap, int maxIters, int16_t* __restrict__ table) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n < 6 || n > cap) return;
+  fvo_rs::draw_subsets(n, maxIters, table + (int64_t)n * maxIters * 5);
+}
+
 __global__ void k_pnp_subsets(const int32_t* __restrict__ npts, int batch, int cap, int maxIters,
-                              int16_t* __restrict__ sub, PnpState* __restrict__ state) {
+                              PnpState* __restrict__ state) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= batch) return;
   int n = npts[b];
@@ -953,8 +992,6 @@ __global__ void k_pnp_subsets(const int32_t* __restrict__ npts, int batch, int c
   st.best_it = -1;
   st.n = n;
   state[b] = st;
-  if (n < 6) return;
-  fvo_rs::draw_subsets(n, maxIters, sub + (int64_t)b * maxIters * 5);
 }
 
 // One lane per RANSAC iteration: EPnP on its subset (undistorted, float32-rounded
@@ -963,7 +1000,8 @@ __global__ void k_pnp_subsets(const int32_t* __restrict__ npts, int batch, int c
 // first iteration is past the frame's current iteration bound exit immediately.
 __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ P3all, const float* __restrict__ p2all,
                                                 int cap, Cam K, float thr2, int maxIters, int it_lo,
-                                                const int16_t* __restrict__ sub, const PnpState* __restrict__ state,
+                                                const int16_t* __restrict__ table, int table_iters,
+                                                const PnpState* __restrict__ state,
                                                 double* __restrict__ model, int32_t* __restrict__ good) {
   extern __shared__ __attribute__((aligned(16))) double smem[];  // [144][64] EPnP MtM (one column per lane)
   double* su = smem;
@@ -977,7 +1015,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ P3all,
   // (scalar loads), so they take no LDS and leave room for two waves per CU
   const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
   const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
-  const int16_t* sb = sub + ((int64_t)b * maxIters + it) * 5;
+  const int16_t* sb = table + ((int64_t)n * table_iters + it) * 5;
   EPnPd<5> e;
   e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
   for (int i = 0; i < 5; ++i) {
@@ -1101,9 +1139,14 @@ int pose_init(fvo_ctx* ctx) {
   const int64_t B = ctx->cfg.max_batch, n = B * ctx->kp_cap, it = B * ctx->pnp_max_iters;
   int rc;
   if ((rc = fvo_alloc(ctx, &ctx->pnp_sub, n)) || (rc = fvo_alloc(ctx, &ctx->pnp_hyp, 2 * n)) ||
-      (rc = fvo_alloc(ctx, &ctx->pnp_subsets, it * 5)) || (rc = fvo_alloc(ctx, &ctx->pnp_models, it * 6)) ||
+      (rc = fvo_alloc(ctx, &ctx->pnp_subsets, (int64_t)(ctx->kp_cap + 1) * ctx->pnp_max_iters * 5)) ||
+      (rc = fvo_alloc(ctx, &ctx->pnp_models, it * 6)) ||
       (rc = fvo_alloc(ctx, &ctx->pnp_good, it)) || (rc = fvo_alloc(ctx, (PnpState**)&ctx->pnp_state, B)))
     return rc;
+  hipLaunchKernelGGL(k_pnp_table, dim3((ctx->kp_cap + 1 + 63) / 64), dim3(64), 0, 0, ctx->kp_cap, ctx->pnp_max_iters,
+                     ctx->pnp_subsets);
+  FVO_LAUNCH_CHECK(ctx);
+  FVO_HIP(ctx, hipDeviceSynchronize());
   return 0;
 }
 
@@ -1131,15 +1174,15 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
     FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_pnp_hyp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   const int first = std::min(maxIters, 128);
   FVO_TIMED(ctx, KN_PNP, s, {
-    hipLaunchKernelGGL(k_pnp_subsets, dim3((batch + 63) / 64), dim3(64), 0, s, npts, batch, cap, maxIters,
-                       ctx->pnp_subsets, st);
+    hipLaunchKernelGGL(k_pnp_subsets, dim3((batch + 63) / 64), dim3(64), 0, s, npts, batch, cap, maxIters, st);
     hipLaunchKernelGGL(k_pnp_hyp, dim3((first + 63) / 64, batch), dim3(64), shm, s, P3, p2, cap, c, thr2, maxIters, 0,
-                       ctx->pnp_subsets, st, ctx->pnp_models, ctx->pnp_good);
+                       ctx->pnp_subsets, ctx->pnp_max_iters, st, ctx->pnp_models, ctx->pnp_good);
     hipLaunchKernelGGL(k_pnp_replay, dim3((batch + 63) / 64), dim3(64), 0, s, batch, maxIters, 0, first, conf,
                        ctx->pnp_good, st);
     if (maxIters > first) {
       hipLaunchKernelGGL(k_pnp_hyp, dim3((maxIters - first + 63) / 64, batch), dim3(64), shm, s, P3, p2, cap, c, thr2,
-                         maxIters, first, ctx->pnp_subsets, st, ctx->pnp_models, ctx->pnp_good);
+                         maxIters, first, ctx->pnp_subsets, ctx->pnp_max_iters, st, ctx->pnp_models,
+                         ctx->pnp_good);
       hipLaunchKernelGGL(k_pnp_replay, dim3((batch + 63) / 64), dim3(64), 0, s, batch, maxIters, first, maxIters, conf,
                          ctx->pnp_good, st);
     }
