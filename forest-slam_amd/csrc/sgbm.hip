@@ -81,6 +81,45 @@ __device__ __forceinline__ void load_run(const uint16_t* base, uint32_t* out) {
   }
 }
 
+// One step of a path over a lane's run with G lanes per column (G = 4: quad; G = 8: half
+// row, neighbours by DPP row shifts, minimum by two quad steps + row_half_mirror); returns
+// the group-wide minimum.
+template <int PQ, int G>
+__device__ __forceinline__ uint32_t hstepG(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
+                                           uint32_t P2) {
+  uint32_t prevLast, nextFirst;
+  if (G == 4) {
+    prevLast = qperm<kQPrev>(st[PQ - 1]);
+    nextFirst = qperm<kQNext>(st[0]);
+  } else {
+    prevLast = (uint32_t)__builtin_amdgcn_mov_dpp((int)st[PQ - 1], 0x111, 0xF, 0xF, false);  // row_shr:1
+    nextFirst = (uint32_t)__builtin_amdgcn_mov_dpp((int)st[0], 0x101, 0xF, 0xF, false);      // row_shl:1
+  }
+  const uint32_t lo0 = q == 0 ? (kSent << 16) : prevLast;
+  const uint32_t hiN = q == G - 1 ? kSent : nextFirst;
+  const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
+  u16x2 mn = splat(0xFFFF);
+  uint32_t oldk = 0;
+#pragma unroll
+  for (int k = 0; k < PQ; ++k) mn = vmin(mn, as_v(sgm_pair<PQ>(st, k, oldk, c[k], P1, mp2, mpv, lo0, hiN)));
+  uint32_t m = as_u(mn);
+  m = min(m & 0xFFFFu, m >> 16);
+  m = min(m, qperm<kQX1>(m));
+  m = min(m, qperm<kQX2>(m));
+  if (G == 8) m = min(m, (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  return m;
+}
+
+template <int NV2>
+__device__ __forceinline__ void load_run2(const uint16_t* base, uint32_t* out) {
+  const uint2* p2 = reinterpret_cast<const uint2*>(base);
+#pragma unroll
+  for (int i = 0; i < NV2; ++i) {
+    uint2 q = p2[i];
+    out[2 * i] = q.x; out[2 * i + 1] = q.y;
+  }
+}
+
 // One step of a horizontal path over a lane's run; returns the quad-wide minimum.
 template <int PQ>
 __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
@@ -111,12 +150,12 @@ __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q
 // 8 hsum rows are a shift register in VGPRs, so the hsum volume never goes to HBM.  The next
 // row's image bytes are fetched before the current row is processed.  Same integer
 // arithmetic as k_sg_hsum + k_sg_vert (order-independent sums).
-template <int D, int CB>
-__global__ __launch_bounds__(4 * CB) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
+template <int D, int CB, int G>
+__global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
                                                     int64_t stride, int pitch, SgParams p, uint16_t* __restrict__ Cvol,
                                                     uint16_t* __restrict__ Vvol) {
-  constexpr int DQ = D / 4, PQ = DQ / 2, NV4 = DQ / 8;
-  constexpr int NT = 4 * CB;                // threads: a quad per column
+  constexpr int DQ = D / G, PQ = DQ / 2, NV2 = DQ / 4;
+  constexpr int NT = G * CB;                // threads: G lanes per column
   constexpr int kCX = CB + 6;               // pixel-cost columns (7-wide box apron)
   constexpr int NRC = kCX + D - 1;          // right-image core pixels
   constexpr int NLI = kCX + 4, NRI = NRC + 4;  // staged pixels per image row (core + 2 each side)
@@ -126,8 +165,8 @@ __global__ __launch_bounds__(4 * CB) void k_sg_costvert(const uint8_t* __restric
   __shared__ uint32_t sCh[kCX + 2 + NRC + 2];                       // (Sobel, intensity), L then R
   __shared__ uint32_t sW[3][kCX + NRC];                            // u, BT min, BT max, L then R
   __shared__ __attribute__((aligned(16))) uint16_t sPC[kCX][D];    // pixel cost
-  const int tid = threadIdx.x, lane = tid & 63, q = lane & 3;
-  const int col = (tid >> 6) * 16 + (lane >> 2);  // 0..63
+  const int tid = threadIdx.x, lane = tid & 63, q = lane % G;
+  const int col = (tid >> 6) * (64 / G) + lane / G;  // 0..CB-1
   const int c0 = blockIdx.x * CB;
   const int s = blockIdx.y, b = blockIdx.z;
   const int H = p.H, W = p.W;
@@ -226,14 +265,12 @@ __global__ __launch_bounds__(4 * CB) void k_sg_costvert(const uint8_t* __restric
     for (int k = 0; k < PQ; ++k) acc[k] = 0;
 #pragma unroll
     for (int t = 0; t < 7; ++t) {
-      const uint4* src = reinterpret_cast<const uint4*>(&sPC[col + t][q * DQ]);
+      const uint2* src = reinterpret_cast<const uint2*>(&sPC[col + t][q * DQ]);
 #pragma unroll
-      for (int k = 0; k < NV4; ++k) {
-        const uint4 w4 = src[k];
-        acc[4 * k] = as_u(as_v(acc[4 * k]) + as_v(w4.x));
-        acc[4 * k + 1] = as_u(as_v(acc[4 * k + 1]) + as_v(w4.y));
-        acc[4 * k + 2] = as_u(as_v(acc[4 * k + 2]) + as_v(w4.z));
-        acc[4 * k + 3] = as_u(as_v(acc[4 * k + 3]) + as_v(w4.w));
+      for (int k = 0; k < NV2; ++k) {
+        const uint2 w2 = src[k];
+        acc[2 * k] = as_u(as_v(acc[2 * k]) + as_v(w2.x));
+        acc[2 * k + 1] = as_u(as_v(acc[2 * k + 1]) + as_v(w2.y));
       }
     }
     // no trailing barrier: the next row's first LDS write (sImg) comes after every thread
@@ -292,15 +329,15 @@ __global__ __launch_bounds__(4 * CB) void k_sg_costvert(const uint8_t* __restric
 #pragma unroll
       for (int j = 0; j < PQ; ++j) win[6][j] = nw[j];
     }
-    minPrev = hstep<PQ>(st, crun, q, P1, minPrev, p.P2);
+    minPrev = hstepG<PQ, G>(st, crun, q, P1, minPrev, p.P2);
     if (y >= first_out && x1 < p.width1) {
       const int64_t yo = (int64_t)(y >> 4) * 16 * plane + (y & 15) * D;
-      uint4* cp = reinterpret_cast<uint4*>(Cvol + colofs + yo);
-      uint4* vp = reinterpret_cast<uint4*>(Vvol + colofs + yo);
+      uint2* cp = reinterpret_cast<uint2*>(Cvol + colofs + yo);
+      uint2* vp = reinterpret_cast<uint2*>(Vvol + colofs + yo);
 #pragma unroll
-      for (int i = 0; i < NV4; ++i) {
-        cp[i] = make_uint4(crun[4 * i], crun[4 * i + 1], crun[4 * i + 2], crun[4 * i + 3]);
-        vp[i] = make_uint4(st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3]);
+      for (int i = 0; i < NV2; ++i) {
+        cp[i] = make_uint2(crun[2 * i], crun[2 * i + 1]);
+        vp[i] = make_uint2(st[2 * i], st[2 * i + 1]);
       }
     }
   }
@@ -316,13 +353,13 @@ __global__ __launch_bounds__(4 * CB) void k_sg_costvert(const uint8_t* __restric
 // scan therefore never waits on a load of its own (the old read-modify-write of the right-view
 // cost drained every outstanding load once per column), and the volume loads of both passes
 // run PF columns ahead.
-template <int D, int PF>
+template <int D, int PF, int G>
 __global__ __launch_bounds__(64) void k_sg_horiz(const uint16_t* __restrict__ Cvol, const uint16_t* __restrict__ Vvol,
                                                  uint16_t* __restrict__ LVvol, int16_t* __restrict__ rawT,
                                                  uint32_t* __restrict__ keyT, SgParams p) {
-  constexpr int DQ = D / 4, PQ = DQ / 2, NV4 = DQ / 8;
-  const int q = threadIdx.x & 3;
-  const int y = blockIdx.x * 16 + (threadIdx.x >> 2);
+  constexpr int DQ = D / G, PQ = DQ / 2, NV2 = DQ / 4;
+  const int q = threadIdx.x % G;
+  const int y = blockIdx.x * (64 / G) + threadIdx.x / G;
   const int b = blockIdx.y;
   const int H = p.H, W = p.W, n1 = p.width1;
   if (y >= H) return;  // whole quads leave together
@@ -334,7 +371,7 @@ __global__ __launch_bounds__(64) void k_sg_horiz(const uint16_t* __restrict__ Cv
   const u16x2 P1 = splat(p.P1);
   const int INVALID = (p.minD - 1) * 16;
   const int64_t colT = (int64_t)b * W * H + y;  // + x*H
-  for (int x = q; x < W; x += 4) {
+  for (int x = q; x < W; x += G) {
     rawT[colT + (int64_t)x * H] = (int16_t)INVALID;
     keyT[colT + (int64_t)x * H] = 0xFFFFFFFFu;
   }
@@ -346,8 +383,8 @@ __global__ __launch_bounds__(64) void k_sg_horiz(const uint16_t* __restrict__ Cv
 #pragma unroll
   for (int j = 0; j < PF; ++j)
     if (j < n1) {
-      load_run<NV4>(Crow + (int64_t)j * XS, cb[j]);
-      load_run<NV4>(Vrow + (int64_t)j * XS, vb[j]);
+      load_run2<NV2>(Crow + (int64_t)j * XS, cb[j]);
+      load_run2<NV2>(Vrow + (int64_t)j * XS, vb[j]);
     }
   for (int x0 = 0; x0 < n1; x0 += PF) {
 #pragma unroll
@@ -358,15 +395,14 @@ __global__ __launch_bounds__(64) void k_sg_horiz(const uint16_t* __restrict__ Cv
 #pragma unroll
         for (int k = 0; k < PQ; ++k) { c[k] = cb[j][k]; v[k] = vb[j][k]; }
         if (x1 + PF < n1) {
-          load_run<NV4>(Crow + (int64_t)(x1 + PF) * XS, cb[j]);
-          load_run<NV4>(Vrow + (int64_t)(x1 + PF) * XS, vb[j]);
+          load_run2<NV2>(Crow + (int64_t)(x1 + PF) * XS, cb[j]);
+          load_run2<NV2>(Vrow + (int64_t)(x1 + PF) * XS, vb[j]);
         }
-        minPrev = hstep<PQ>(st, c, q, P1, minPrev, p.P2);
-        uint4* lp = reinterpret_cast<uint4*>(LVrow + (int64_t)x1 * XS);
+        minPrev = hstepG<PQ, G>(st, c, q, P1, minPrev, p.P2);
+        uint2* lp = reinterpret_cast<uint2*>(LVrow + (int64_t)x1 * XS);
 #pragma unroll
-        for (int i = 0; i < NV4; ++i)
-          lp[i] = make_uint4(as_u(as_v(st[4 * i]) + as_v(v[4 * i])), as_u(as_v(st[4 * i + 1]) + as_v(v[4 * i + 1])),
-                             as_u(as_v(st[4 * i + 2]) + as_v(v[4 * i + 2])), as_u(as_v(st[4 * i + 3]) + as_v(v[4 * i + 3])));
+        for (int i = 0; i < NV2; ++i)
+          lp[i] = make_uint2(as_u(as_v(st[2 * i]) + as_v(v[2 * i])), as_u(as_v(st[2 * i + 1]) + as_v(v[2 * i + 1])));
       }
     }
   }
@@ -380,8 +416,8 @@ __global__ __launch_bounds__(64) void k_sg_horiz(const uint16_t* __restrict__ Cv
 #pragma unroll
   for (int j = 0; j < PF; ++j)
     if (j < n1) {
-      load_run<NV4>(Crow + (int64_t)(n1 - 1 - j) * XS, cb[j]);
-      load_run<NV4>(LVrow + (int64_t)(n1 - 1 - j) * XS, vb[j]);
+      load_run2<NV2>(Crow + (int64_t)(n1 - 1 - j) * XS, cb[j]);
+      load_run2<NV2>(LVrow + (int64_t)(n1 - 1 - j) * XS, vb[j]);
     }
   for (int i0 = 0; i0 < n1; i0 += PF) {
 #pragma unroll
@@ -392,10 +428,10 @@ __global__ __launch_bounds__(64) void k_sg_horiz(const uint16_t* __restrict__ Cv
 #pragma unroll
         for (int k = 0; k < PQ; ++k) { c[k] = cb[j][k]; v[k] = vb[j][k]; }
         if (i + PF < n1) {
-          load_run<NV4>(Crow + (int64_t)(x1 - PF) * XS, cb[j]);
-          load_run<NV4>(LVrow + (int64_t)(x1 - PF) * XS, vb[j]);
+          load_run2<NV2>(Crow + (int64_t)(x1 - PF) * XS, cb[j]);
+          load_run2<NV2>(LVrow + (int64_t)(x1 - PF) * XS, vb[j]);
         }
-        minPrev = hstep<PQ>(st, c, q, P1, minPrev, p.P2);
+        minPrev = hstepG<PQ, G>(st, c, q, P1, minPrev, p.P2);
         // local first-minimum over this lane's run, with its S neighbours
         int best = 0x7FFFFFFF, bd = 0, sm1 = 0, sp1 = 0, prevv = 0;
         bool cap = false;
@@ -413,18 +449,22 @@ __global__ __launch_bounds__(64) void k_sg_horiz(const uint16_t* __restrict__ Cv
             prevv = sv;
           }
         }
-        const int fromPrev = (int)qperm<kQPrev>(sLast), fromNext = (int)qperm<kQNext>(sFirst);
+        const int fromPrev = G == 4 ? (int)qperm<kQPrev>(sLast) : __builtin_amdgcn_mov_dpp((int)sLast, 0x111, 0xF, 0xF, false);
+        const int fromNext = G == 4 ? (int)qperm<kQNext>(sFirst) : __builtin_amdgcn_mov_dpp((int)sFirst, 0x101, 0xF, 0xF, false);
         if (bd == 0) sm1 = fromPrev;
         if (bd == DQ - 1) sp1 = fromNext;
         bd += q * DQ;
-        // quad reduction: smaller cost wins, ties go to the smaller disparity
+        // group reduction: smaller cost wins, ties go to the smaller disparity
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
+        for (int r = 0; r < (G == 8 ? 3 : 2); ++r) {
           int ob, od, om, op;
           if (r == 0) {
             ob = (int)qperm<kQX1>(best); od = (int)qperm<kQX1>(bd); om = (int)qperm<kQX1>(sm1); op = (int)qperm<kQX1>(sp1);
-          } else {
+          } else if (r == 1) {
             ob = (int)qperm<kQX2>(best); od = (int)qperm<kQX2>(bd); om = (int)qperm<kQX2>(sm1); op = (int)qperm<kQX2>(sp1);
+          } else {  // row_half_mirror: the other quad of the 8 lanes
+            ob = __builtin_amdgcn_mov_dpp(best, 0x141, 0xF, 0xF, false); od = __builtin_amdgcn_mov_dpp(bd, 0x141, 0xF, 0xF, false);
+            om = __builtin_amdgcn_mov_dpp(sm1, 0x141, 0xF, 0xF, false); op = __builtin_amdgcn_mov_dpp(sp1, 0x141, 0xF, 0xF, false);
           }
           if (ob < best || (ob == best && od < bd)) { best = ob; bd = od; sm1 = om; sp1 = op; }
         }
@@ -453,7 +493,7 @@ __global__ __launch_bounds__(64) void k_sg_horiz(const uint16_t* __restrict__ Cv
     const uint32_t k = __hip_atomic_load(keyT + colT + (int64_t)x2 * H, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return k == 0xFFFFFFFFu ? INVALID : (int)(0xFFFFu - (k & 0xFFFFu)) + p.minX1 - x2;
   };
-  for (int x = p.minX1 + q; x < p.minX1 + n1; x += 4) {
+  for (int x = p.minX1 + q; x < p.minX1 + n1; x += G) {
     const int64_t ix = colT + (int64_t)x * H;
     const int d1 = rawT[ix];
     if (d1 == INVALID) continue;
@@ -511,7 +551,9 @@ SgParams make_params(const fvo_config& c) {
   return p;
 }
 
-// Experiment / tuning knobs (read per launch): FVO_SG_CB columns per cost block (16/32/64),
+// Experiment / tuning knobs (read per launch): FVO_SG_G lanes per column in the cost pass
+// (4 or 8), FVO_SG_CB columns per cost block (G=4: 32/64; G=8: 16/32), FVO_SG_HG lanes per
+// row in the horizontal pass (4 or 8),
 // FVO_SG_PF horizontal-pass prefetch depth (1/2/4), FVO_SG_CHUNKS batch chunks alternated
 // over the caller's stream and a second stream (cost pass of one chunk overlaps the
 // HBM-bound horizontal pass of the other).  All variants are bit-identical.
@@ -523,18 +565,22 @@ int env_int(const char* name, int def) {
 template <int D>
 void launch_chunk(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_t* R, int nb, int64_t stride,
                   int pitch, uint16_t* C, uint16_t* V, uint16_t* LV, int16_t* raw, uint32_t* key, int16_t* disp,
-                  int cb, int pf, hipStream_t s) {
+                  int cb, int g, int pf, hipStream_t s) {
   const dim3 gcv((p.width1 + cb - 1) / cb, p.nstripes, nb);
   FVO_TIMED(ctx, KN_SG_VERT, s, {
-    if (cb == 16) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 16>), gcv, dim3(64), 0, s, L, R, stride, pitch, p, C, V);
-    else if (cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, C, V);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 64>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, C, V);
+    if (g == 8 && cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 8>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, C, V);
+    else if (g == 8) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 16, 8>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, C, V);
+    else if (cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 4>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, C, V);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 64, 4>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, C, V);
   });
-  const dim3 ghz((p.H + 15) / 16, nb);
+  const int hg = env_int("FVO_SG_HG", 4);
+  const dim3 ghz(hg == 8 ? (p.H + 7) / 8 : (p.H + 15) / 16, nb);
   FVO_TIMED(ctx, KN_SG_HORIZ, s, {
-    if (pf == 1) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_horiz<D, 1>), ghz, dim3(64), 0, s, C, V, LV, raw, key, p);
-    else if (pf == 4) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_horiz<D, 4>), ghz, dim3(64), 0, s, C, V, LV, raw, key, p);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_horiz<D, 2>), ghz, dim3(64), 0, s, C, V, LV, raw, key, p);
+    if (hg == 8 && pf == 2) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_horiz<D, 2, 8>), ghz, dim3(64), 0, s, C, V, LV, raw, key, p);
+    else if (hg == 8) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_horiz<D, 1, 8>), ghz, dim3(64), 0, s, C, V, LV, raw, key, p);
+    else if (pf == 2) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_horiz<D, 2, 4>), ghz, dim3(64), 0, s, C, V, LV, raw, key, p);
+    else if (pf == 4) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_horiz<D, 4, 4>), ghz, dim3(64), 0, s, C, V, LV, raw, key, p);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_horiz<D, 1, 4>), ghz, dim3(64), 0, s, C, V, LV, raw, key, p);
   });
   FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.H + 255) / 256, p.W, nb), dim3(256), 0, s,
                                                      raw, disp, p.W, p.H));
@@ -543,7 +589,7 @@ void launch_chunk(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8
 template <int D>
 void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_t* R, int batch, int64_t stride,
                  int pitch, int16_t* disp, hipStream_t s) {
-  const int cb = env_int("FVO_SG_CB", 64), pf = env_int("FVO_SG_PF", 1);
+  const int g = env_int("FVO_SG_G", 8), cb = env_int("FVO_SG_CB", g == 8 ? 32 : 64), pf = env_int("FVO_SG_PF", 1);
   const int nch = std::max(1, std::min(env_int("FVO_SG_CHUNKS", 1), batch));
   const int64_t vol = (int64_t)p.HG * 16 * p.width1 * D, img = (int64_t)p.H * p.W;
   if (nch > 1) {
@@ -556,7 +602,7 @@ void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_
     hipStream_t sk = (k & 1) ? ctx->sg_s2 : s;
     launch_chunk<D>(ctx, p, L + b0 * stride, R + b0 * stride, b1 - b0, stride, pitch, ctx->sg_L + b0 * vol,
                     ctx->sg_V + b0 * vol, ctx->sg_cost + b0 * vol, ctx->sg_raw + b0 * img, ctx->sg_d2 + b0 * img,
-                    disp + b0 * img, cb, pf, sk);
+                    disp + b0 * img, cb, g, pf, sk);
   }
   if (nch > 1) {
     (void)hipEventRecord(ctx->sg_join, ctx->sg_s2);

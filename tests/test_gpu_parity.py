@@ -258,12 +258,16 @@ def sgbm_ref(oracle_mod, frames):
     return [oracle_mod.sgbm(L, R) for L, R in frames]
 
 
-@pytest.mark.parametrize("cb,pf,chunks", [(64, 1, 1), (32, 2, 2), (16, 4, 3), (64, 4, 2)])
-def test_sgbm_variants_bit_exact(frames, sgbm_ref, monkeypatch, cb, pf, chunks):
-    """Every SGBM launch variant (columns per cost block, horizontal prefetch depth, batch
-    chunks pipelined over two streams) is bit-identical to the oracle."""
+@pytest.mark.parametrize("g,cb,hg,pf,chunks", [(4, 64, 4, 1, 1), (4, 32, 4, 2, 2), (8, 32, 8, 1, 1), (8, 16, 8, 2, 3),
+                                                (8, 32, 4, 4, 2)])
+def test_sgbm_variants_bit_exact(frames, sgbm_ref, monkeypatch, g, cb, hg, pf, chunks):
+    """Every SGBM launch variant (lanes per column and columns per block of the cost pass,
+    horizontal prefetch depth, batch chunks pipelined over two streams) is bit-identical to
+    the oracle."""
     from forest_slam_amd import _lib
+    monkeypatch.setenv("FVO_SG_G", str(g))
     monkeypatch.setenv("FVO_SG_CB", str(cb))
+    monkeypatch.setenv("FVO_SG_HG", str(hg))
     monkeypatch.setenv("FVO_SG_PF", str(pf))
     monkeypatch.setenv("FVO_SG_CHUNKS", str(chunks))
     ctx = _lib.Context(960, 600, max_batch=len(frames))
