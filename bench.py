@@ -143,6 +143,8 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=4, help="CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-ate", type=int, default=1, help="ATE of the CPU reference path on the ATE frames")
     ap.add_argument("--overlap-sgbm", type=int, default=1, help="SGBM of step k+1 on a side stream during step k")
+    ap.add_argument("--ba-max-landmarks", type=int, default=0, help="per-window landmark cap (0 = library default)")
+    ap.add_argument("--ba-max-obs", type=int, default=0, help="per-window observation cap (0 = library default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -168,8 +170,9 @@ def main():
     seq = synth.StereoSequence(seed=rank, n_frames=B + 1, W=W, H=H, device=dev)
     L_all, R_all = seq.frames(range(B + 1))
     torch.cuda.synchronize()
+    ba_caps = {k: v for k, v in (("ba_max_landmarks", args.ba_max_landmarks), ("ba_max_obs", args.ba_max_obs)) if v}
     fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=B, nfeatures=args.nfeatures, device=dev,
-                           ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm))
+                           ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm), **ba_caps)
     fe.prime(L_all[0], R_all[0])
     Lb, Rb = L_all[1:].contiguous(), R_all[1:].contiguous()
 
@@ -243,7 +246,7 @@ def main():
         aseq = synth.StereoSequence(seed=100, n_frames=args.ate_frames, W=W, H=H, device=dev)
         La, Ra = aseq.frames(range(aseq.n))
         afe = vo.StereoFrontEnd(W, H, aseq.K, synth.DIST_L, synth.BASELINE, batch=min(B, 32),
-                                nfeatures=args.nfeatures, device=dev, ba_window=args.ba_window)
+                                nfeatures=args.nfeatures, device=dev, ba_window=args.ba_window, **ba_caps)
         gt = ev.tum_rows(aseq.t, aseq.T_wc)
         # the estimate is the camera trajectory in the first camera's frame; Sim(3)-align
         rows, _, st = vo.run_sequence(afe, La, Ra, aseq.t, use_ba=True)
@@ -268,6 +271,8 @@ def main():
     if rank == 0 and world == 1 and args.cpu_frames > 0:
         cpu = cpu_baseline(args.cpu_frames, args.nfeatures, W, H)
 
+    cfg_name = ("configs[1]" if (W, H, args.nfeatures) == (960, 600, 1000) else
+                "configs[4] (1080p, 2000 kp, BA window 20)" if (W, H) == (1920, 1080) else "custom")
     if rank == 0:
         out = {
             "metric": "stereo frames/sec (extract+match+local-BA) at 600p, 1/8 MI355X; ATE RMSE",
@@ -284,7 +289,7 @@ def main():
                      "BA Schur GEMM on MFMA), f64 (PnP, BA)",
             "data": "synthetic: ray-cast forest stereo along the 1018_00 GT path (seed = rank), "
                     "BotanicGarden bag not available",
-            "config": {"workload": "stereo VO front end, configs[1]: 960x600, ORB nfeatures=1000, "
+            "config": {"workload": f"stereo VO front end, {cfg_name}: {W}x{H}, ORB nfeatures={args.nfeatures}, "
                                    "BF-Hamming xcheck (L+R), SGBM-3way 96 disp, back-projection, PnP-RANSAC"
                                    + (f", local BA K={args.ba_window}" if args.ba_window else ""),
                        "frames_per_step_per_gpu": B, "width": W, "height": H, "nfeatures": args.nfeatures,

@@ -26,10 +26,10 @@ class FvoConfig(ctypes.Structure):
             "nlevels", "edge_threshold", "first_level", "wta_k", "score_type", "patch_size", "fast_threshold",
             "min_disparity", "num_disparities", "block_size", "P1", "P2", "disp12_max_diff", "pre_filter_cap",
             "uniqueness_ratio", "sgbm_stripes", "kp_capacity", "stages", "ba_window", "ba_max_landmarks",
-            "ba_max_obs")]
+            "ba_max_obs", "sgbm_max_batch")]
 
 
-ABI_VERSION = 3  # FVO_ABI_VERSION of include/fvo.h
+ABI_VERSION = 4  # FVO_ABI_VERSION of include/fvo.h
 STAGE_ORB, STAGE_BF, STAGE_SGBM, STAGE_POSE, STAGE_BA, STAGE_MONO = 1, 2, 4, 8, 16, 32
 
 # name -> (restype, argtypes); mirrors include/fvo.h

@@ -53,6 +53,7 @@ void fvo_config_default(fvo_config* c, int32_t width, int32_t height) {
   c->ba_window = 10;
   c->ba_max_landmarks = 4096;
   c->ba_max_obs = 32768;
+  c->sgbm_max_batch = 0;
 }
 
 static void release(fvo_ctx* c) {
@@ -151,6 +152,8 @@ int fvo_sgbm(fvo_ctx* c, const uint8_t* left, const uint8_t* right, int32_t batc
   if (batch == 0) return 0;
   if (!left || !right || !disparity) return fvo_fail(c, "null pointer argument");
   if (pitch < c->cfg.width || image_stride < (int64_t)pitch * c->cfg.height) return fvo_fail(c, "bad pitch/stride");
+  if (batch > (c->cfg.sgbm_max_batch > 0 ? c->cfg.sgbm_max_batch : c->cfg.max_batch))
+    return fvo_fail(c, "batch exceeds sgbm_max_batch");
   return sgbm_run(c, left, right, batch, image_stride, pitch, disparity, (hipStream_t)stream);
 }
 

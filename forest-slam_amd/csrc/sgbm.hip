@@ -621,7 +621,8 @@ int sgbm_init(fvo_ctx* ctx) {
   if (c.sgbm_stripes < 1) return fvo_fail(ctx, "SGBM: stripes must be >= 1");
   SgParams p = make_params(c);
   if (p.width1 <= 0) return fvo_fail(ctx, "SGBM: image narrower than numDisparities");
-  const int64_t B = c.max_batch, plane = (int64_t)p.width1 * p.D;
+  const int64_t B = c.sgbm_max_batch > 0 ? std::min(c.sgbm_max_batch, c.max_batch) : c.max_batch;
+  const int64_t plane = (int64_t)p.width1 * p.D;
   int rc;
   // sg_L: C, sg_V: V, sg_cost: LV = L + V; each [B][HG][width1][16][D] u16
   const int64_t vol = (int64_t)p.HG * 16 * plane;

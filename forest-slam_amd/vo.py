@@ -41,6 +41,7 @@ class StereoFrontEnd:
         if self.ba_window:
             stages |= _lib.STAGE_BA
             params.setdefault("ba_window", self.ba_window)
+        params.setdefault("sgbm_max_batch", batch)  # SGBM runs on the step's B pairs (ORB on 2B images)
         self.ctx = _lib.Context(width, height, max_batch=2 * batch, device=device, nfeatures=nfeatures,
                                 stages=stages, **params)
         self.dev = self.ctx.device

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define FVO_ABI_VERSION 3
+#define FVO_ABI_VERSION 4
 
 typedef struct fvo_ctx fvo_ctx;
 typedef void* fvo_stream; /* hipStream_t */
@@ -85,6 +85,8 @@ typedef struct fvo_config {
   int32_t ba_window;        /* frames per BA window K (10); max 21 */
   int32_t ba_max_landmarks; /* per-window landmark cap (4096) */
   int32_t ba_max_obs;       /* per-window observation cap (32768) */
+  int32_t sgbm_max_batch;   /* max pairs per fvo_sgbm call (0 = max_batch): the SGBM cost
+                               volumes (3 x ~100 MB per pair at 600p) are sized by it */
 } fvo_config;
 
 /* fvo_config.stages: a context only serves the stages it was created for (e.g. a
