@@ -45,6 +45,11 @@ struct BaCam {
 
 constexpr int kKMax = 21;
 constexpr int kBlock = 256;
+// k_ba_lin: blocks per window; block p reduces the landmark chunks p, p + kLinParts, ... into
+// one partial Schur product (MFMA accumulators kept across its chunks), so k_ba_solve sums
+// kLinParts partials instead of one per chunk.  Fixed chunk order: deterministic.
+constexpr int kLinParts = 16;
+constexpr int kLinMaxTiles = 9;  // 16x16 tiles per wave: 36 upper tiles at NR = 128 / 4 waves
 constexpr double kD2Mono = 5.991, kD2Stereo = 7.815, kMinZ = 0.01, kLam0 = 1e-3;
 
 struct BaState {
@@ -56,7 +61,7 @@ struct BaState {
 };
 
 struct BaDims {
-  int Lmax, Omax, K, cap, NR, LPC, NCH, NCU;
+  int Lmax, Omax, K, cap, NR, LPC, NCH, NCU, NPART;
   int64_t oSt, oX0, oX1, oL, oG, oLs, oObs, oFl, oW, oGp, oCp, oNext, oHdr, win;
 };
 
@@ -458,51 +463,99 @@ __global__ __launch_bounds__(kBlock) void k_ba_pp(BaIn in, void* ws, BaDims dm, 
   }
 }
 
-// landmark blocks of a chunk + its share of the reduced camera system on MFMA
+// landmark blocks of a window's chunks + their share of the reduced camera system on MFMA
+// (tile k of the enumeration I <= J over the pose rows and the z column goes to wave k & 3)
+__device__ __forceinline__ void lin_tile(int k, int ntu, int NT, int& I, int& J) {
+  int idx = 0;
+  for (int i = 0; i < ntu; ++i)
+    for (int j = i; j < NT; ++j) {
+      if (j >= ntu && j != NT - 1) continue;
+      if (idx++ == k) { I = i; J = j; return; }
+    }
+  I = J = -1;
+}
+
 __global__ __launch_bounds__(kBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm, BaCam cam) {
-  extern __shared__ double sY[];  // [3 LPC][NR + 2]
+  extern __shared__ double sY[];  // [3 LPC][NR + 2], then per-observation terms, then L factors
   const BaWin v = view(ws, dm, blockIdx.x);
   const BaState* S = v.st;
   if (!S->active) return;
-  const int L = S->L, c = blockIdx.y, LPC = dm.LPC;
-  if (c * LPC >= L) return;
+  const int L = S->L, part = blockIdx.y, LPC = dm.LPC;
+  double* sHg = sY + 3 * LPC * (dm.NR + 2);  // [LPC * K][9]
+  double* sLf = sHg + 9 * LPC * dm.K;        // [LPC][6]
+  if (part * LPC >= L) return;  // no chunk for this partial (k_ba_solve sums only the used ones)
   const int n = S->n;
   const int np = 6 * (n - 1);
   const int NR = dm.NR, NRP = NR + 2, rows = 3 * LPC;
   const double lam = S->lam;
   const double* X = cur_X(v, S);
-  for (int i = threadIdx.x; i < rows * NRP; i += kBlock) sY[i] = 0.0;
-  __syncthreads();
-  const int t = threadIdx.x, l = c * LPC + t;
-  if (t < LPC && l < L) {
-    const int o0 = v.lstart[l], o1 = v.lstart[l + 1];
-    double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-    for (int oi = o0; oi < o1; ++oi) {
-      const BaObs o = v.obs[oi];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int NT = NR / 16, ntu = (np + 15) / 16;  // tiles covering the pose rows
+  int ntiles = 0;
+  for (int i = 0; i < ntu; ++i) ntiles += (ntu - i) + (ntu < NT ? 1 : 0);
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  d4 acc[kLinMaxTiles][2];
+#pragma unroll
+  for (int lt = 0; lt < kLinMaxTiles; ++lt) acc[lt][0] = acc[lt][1] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int c = part; c * LPC < L; c += dm.NPART) {
+    for (int i = threadIdx.x; i < rows * NRP; i += kBlock) sY[i] = 0.0;
+    __syncthreads();
+    // the chunk's observations are contiguous (landmark-major): [ob0, ob1)
+    const int lc0 = c * LPC, lc1 = min(L, lc0 + LPC);
+    const int ob0 = v.lstart[lc0], nob = v.lstart[lc1] - ob0;
+    // (a) per observation: its landmark-block terms w Jl^T Jl (upper 6) and w Jl^T r (3)
+    for (int i = threadIdx.x; i < nob; i += kBlock) {
+      const BaObs o = v.obs[ob0 + i];
       double r[3], w, rho, Jp[3][6], Jl[3][3];
-      ba_eval<true>(S->T[o.frame], X + 3 * l, o, cam, obs_is2(in, o), r, w, rho, Jp, Jl);
+      ba_eval<true>(S->T[o.frame], X + 3 * o.lm, o, cam, obs_is2(in, o), r, w, rho, Jp, Jl);
+      double* hg = sHg + 9 * i;
       int q = 0;
       for (int a = 0; a < 3; ++a) {
-        for (int b = a; b < 3; ++b) H[q++] += w * (Jl[0][a] * Jl[0][b] + Jl[1][a] * Jl[1][b] + Jl[2][a] * Jl[2][b]);
-        g[a] += w * (Jl[0][a] * r[0] + Jl[1][a] * r[1] + Jl[2][a] * r[2]);
+        for (int b = a; b < 3; ++b) hg[q++] = w * (Jl[0][a] * Jl[0][b] + Jl[1][a] * Jl[1][b] + Jl[2][a] * Jl[2][b]);
+        hg[6 + a] = w * (Jl[0][a] * r[0] + Jl[1][a] * r[1] + Jl[2][a] * r[2]);
       }
     }
-    // damped Cholesky of [H0 H1 H2; . H3 H4; . . H5]
-    const double a00 = H[0] + lam * H[0] + 1e-6, a11 = H[3] + lam * H[3] + 1e-6, a22 = H[5] + lam * H[5] + 1e-6;
-    const double l00 = sqrt(a00);
-    const double l10 = H[1] / l00, l20 = H[2] / l00;
-    const double l11 = sqrt(a11 - l10 * l10);
-    const double l21 = (H[4] - l20 * l10) / l11;
-    const double l22 = sqrt(a22 - l20 * l20 - l21 * l21);
-    double* Lf = v.Lf + 6 * l;
-    Lf[0] = l00; Lf[1] = l10; Lf[2] = l11; Lf[3] = l20; Lf[4] = l21; Lf[5] = l22;
-    v.gl[3 * l] = g[0]; v.gl[3 * l + 1] = g[1]; v.gl[3 * l + 2] = g[2];
-    double* Y0 = sY + 3 * t * NRP;
-    for (int oi = o0; oi < o1; ++oi) {
-      const int f = v.obs[oi].frame;
+    __syncthreads();
+    // (b) per landmark: the terms summed in observation order, damped Cholesky, z = L^-1 g
+    const int t = threadIdx.x, l = lc0 + t;
+    if (t < LPC && l < L) {
+      const int o0 = v.lstart[l], o1 = v.lstart[l + 1];
+      double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+      for (int oi = o0; oi < o1; ++oi) {
+        const double* hg = sHg + 9 * (oi - ob0);
+        for (int q = 0; q < 6; ++q) H[q] += hg[q];
+        for (int a = 0; a < 3; ++a) g[a] += hg[6 + a];
+      }
+      // damped Cholesky of [H0 H1 H2; . H3 H4; . . H5]
+      const double a00 = H[0] + lam * H[0] + 1e-6, a11 = H[3] + lam * H[3] + 1e-6, a22 = H[5] + lam * H[5] + 1e-6;
+      const double l00 = sqrt(a00);
+      const double l10 = H[1] / l00, l20 = H[2] / l00;
+      const double l11 = sqrt(a11 - l10 * l10);
+      const double l21 = (H[4] - l20 * l10) / l11;
+      const double l22 = sqrt(a22 - l20 * l20 - l21 * l21);
+      double* Lf = v.Lf + 6 * l;
+      Lf[0] = l00; Lf[1] = l10; Lf[2] = l11; Lf[3] = l20; Lf[4] = l21; Lf[5] = l22;
+      double* sl = sLf + 6 * t;
+      sl[0] = l00; sl[1] = l10; sl[2] = l11; sl[3] = l20; sl[4] = l21; sl[5] = l22;
+      v.gl[3 * l] = g[0]; v.gl[3 * l + 1] = g[1]; v.gl[3 * l + 2] = g[2];
+      double* Y0 = sY + 3 * t * NRP;
+      const double z0 = g[0] / l00, z1 = (g[1] - l10 * z0) / l11, z2 = (g[2] - l20 * z0 - l21 * z1) / l22;
+      Y0[NR - 1] = z0;
+      Y0[NRP + NR - 1] = z1;
+      Y0[2 * NRP + NR - 1] = z2;
+    }
+    __syncthreads();
+    // (c) per observation: rows 6 (f-1) .. 6 (f-1) + 5 of W L^-T (solve L y = W_p)
+    for (int i = threadIdx.x; i < nob; i += kBlock) {
+      const BaObs o = v.obs[ob0 + i];
+      const int f = o.frame;
       if (f == 0) continue;
-      const double* Wo = v.W + (int64_t)oi * 18;
-      for (int p = 0; p < 6; ++p) {  // row p of W L^-T: solve L y = W_p
+      const int tl = o.lm - lc0;
+      const double* sl = sLf + 6 * tl;
+      const double l00 = sl[0], l10 = sl[1], l11 = sl[2], l20 = sl[3], l21 = sl[4], l22 = sl[5];
+      const double* Wo = v.W + (int64_t)(ob0 + i) * 18;
+      double* Y0 = sY + 3 * tl * NRP;
+      for (int p = 0; p < 6; ++p) {
         const double y0 = Wo[3 * p] / l00;
         const double y1 = (Wo[3 * p + 1] - l10 * y0) / l11;
         const double y2 = (Wo[3 * p + 2] - l20 * y0 - l21 * y1) / l22;
@@ -512,33 +565,36 @@ __global__ __launch_bounds__(kBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm,
         Y0[2 * NRP + col] = y2;
       }
     }
-    const double z0 = g[0] / l00, z1 = (g[1] - l10 * z0) / l11, z2 = (g[2] - l20 * z0 - l21 * z1) / l22;
-    Y0[NR - 1] = z0;
-    Y0[NRP + NR - 1] = z1;
-    Y0[2 * NRP + NR - 1] = z2;
-  }
-  __syncthreads();
-  // G_chunk = Yt^T Yt on MFMA, upper 16x16 tiles that intersect the np x np system or
-  // its z column; A[i][k] = Yt[k][16I + i], B[k][j] = Yt[k][16J + j], lane holds k = lane >> 4
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int NT = NR / 16, ntu = (np + 15) / 16;  // tiles covering the pose rows
-  double* Gc = v.Gp + (int64_t)c * NR * NR;
-  typedef double d4 __attribute__((ext_vector_type(4)));
-  int pidx = 0;
-  for (int I = 0; I < ntu; ++I)
-    for (int J = I; J < NT; ++J) {
-      if (J >= ntu && J != NT - 1) continue;  // only the z column beyond the pose rows
-      if ((pidx++ & 3) != wid) continue;
-      d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-      const double* ya = sY + (lane >> 4) * NRP + 16 * I + (lane & 15);
-      const double* yb = sY + (lane >> 4) * NRP + 16 * J + (lane & 15);
-      for (int k0 = 0; k0 < rows; k0 += 8) {
-        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[k0 * NRP], yb[k0 * NRP], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[(k0 + 4) * NRP], yb[(k0 + 4) * NRP], acc1, 0, 0, 0);
+    __syncthreads();
+    // G += Yt^T Yt on MFMA: A[i][k] = Yt[k][16I + i], B[k][j] = Yt[k][16J + j], lane holds k = lane >> 4
+#pragma unroll
+    for (int lt = 0; lt < kLinMaxTiles; ++lt) {
+      const int k = 4 * lt + wid;
+      if (k < ntiles) {
+        int I, J;
+        lin_tile(k, ntu, NT, I, J);
+        const double* ya = sY + (lane >> 4) * NRP + 16 * I + (lane & 15);
+        const double* yb = sY + (lane >> 4) * NRP + 16 * J + (lane & 15);
+        for (int k0 = 0; k0 < rows; k0 += 8) {
+          acc[lt][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[k0 * NRP], yb[k0 * NRP], acc[lt][0], 0, 0, 0);
+          acc[lt][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[(k0 + 4) * NRP], yb[(k0 + 4) * NRP], acc[lt][1], 0, 0, 0);
+        }
       }
-      // f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
-      for (int i = 0; i < 4; ++i) Gc[(16 * I + (lane >> 4) + 4 * i) * NR + 16 * J + (lane & 15)] = acc0[i] + acc1[i];
     }
+    __syncthreads();  // sY is rewritten by the next chunk
+  }
+  // f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
+  double* Gc = v.Gp + (int64_t)part * NR * NR;
+#pragma unroll
+  for (int lt = 0; lt < kLinMaxTiles; ++lt) {
+    const int k = 4 * lt + wid;
+    if (k < ntiles) {
+      int I, J;
+      lin_tile(k, ntu, NT, I, J);
+      for (int i = 0; i < 4; ++i)
+        Gc[(16 * I + (lane >> 4) + 4 * i) * NR + 16 * J + (lane & 15)] = acc[lt][0][i] + acc[lt][1][i];
+    }
+  }
 }
 
 // reduced camera system, Cholesky, pose step and tentative poses
@@ -551,7 +607,7 @@ __global__ __launch_bounds__(kBlock) void k_ba_solve(void* ws, BaDims dm) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int n = S->n, L = S->L, NR = dm.NR;
   const int np = 6 * (n - 1);
-  const int nch = (L + dm.LPC - 1) / dm.LPC;
+  const int nch0 = (L + dm.LPC - 1) / dm.LPC, nch = nch0 < dm.NPART ? nch0 : dm.NPART;  // partials used
   const double lam = S->lam;
   double* rhs = sS + np * np;
   // S = H_pp + lam diag + 1e-6 I - sum_c G_c (upper triangle computed, mirrored); 16 x 16
@@ -799,6 +855,7 @@ BaDims make_dims(const fvo_ctx* ctx) {
   d.NR = 6 * (d.K - 1) < 63 ? 64 : 128;
   d.LPC = d.NR == 64 ? 64 : 32;  // LDS slice 3 LPC x (NR + 2) doubles <= 99 KB
   d.NCH = (d.Lmax + d.LPC - 1) / d.LPC;
+  d.NPART = d.NCH < kLinParts ? d.NCH : kLinParts;
   d.NCU = (d.Lmax + kBlock - 1) / kBlock;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
@@ -815,7 +872,7 @@ BaDims make_dims(const fvo_ctx* ctx) {
   d.oObs = take((int64_t)sizeof(BaObs) * d.Omax);
   d.oFl = take(4ll * d.Omax);
   d.oW = take(8ll * 18 * d.Omax);
-  d.oGp = take(8ll * d.NCH * d.NR * d.NR);
+  d.oGp = take(8ll * d.NPART * d.NR * d.NR);
   d.oCp = take(8ll * d.NCU);
   d.oNext = take(4ll * kKMax * d.cap);
   d.oHdr = take(4ll * (8 + kKMax + 1));
@@ -823,7 +880,7 @@ BaDims make_dims(const fvo_ctx* ctx) {
   return d;
 }
 
-size_t lin_shm(const BaDims& d) { return (size_t)8 * 3 * d.LPC * (d.NR + 2); }
+size_t lin_shm(const BaDims& d) { return (size_t)8 * (3 * d.LPC * (d.NR + 2) + 9 * d.LPC * d.K + 6 * d.LPC); }
 size_t solve_shm(int K) {
   const int np = 6 * (K - 1);
   return (size_t)8 * (np * np + 2 * np);  // S, rhs, pivot roots
@@ -878,7 +935,7 @@ int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* mat
   void* ws = ctx->ba_ws;
   FVO_TIMED(ctx, KN_BA_BUILD, s,
             hipLaunchKernelGGL(k_ba_build, dim3(nwin), dim3(kBlock), (size_t)cap, s, in, ws, d, first_end, first_valid));
-  const dim3 gcu(nwin, d.NCU), gch(nwin, d.NCH), gfr(nwin, d.K - 1);
+  const dim3 gcu(nwin, d.NCU), gch(nwin, d.NPART), gfr(nwin, d.K - 1);
   const size_t shl = lin_shm(d), shs = solve_shm(d.K);
   FVO_TIMED(ctx, KN_BA_SOLVE, s, {
     hipLaunchKernelGGL(k_ba_cost, gcu, dim3(kBlock), 0, s, in, ws, d, cam, 0);
