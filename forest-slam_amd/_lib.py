@@ -60,6 +60,10 @@ SIGNATURES = {
     "fvo_recover_pose": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, ctypes.c_double, ctypes.c_double,
                                         ctypes.c_double, ctypes.c_double, _P, _P, _P, _P, _P]),
     "fvo_undistort_gray": (ctypes.c_int, [_P, _P, _I, _L, _I, _P, _P, _P, _L, _I, _P]),
+    "fvo_map_transform": (ctypes.c_int, [_P, _P, _I, _P, _I, _L, _P, _P, _L, _P, _P, _P]),
+    "fvo_voxel_workspace_bytes": (ctypes.c_int64, [_L]),
+    "fvo_voxel_down_sample": (ctypes.c_int, [_P, _P, _L, ctypes.c_double, _P, _L, _P, _P, _P, _P]),
+    "fvo_motion_blur": (ctypes.c_int, [_P, _P, _I, _L, _I, _I, ctypes.c_double, _P, _P, _I, _P, _P, _L, _I, _P]),
     "fvo_test_retain_best": (ctypes.c_int, [_P, _P, _I, _I, _P, _P, _P]),
     "fvo_debug_buffer": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
     "fvo_kernel_count": (ctypes.c_int, []),
@@ -314,6 +318,74 @@ class Context:
         self._check(self.L.fvo_undistort_gray(self.h, _ptr(bgr), B, H * W * 3, W * 3, Kh, dh, _ptr(out), H * W, W,
                                               _stream(self.device)))
         return out
+
+    def motion_blur(self, img, ksize, centers=None, n_centers=None, angle=0.0, out=None, mask=None):
+        """apply_random_motion_blur (stereo_slam.py:142-178) on gray u8 [B,H,W] images.
+        centers: i32 [B,cap] flat pixel indices on the device (or None: no blurred pixel),
+        n_centers: i32 [B] device counts.  Returns (out u8 [B,H,W], mask u8 [B,H,W])."""
+        if img.dim() == 2:
+            img = img[None]
+        if img.dtype != torch.uint8:
+            raise TypeError("img must be uint8 [B,H,W]")
+        img = img.contiguous()
+        B, H, W = img.shape
+        if (H, W) != (self.height, self.width):
+            raise ValueError(f"context is {self.width}x{self.height}, got {W}x{H}")
+        if out is None:
+            out = torch.empty_like(img)
+        if mask is None:
+            mask = torch.empty_like(img)
+        if centers is None:
+            cptr, nptr, cap = None, None, 0
+        else:
+            if centers.dtype != torch.int32 or n_centers is None or n_centers.dtype != torch.int32:
+                raise TypeError("centers / n_centers must be int32 device tensors")
+            centers, n_centers = centers.contiguous(), n_centers.contiguous()
+            if centers.dim() != 2 or centers.shape[0] != B or n_centers.numel() != B:
+                raise ValueError("centers must be [B, cap] and n_centers [B]")
+            cptr, nptr, cap = _ptr(centers), _ptr(n_centers), int(centers.shape[1])
+        self._check(self.L.fvo_motion_blur(self.h, _ptr(img), B, H * W, W, int(ksize), float(angle), cptr, nptr, cap,
+                                           _ptr(mask), _ptr(out), H * W, W, _stream(self.device)))
+        return out, mask
+
+    def map_transform(self, points, n_points, T, map_count, map_xyz64=None, map_xyz32=None):
+        """Append T[b] @ [p; 1] of every set b to the map (stereo_slam.py:308-318; fvo_map_transform).
+        points f32 [B,cap,>=3], n_points i32 [B], T f64 [B,4,4] (all device); map_count i32 [1]
+        (device, advanced by the call); map_xyz64 f64 [M,3] and/or map_xyz32 f32 [M,3]."""
+        if points.dtype != torch.float32 or points.dim() != 3 or points.shape[2] < 3:
+            raise TypeError("points must be float32 [B, cap, >=3]")
+        if map_xyz64 is None and map_xyz32 is None:
+            raise ValueError("need map_xyz64 and/or map_xyz32")
+        points, T = points.contiguous(), T.to(torch.float64).contiguous()
+        B, cap, st = points.shape
+        if T.shape != (B, 4, 4) or n_points.dtype != torch.int32 or n_points.numel() != B:
+            raise ValueError("T must be [B,4,4] and n_points int32 [B]")
+        caps = [m.shape[0] for m in (map_xyz64, map_xyz32) if m is not None]
+        self._check(self.L.fvo_map_transform(self.h, _ptr(points), st, _ptr(n_points), B, cap, _ptr(T),
+                                             _ptr(map_count), min(caps),
+                                             _ptr(map_xyz64) if map_xyz64 is not None else None,
+                                             _ptr(map_xyz32) if map_xyz32 is not None else None,
+                                             _stream(self.device)))
+        return map_count
+
+    def voxel_down_sample(self, points, voxel_size, workspace=None):
+        """Open3D voxel_down_sample (mono_slam.py:155): points f64 [N,3] (device) ->
+        (out f64 [N,3] (first n rows valid, voxel-index order), n i32[1], status i32[1])."""
+        if points.dtype != torch.float64 or points.dim() != 2 or points.shape[1] != 3:
+            raise TypeError("points must be float64 [N, 3]")
+        points = points.contiguous()
+        n = points.shape[0]
+        out = torch.empty((max(n, 1), 3), dtype=torch.float64, device=self.device)
+        cnt = torch.zeros((1,), dtype=torch.int32, device=self.device)
+        status = torch.zeros((1,), dtype=torch.int32, device=self.device)
+        wb = int(self.L.fvo_voxel_workspace_bytes(n)) if n > 0 else 0
+        if n > 0 and wb < 0:
+            raise RuntimeError("fvo_voxel_workspace_bytes failed")
+        if workspace is None or workspace.numel() < wb:
+            workspace = torch.empty((max(wb, 1),), dtype=torch.uint8, device=self.device)
+        self._check(self.L.fvo_voxel_down_sample(self.h, _ptr(points), n, float(voxel_size), _ptr(workspace), wb,
+                                                 _ptr(out), _ptr(cnt), _ptr(status), _stream(self.device)))
+        return out, cnt, status
 
     def gather_matches(self, kp0, kp1, matches, nmatch, out=None):
         """mkpts0/mkpts1 of a BF match list (fvo_gather_matches): (p0 f32[B,cap,2], p1, n i32[B])."""

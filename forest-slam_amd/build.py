@@ -13,7 +13,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libfvo.so")
-SOURCES = ["capi.cpp", "orb.hip", "bf.hip", "sgbm.hip", "pose.hip", "ba.hip", "essential.hip", "ingest.hip"]
+SOURCES = ["capi.cpp", "orb.hip", "bf.hip", "sgbm.hip", "pose.hip", "ba.hip", "essential.hip", "ingest.hip", "map.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
          "-fno-fast-math", "-Wno-unused-result", "-Wno-unused-function", "-Wno-unused-variable"]

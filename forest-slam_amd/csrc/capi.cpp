@@ -264,6 +264,60 @@ int fvo_undistort_gray(fvo_ctx* c, const uint8_t* bgr, int32_t batch, int64_t sr
   return ingest_run(c, bgr, batch, src_stride, src_pitch, K, dist, gray, dst_stride, dst_pitch, (hipStream_t)stream);
 }
 
+int fvo_motion_blur(fvo_ctx* c, const uint8_t* img, int32_t batch, int64_t src_stride, int32_t src_pitch,
+                    int32_t ksize, double angle, const int32_t* centers, const int32_t* n_centers, int32_t centers_cap,
+                    uint8_t* mask, uint8_t* out, int64_t dst_stride, int32_t dst_pitch, fvo_stream stream) {
+  if (!c) return -1;
+  if (batch < 0 || batch > c->cfg.max_batch) return fvo_fail(c, "batch exceeds max_batch");
+  if (batch == 0) return 0;
+  if (!img || !mask || !out || (centers_cap > 0 && (!centers || !n_centers))) return fvo_fail(c, "null pointer argument");
+  if (angle != 0.0) return fvo_fail(c, "motion blur: only angle 0 is supported (the reference's value)");
+  const int W = c->cfg.width, H = c->cfg.height;
+  if (ksize < 1 || ksize > 31) return fvo_fail(c, "motion blur: ksize must be in [1, 31]");
+  if (W <= ksize || H <= ksize) return fvo_fail(c, "motion blur: image smaller than the kernel");
+  if (centers_cap < 0) return fvo_fail(c, "centers_cap < 0");
+  if (src_pitch < W || src_stride < (int64_t)src_pitch * H || dst_pitch < W || dst_stride < (int64_t)dst_pitch * H)
+    return fvo_fail(c, "bad pitch/stride");
+  if (img == out) return fvo_fail(c, "motion blur: out must not alias img");
+  return motion_blur_run(c, img, batch, src_stride, src_pitch, ksize, centers, n_centers, centers_cap, mask, out,
+                         dst_stride, dst_pitch, (hipStream_t)stream);
+}
+
+int fvo_map_transform(fvo_ctx* c, const float* points, int32_t point_stride, const int32_t* n_points, int32_t batch,
+                      int64_t cap, const double* T, int32_t* map_count, int64_t map_cap, double* map_xyz64,
+                      float* map_xyz32, fvo_stream stream) {
+  if (!c) return -1;
+  if (batch < 0) return fvo_fail(c, "batch < 0");
+  if (batch == 0) return 0;
+  if (!points || !n_points || !T || !map_count || (!map_xyz64 && !map_xyz32)) return fvo_fail(c, "null pointer argument");
+  if (point_stride < 3) return fvo_fail(c, "point_stride must be >= 3 floats");
+  if (cap < 1 || cap > (int64_t)1 << 31) return fvo_fail(c, "cap must be in [1, 2^31]");
+  if (map_cap < 0) return fvo_fail(c, "map_cap < 0");
+  return map_transform_run(c, points, point_stride, n_points, batch, cap, T, map_count, map_cap, map_xyz64, map_xyz32,
+                           (hipStream_t)stream);
+}
+
+int64_t fvo_voxel_workspace_bytes(int64_t n_points) {
+  if (n_points < 1 || n_points > INT32_MAX) return -1;
+  return voxel_workspace_bytes(n_points);
+}
+
+int fvo_voxel_down_sample(fvo_ctx* c, const double* points, int64_t n_points, double voxel_size, void* workspace,
+                          int64_t workspace_bytes, double* out, int32_t* n_out, int32_t* status, fvo_stream stream) {
+  if (!c) return -1;
+  if (!out || !n_out || (n_points > 0 && (!points || !workspace))) return fvo_fail(c, "null pointer argument");
+  if (!(voxel_size > 0.0)) return fvo_fail(c, "voxel_size must be > 0");
+  if (n_points < 0 || n_points > INT32_MAX) return fvo_fail(c, "n_points out of range");
+  if (n_points == 0) {  // Open3D: an empty cloud downsamples to an empty cloud
+    FVO_HIP(c, hipMemsetAsync(n_out, 0, 4, (hipStream_t)stream));
+    if (status) FVO_HIP(c, hipMemsetAsync(status, 0, 4, (hipStream_t)stream));
+    return 0;
+  }
+  if (workspace_bytes < 0) return fvo_fail(c, "workspace_bytes < 0");
+  return voxel_run(c, points, n_points, voxel_size, workspace, (size_t)workspace_bytes, out, n_out, status,
+                   (hipStream_t)stream);
+}
+
 int fvo_kernel_count(void) { return KN_COUNT; }
 
 const char* fvo_kernel_name(int id) {
@@ -271,7 +325,7 @@ const char* fvo_kernel_name(int id) {
       "orb_copy_level0", "orb_resize", "orb_fast_score", "orb_nms_count", "orb_row_scan", "orb_nms_compact",
       "orb_select_fast", "orb_harris", "orb_select_harris", "orb_offsets", "orb_angle", "orb_blur", "orb_brief",
       "bf_argmin", "bf_finish", "sgbm_hsum", "sgbm_vert", "sgbm_horiz", "sgbm_median", "backproject",
-      "pnp_ransac", "ba_stereo", "ba_build", "ba_solve", "gather_matches", "essential_ransac", "recover_pose", "ingest_undistort_gray"};
+      "pnp_ransac", "ba_stereo", "ba_build", "ba_solve", "gather_matches", "essential_ransac", "recover_pose", "ingest_undistort_gray", "motion_blur", "map_transform", "voxel_down_sample"};
   return (id >= 0 && id < KN_COUNT) ? names[id] : "";
 }
 

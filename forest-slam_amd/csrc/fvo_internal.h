@@ -40,7 +40,7 @@ enum FvoKernel {
   KN_ORB_COPY, KN_ORB_RESIZE, KN_ORB_FAST, KN_ORB_NMS_COUNT, KN_ORB_ROW_SCAN, KN_ORB_COMPACT, KN_ORB_SELECT1,
   KN_ORB_HARRIS, KN_ORB_SELECT2, KN_ORB_OFFSETS, KN_ORB_ANGLE, KN_ORB_BLUR, KN_ORB_BRIEF, KN_BF_ARGMIN,
   KN_BF_FINISH, KN_SG_HSUM, KN_SG_VERT, KN_SG_HORIZ, KN_SG_MEDIAN, KN_BACKPROJECT, KN_PNP, KN_BA_STEREO,
-  KN_BA_BUILD, KN_BA_SOLVE, KN_GATHER, KN_ESSENTIAL, KN_RECOVER, KN_INGEST, KN_COUNT
+  KN_BA_BUILD, KN_BA_SOLVE, KN_GATHER, KN_ESSENTIAL, KN_RECOVER, KN_INGEST, KN_MOTION_BLUR, KN_MAP_XFORM, KN_VOXEL, KN_COUNT
 };
 
 struct TimingRec {
@@ -156,6 +156,14 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
 
 int ingest_run(fvo_ctx* ctx, const uint8_t* bgr, int batch, int64_t sstride, int spitch, const double* K,
                const double* dist, uint8_t* gray, int64_t dstride, int dpitch, hipStream_t s);
+int motion_blur_run(fvo_ctx* ctx, const uint8_t* img, int batch, int64_t sstride, int spitch, int ksize,
+                    const int32_t* centers, const int32_t* ncent, int cap, uint8_t* mask, uint8_t* out,
+                    int64_t dstride, int dpitch, hipStream_t s);
+int map_transform_run(fvo_ctx* ctx, const float* pts, int stride, const int32_t* npts, int batch, int64_t cap,
+                      const double* T, int32_t* count, int64_t map_cap, double* out64, float* out32, hipStream_t s);
+int64_t voxel_workspace_bytes(int64_t n);
+int voxel_run(fvo_ctx* ctx, const double* pts, int64_t n, double voxel, void* ws, size_t ws_bytes, double* out,
+              int32_t* n_out, int32_t* status, hipStream_t s);
 int mono_init(fvo_ctx* ctx);
 int gather_run(fvo_ctx* ctx, const float* kp0, const float* kp1, const int32_t* matches, const int32_t* nmatch,
                int batch, int cap, float* p0, float* p1, int32_t* npts, hipStream_t s);

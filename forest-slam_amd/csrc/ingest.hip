@@ -132,3 +132,150 @@ int ingest_run(fvo_ctx* ctx, const uint8_t* bgr, int batch, int64_t sstride, int
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Motion-blur ablation — stereo_slam.py:141-178 (forest_slam_ros/src/stereo_slam.py:142-178),
+// SURVEY.md §8f rank 3:
+//   apply_motion_blur:        kernel = warpAffine(diag(ones(k)), rot((k//2, k//2), angle=0)) / k
+//                             blurred = cv2.filter2D(image, -1, kernel)   (BORDER_REFLECT_101)
+//   apply_random_motion_blur: mask = union of (2*(k//2)+1)^2 squares around random.sample()d
+//                             pixels (clipped), out = np.where(mask, blurred, image)
+// At angle 0 the rotation is the identity and the kernel is the k-tap diagonal 1/k with
+// anchor (k//2, k//2), so tap i reads src(y + i - a, x + i - a).  filter2D's arithmetic:
+//   k*k <  130: direct Filter2D<uchar, float>: the nonzero taps in row-major (= diagonal)
+//               order accumulated by FilterVec_8u, s = fma(x_i, (float)(1/k), s) from 0,
+//               then cvRound (half to even) and saturate;
+//   k*k >= 130: dftFilter2D (crossCorr in float32).  Its result is the exact S/k within DFT
+//               rounding; S/k is never closer than 1/(2k) to a rounding boundary except at the
+//               exact ties S = q*k + k/2 (even k), which are taken half to even (unpinned).
+// One kernel: block = 256 columns x 32 rows (64 threads x 4 px per row, 4 row groups); the
+// (32+k-1) x (256+k-1) source tile (REFLECT_101 resolved while staging) in LDS; mask and
+// source read as dwords, the mask decides per pixel (only masked pixels are blurred); one
+// 32-bit store per thread and row.
+
+namespace {
+
+constexpr int kMbTileW = 256, kMbTileH = 32, kMbMaxK = 31;
+
+__device__ __forceinline__ int reflect101(int p, int n) {
+  if (n == 1) return 0;
+  while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+  return p;
+}
+
+__global__ __launch_bounds__(256) void k_mb_mask(const int32_t* __restrict__ centers, const int32_t* __restrict__ ncent,
+                                                 int cap, uint8_t* __restrict__ mask, int64_t mstride, int W, int H,
+                                                 int half) {
+  // thread = (center, row of its square); the square is written with byte stores of 1 (races write equal values)
+  const int b = blockIdx.y, side = 2 * half + 1;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = min(ncent[b], cap);
+  if (t >= (int64_t)n * side) return;
+  const int c = (int)(t / side), r = (int)(t % side);
+  const int p = centers[(int64_t)b * cap + c];
+  if (p < 0 || p >= W * H) return;  // not a pixel index: ignored
+  const int y = p / W, x = p % W;
+  const int yy = y - half + r;
+  if (yy < 0 || yy >= H) return;
+  const int x0 = max(0, x - half), x1 = min(W, x + half + 1);
+  uint8_t* M = mask + b * mstride + (int64_t)yy * W;
+  for (int xx = x0; xx < x1; ++xx) M[xx] = 1;
+}
+
+template <bool kDirect>
+__global__ __launch_bounds__(256) void k_mb_blur(const uint8_t* __restrict__ src, int64_t sstride, int spitch,
+                                                 const uint8_t* __restrict__ mask, int64_t mstride,
+                                                 uint8_t* __restrict__ dst, int64_t dstride, int dpitch, int W, int H,
+                                                 int k, float kf) {
+  // block = 256 columns x kMbTileH rows; thread = 4 consecutive pixels in each of kMbTileH/4 rows
+  __shared__ uint8_t tile[kMbTileH + kMbMaxK - 1][kMbTileW + kMbMaxK - 1 + 1];
+  const int b = blockIdx.z, a = k / 2;
+  const int x0 = blockIdx.x * kMbTileW, y0 = blockIdx.y * kMbTileH;
+  const uint8_t* S = src + b * sstride;
+  const int th = min(kMbTileH, H - y0) + k - 1, tw = kMbTileW + k - 1;
+  for (int r = 0; r < th; ++r) {  // row-wise fill: REFLECT_101 row index once per row, coalesced columns
+    const uint8_t* Srow = S + (int64_t)reflect101(y0 - a + r, H) * spitch;
+    for (int c = threadIdx.x; c < tw; c += 256) {
+      const int gx = x0 - a + c;  // columns past W-1+k feed no output
+      tile[r][c] = gx < W + k ? Srow[reflect101(gx, W)] : 0;
+    }
+  }
+  __syncthreads();
+  const int lx = (threadIdx.x & 63) * 4, xb = x0 + lx;
+  if (xb >= W) return;
+  const bool full = xb + 4 <= W;
+#pragma unroll 1
+  for (int ly = threadIdx.x >> 6; ly < kMbTileH; ly += 4) {
+    const int y = y0 + ly;
+    if (y >= H) break;
+    const uint8_t* Mrow = mask + b * mstride + (int64_t)y * W + xb;
+    const uint8_t* Srow = S + (int64_t)y * spitch + xb;
+    uint32_t m4 = 0, s4 = 0;
+    if (full && ((((uintptr_t)Mrow) | ((uintptr_t)Srow)) & 3) == 0) {
+      m4 = *reinterpret_cast<const uint32_t*>(Mrow);
+      s4 = *reinterpret_cast<const uint32_t*>(Srow);
+    } else {
+      for (int q = 0; q < 4 && xb + q < W; ++q) {
+        m4 |= (uint32_t)Mrow[q] << (8 * q);
+        s4 |= (uint32_t)Srow[q] << (8 * q);
+      }
+    }
+    uint32_t packed = s4;
+    if (m4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!((m4 >> (8 * q)) & 0xff)) continue;
+        uint32_t v;
+        if (kDirect) {
+          float sum = 0.f;
+          for (int i = 0; i < k; ++i) sum = __builtin_fmaf((float)tile[ly + i][lx + q + i], kf, sum);
+          const int r = (int)rintf(sum);
+          v = (uint32_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+        } else {
+          int sum = 0;
+          for (int i = 0; i < k; ++i) sum += tile[ly + i][lx + q + i];
+          int qq = sum / k;
+          const int rem = sum - qq * k;
+          if (2 * rem > k || (2 * rem == k && (qq & 1))) ++qq;
+          v = (uint32_t)(qq > 255 ? 255 : qq);
+        }
+        packed = (packed & ~(0xffu << (8 * q))) | (v << (8 * q));
+      }
+    }
+    uint8_t* D = dst + b * dstride + (int64_t)y * dpitch + xb;
+    if (full && (((uintptr_t)D) & 3) == 0) {
+      *reinterpret_cast<uint32_t*>(D) = packed;
+    } else {
+      for (int q = 0; q < 4 && xb + q < W; ++q) D[q] = (uint8_t)(packed >> (8 * q));
+    }
+  }
+}
+
+}  // namespace
+
+int motion_blur_run(fvo_ctx* ctx, const uint8_t* img, int batch, int64_t sstride, int spitch, int ksize,
+                    const int32_t* centers, const int32_t* ncent, int cap, uint8_t* mask, uint8_t* out,
+                    int64_t dstride, int dpitch, hipStream_t s) {
+  const int W = ctx->cfg.width, H = ctx->cfg.height;
+  const int64_t mstride = (int64_t)W * H;
+  const int half = ksize / 2, side = 2 * half + 1;
+  FVO_HIP(ctx, hipMemsetAsync(mask, 0, (size_t)mstride * batch, s));
+  if (cap > 0) {
+    dim3 mgrid((unsigned)(((int64_t)cap * side + 255) / 256), batch);
+    hipLaunchKernelGGL(k_mb_mask, mgrid, dim3(256), 0, s, centers, ncent, cap, mask, mstride, W, H, half);
+    FVO_LAUNCH_CHECK(ctx);
+  }
+  dim3 grid((W + kMbTileW - 1) / kMbTileW, (H + kMbTileH - 1) / kMbTileH, batch);
+  const bool direct = ksize * ksize < 130;
+  const float kf = (float)(1.0 / ksize);
+  FVO_TIMED(ctx, KN_MOTION_BLUR, s, {
+    if (direct)
+      hipLaunchKernelGGL(k_mb_blur<true>, grid, dim3(256), 0, s, img, sstride, spitch, mask, mstride, out, dstride,
+                         dpitch, W, H, ksize, kf);
+    else
+      hipLaunchKernelGGL(k_mb_blur<false>, grid, dim3(256), 0, s, img, sstride, spitch, mask, mstride, out, dstride,
+                         dpitch, W, H, ksize, kf);
+  });
+  FVO_LAUNCH_CHECK(ctx);
+  return 0;
+}

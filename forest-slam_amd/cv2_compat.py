@@ -221,6 +221,38 @@ class StereoSGBM:
         return self.computeDevice(left, right).cpu().numpy()
 
 
+# --------------------------------------------------------------------------- motion blur
+def blur_centers(height, width, blur_percentage=10, rng=None):
+    """The pixels apply_random_motion_blur blurs around (stereo_slam.py:161-165):
+    random.sample(range(H*W), int(H*W*(blur_percentage/100.0))).  The reference draws from
+    Python's unseeded global `random`; pass a seeded `random.Random` for reproducible runs
+    (rng=None uses the global module state, as the reference does)."""
+    import random
+    n = int((height * width) * (blur_percentage / 100.0))
+    return np.asarray((rng or random).sample(range(height * width), n), dtype=np.int32)
+
+
+_blur_cache = _CtxCache()
+
+
+def apply_random_motion_blur(image, blur_percentage=10, kernel_size=15, angle=0, rng=None, centers=None):
+    """stereo_slam.py:157-178 on the GPU (fvo_motion_blur): blur the whole image with the
+    k-tap motion kernel (apply_motion_blur, :142-154) and keep it inside the union of the
+    squares around the sampled pixels.  `centers` overrides the sampling (flat indices)."""
+    if angle != 0:
+        raise NotImplementedError("apply_random_motion_blur: only angle=0 (the reference's value) is implemented")
+    img = _u8_image(image)
+    H, W = img.shape
+    if centers is None:
+        centers = blur_centers(H, W, blur_percentage, rng)
+    c = torch.from_numpy(np.ascontiguousarray(centers, dtype=np.int32)).to(img.device)[None]
+    n = torch.tensor([c.shape[1]], dtype=torch.int32, device=img.device)
+    ctx = _blur_cache.get((W, H), lambda: _lib.Context(W, H, max_batch=1, stages=_lib.STAGE_BF,
+                                                                   kp_capacity=64))
+    out, _ = ctx.motion_blur(img, kernel_size, c if c.shape[1] else None, n, angle=float(angle))
+    return out[0].cpu().numpy()
+
+
 def StereoSGBM_create(minDisparity=0, numDisparities=16, blockSize=3, P1=0, P2=0, disp12MaxDiff=0, preFilterCap=0,
                       uniquenessRatio=0, speckleWindowSize=0, speckleRange=0, mode=STEREO_SGBM_MODE_SGBM):
     return StereoSGBM(minDisparity, numDisparities, blockSize, P1, P2, disp12MaxDiff, preFilterCap, uniquenessRatio,

@@ -24,6 +24,13 @@
  *                              mono_slam.py:112-117
  *   fvo_undistort_gray      <- cv2.cvtColor(cv2.undistort(img, K, dist), cv2.COLOR_BGR2GRAY)
  *                              stereo_slam.py:184-186, :196-198; mono_slam.py:92-93
+ *   fvo_motion_blur         <- apply_random_motion_blur(img, blur_percentage, kernel_size, angle=0)
+ *                              (cv2.getRotationMatrix2D + warpAffine + filter2D + np.where)
+ *                              forest_slam_ros/src/stereo_slam.py:142-178, :194, :206
+ *   fvo_map_transform       <- (cum @ hstack(points3D, 1).T)[:3].T appended to the map + PointCloud2
+ *                              float32 packing: stereo_slam.py:308-318; mono_slam.py:148; gt_mapping.py
+ *   fvo_voxel_down_sample   <- open3d PointCloud.voxel_down_sample(voxel_size=0.5)
+ *                              mono_slam.py:151-155, gt_mapping.py:62-66
  *
  * Conventions
  *  - All array pointers are DEVICE pointers owned by the caller (e.g. torch tensors'
@@ -223,6 +230,42 @@ int fvo_recover_pose(fvo_ctx* ctx, const double* E, const int32_t* e_status, con
 int fvo_undistort_gray(fvo_ctx* ctx, const uint8_t* bgr, int32_t batch, int64_t src_stride, int32_t src_pitch,
                        const double* K, const double* dist, uint8_t* gray, int64_t dst_stride, int32_t dst_pitch,
                        fvo_stream stream);
+
+/* Motion-blur ablation on `batch` gray images (any stage; no workspace), image size = the
+ * context's width x height:  out = np.where(mask, cv2.filter2D(img, -1, diag(ones(k))/k), img)
+ * where mask = union of the (2*(k//2)+1)^2 squares (clipped) centred on the sampled pixels.
+ * ksize in [1, 31], smaller than the image; angle must be 0 (the only value the reference uses;
+ * other angles return an error).  filter2D arithmetic: direct float path for k*k < 130, exact
+ * S/k (the DFT path's value) otherwise — see csrc/ingest.hip.
+ * centers: [batch][centers_cap] int32 flat pixel indices y*W+x (random.sample(range(H*W), n)),
+ *          n_centers [batch] device counts (<= centers_cap); centers_cap 0 = no blur (mask empty).
+ * mask:    [batch][H][W] u8 device scratch, written (0/1).
+ * img/out: [batch] u8 images (b*stride, rows pitch bytes apart); out must not alias img. */
+int fvo_motion_blur(fvo_ctx* ctx, const uint8_t* img, int32_t batch, int64_t src_stride, int32_t src_pitch,
+                    int32_t ksize, double angle, const int32_t* centers, const int32_t* n_centers, int32_t centers_cap,
+                    uint8_t* mask, uint8_t* out, int64_t dst_stride, int32_t dst_pitch, fvo_stream stream);
+
+/* Map accumulation (any stage; no workspace).  For each of `batch` point sets b (float32 xyz,
+ * point p of set b at points + (b*cap + p)*point_stride, n_points[b] device counts <= cap) and
+ * its 4x4 row-major fp64 transform T[b] (device, [batch][16]):
+ *   x' = ((T[0] x + T[1] y) + T[2] z) + T[3]   (likewise rows 1, 2; fp64, no contraction)
+ * appended to the map in set order starting at *map_count (device), which is then advanced by
+ * the total.  map_xyz64 (fp64, [map_cap][3]) and/or map_xyz32 (the PointCloud2 FLOAT32 x/y/z
+ * record, [map_cap][3]) may be NULL (not both); points past map_cap are dropped while
+ * *map_count still counts them (caller checks for overflow). */
+int fvo_map_transform(fvo_ctx* ctx, const float* points, int32_t point_stride, const int32_t* n_points, int32_t batch,
+                      int64_t cap, const double* T, int32_t* map_count, int64_t map_cap, double* map_xyz64,
+                      float* map_xyz32, fvo_stream stream);
+
+/* Open3D PointCloud::VoxelDownSample(voxel_size) of n_points fp64 xyz points (device [n][3]):
+ * vmin = min_bound - voxel/2, voxel index floor((p - vmin)/voxel), per voxel the fp64 sum of
+ * its points in input order divided by the count.  Output: out [<= n][3] fp64 ordered by
+ * voxel index (x, then y, then z — Open3D's hash-map order is unspecified), *n_out (device).
+ * workspace: device scratch of fvo_voxel_workspace_bytes(n_points) bytes (caller-owned).
+ * status (device, may be NULL): 0 ok, 1 = a voxel index outside [0, 2^21) (result invalid). */
+int64_t fvo_voxel_workspace_bytes(int64_t n_points);
+int fvo_voxel_down_sample(fvo_ctx* ctx, const double* points, int64_t n_points, double voxel_size, void* workspace,
+                          int64_t workspace_bytes, double* out, int32_t* n_out, int32_t* status, fvo_stream stream);
 
 /* Test hook: KeyPointsFilter::retainBest on `n` float responses (device memory) with the
  * product's selection kernel.  idx_out [n] receives the surviving original indices in

@@ -25,6 +25,8 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <algorithm>
+#include <vector>
 
 namespace ing {
 
@@ -122,6 +124,65 @@ void ref_undistort_map(int H, int W, const double* K, const double* dist, int16_
       mxy[((size_t)r * W + c) * 2 + 1] = (int16_t)sy;
       frac[(size_t)r * W + c] = (uint16_t)f;
     }
+}
+
+
+// Motion-blur ablation, forest_slam_ros/src/stereo_slam.py:142-178:
+//   kernel = warpAffine(np.diag(np.ones(k)), getRotationMatrix2D((k//2, k//2), 0, 1), (k, k)) / k
+//     (angle 0: M = [[1, 0, 0], [0, 1, 0]], the warp is the identity -> diag(1/k), float64)
+//   blurred = cv2.filter2D(img, -1, kernel)  (anchor (k//2, k//2), BORDER_REFLECT_101)
+//     OpenCV 4.x filter.dispatch.cpp: kernels with k*k >= 130 (8U -> 8U, SSE3 host) go to
+//     dftFilter2D (crossCorr in float32, cvRound on convert): its value is S/k within DFT
+//     rounding; restated as the exact S/k, ties (even k, S = q*k + k/2) half to even (unpinned);
+//     smaller kernels go to Filter2D<uchar, Cast<float, uchar>, FilterVec_8u>: nonzero taps
+//     (preprocess2DKernel, row-major) with float coefficients, s = fma(x, kf, s) from delta 0
+//     (v_muladd on the AVX2+FMA3 dispatch), v_round (half to even), saturate.
+//   mask[max(0, y-k//2):min(H, y+k//2+1), max(0, x-k//2):min(W, x+k//2+1)] = 1 per sampled pixel
+//   out = np.where(mask, blurred, img)
+static int refl101(int p, int n) {
+  if (n == 1) return 0;
+  while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+  return p;
+}
+
+void ref_motion_blur(const uint8_t* img, int H, int W, int k, const int32_t* centers, int n_centers, uint8_t* mask,
+                     uint8_t* out) {
+  // the kernel matrix (angle 0) and its nonzero taps in row-major order
+  std::vector<double> kern((size_t)k * k, 0.0);
+  for (int i = 0; i < k; ++i) kern[(size_t)i * k + i] = 1.0 / k;
+  std::vector<int> ty, tx;
+  std::vector<float> tw;
+  for (int r = 0; r < k; ++r)
+    for (int c = 0; c < k; ++c)
+      if (kern[(size_t)r * k + c] != 0.0) { ty.push_back(r); tx.push_back(c); tw.push_back((float)kern[(size_t)r * k + c]); }
+  const int ax = k / 2, ay = k / 2;
+  const bool dft = k * k >= 130;
+  std::vector<uint8_t> blurred((size_t)H * W);
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) {
+      int v;
+      if (dft) {
+        long S = 0;
+        for (size_t t = 0; t < ty.size(); ++t) S += img[(size_t)refl101(y + ty[t] - ay, H) * W + refl101(x + tx[t] - ax, W)];
+        long q = S / k, r = S % k;
+        if (2 * r > k || (2 * r == k && (q & 1))) ++q;
+        v = (int)q;
+      } else {
+        float s = 0.f;
+        for (size_t t = 0; t < ty.size(); ++t)
+          s = std::fma((float)img[(size_t)refl101(y + ty[t] - ay, H) * W + refl101(x + tx[t] - ax, W)], tw[t], s);
+        v = (int)std::nearbyint(s);
+      }
+      blurred[(size_t)y * W + x] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+    }
+  std::memset(mask, 0, (size_t)H * W);
+  const int h = k / 2;
+  for (int i = 0; i < n_centers; ++i) {
+    const int y = centers[i] / W, x = centers[i] % W;
+    for (int yy = std::max(0, y - h); yy < std::min(H, y + h + 1); ++yy)
+      for (int xx = std::max(0, x - h); xx < std::min(W, x + h + 1); ++xx) mask[(size_t)yy * W + xx] = 1;
+  }
+  for (size_t p = 0; p < (size_t)H * W; ++p) out[p] = mask[p] ? blurred[p] : img[p];
 }
 
 }  // extern "C"

@@ -272,6 +272,38 @@ def undistort_gray(bgr: np.ndarray, K: np.ndarray, dist) -> np.ndarray:
     return out
 
 
+def motion_blur(img: np.ndarray, ksize: int, centers) -> tuple:
+    """apply_random_motion_blur(img, kernel_size=ksize, angle=0) with the sampled pixels given
+    (forest_slam_ros/src/stereo_slam.py:142-178) -> (out u8[H,W], mask u8[H,W])."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    H, W = img.shape
+    c = np.ascontiguousarray(centers, dtype=np.int32).reshape(-1)
+    out = np.zeros((H, W), np.uint8)
+    mask = np.zeros((H, W), np.uint8)
+    lib().ref_motion_blur(_p(img, _u8p), H, W, int(ksize), _p(c, _i32p), len(c), _p(mask, _u8p), _p(out, _u8p))
+    return out, mask
+
+
+def map_transform(points: np.ndarray, T: np.ndarray):
+    """(cum @ hstack(points, 1).T)[:3].T (stereo_slam.py:308-311) -> (f64 [n,3], float32 PointCloud2 xyz)."""
+    P = np.ascontiguousarray(points, dtype=np.float32)
+    T = np.ascontiguousarray(T, dtype=np.float64).reshape(16)
+    n, st = P.shape
+    o64 = np.zeros((n, 3))
+    o32 = np.zeros((n, 3), np.float32)
+    lib().ref_map_transform(_p(P, _f32p), ctypes.c_int64(n), st, _p(T, _f64p), _p(o64, _f64p), _p(o32, _f32p))
+    return o64, o32
+
+
+def voxel_down_sample(points: np.ndarray, voxel_size: float) -> np.ndarray:
+    """Open3D PointCloud.voxel_down_sample (mono_slam.py:155), voxels in (ix, iy, iz) order."""
+    P = np.ascontiguousarray(points, dtype=np.float64)
+    out = np.zeros((max(len(P), 1), 3))
+    lib().ref_voxel_down_sample.restype = ctypes.c_int64
+    n = lib().ref_voxel_down_sample(_p(P, _f64p), ctypes.c_int64(len(P)), ctypes.c_double(voxel_size), _p(out, _f64p))
+    return out[:n]
+
+
 def undistort_map(H: int, W: int, K: np.ndarray, dist):
     """(map xy i16[H,W,2], fractional index u16[H,W]) of initUndistortRectifyMap(CV_16SC2)."""
     K = np.ascontiguousarray(K, dtype=np.float64).reshape(9)

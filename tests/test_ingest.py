@@ -69,3 +69,105 @@ def test_gpu_undistort_gray_matches_oracle(oracle_mod):
             for b in range(3):
                 want = oracle_mod.undistort_gray(imgs[b], K, d)
                 assert np.array_equal(got[b], want), (W, H, b, int((got[b] != want).sum()))
+
+
+# ----------------------------------------------------------------------- motion-blur ablation
+# apply_random_motion_blur (forest_slam_ros/src/stereo_slam.py:142-178).
+# Parity vs OpenCV is unpinned (no cv2 here): the oracle restates filter2D's direct float path
+# (k*k < 130) and the exact S/k of its DFT path (k*k >= 130); both are checked below against
+# an independent integer evaluation away from exact ties.
+
+def _blur_numpy(img, k, centers):
+    """Independent restatement: exact S/k rounded (ties reported), the reference's mask loop."""
+    H, W = img.shape
+    a = k // 2
+    p = np.pad(img.astype(np.int64), k, mode="reflect")  # numpy 'reflect' == BORDER_REFLECT_101
+    S = sum(p[k - a + i:k - a + i + H, k - a + i:k - a + i + W] for i in range(k))
+    mask = np.zeros((H, W), np.uint8)
+    for pix in centers:  # stereo_slam.py:167-171
+        y, x = pix // W, pix % W
+        mask[max(0, y - a):min(H, y + a + 1), max(0, x - a):min(W, x + a + 1)] = 1
+    return np.floor(S / k + 0.5), (S % k) * 2 == k, mask
+
+
+def test_golden_blur_reproduces(oracle_mod):
+    g = np.load(os.path.join(GOLDEN, "golden_blur.npz"))
+    for k in (10, 15, 20):
+        out, mask = oracle_mod.motion_blur(g["img"], k, g["centers"])
+        assert np.array_equal(out, g[f"out{k}"]) and np.array_equal(mask, g[f"mask{k}"])
+
+
+@pytest.mark.parametrize("k", [3, 10, 11, 12, 15, 20])
+def test_blur_oracle_matches_exact_sum(oracle_mod, k):
+    rng = np.random.default_rng(k)
+    img = rng.integers(0, 256, (48, 70), dtype=np.uint8)
+    centers = rng.choice(48 * 70, 40, replace=False).astype(np.int32)
+    out, mask = oracle_mod.motion_blur(img, k, centers)
+    exact, tie, mask_np = _blur_numpy(img, k, centers)
+    assert np.array_equal(mask, mask_np)
+    assert np.array_equal(out[mask == 0], img[mask == 0])
+    sel = (mask == 1) & ~tie
+    assert np.array_equal(out[sel], exact[sel].astype(np.uint8))
+    if k * k >= 130:  # DFT path: ties half to even
+        q = np.floor(exact - 0.5)
+        want = np.where(q % 2 == 0, q, q + 1)
+        assert np.array_equal(out[(mask == 1) & tie], want[(mask == 1) & tie].astype(np.uint8))
+
+
+def test_blur_zero_percent_is_identity(oracle_mod):
+    # the reference's active call: blur_percentage=0, kernel_size=20 (stereo_slam.py:194, :206)
+    from forest_slam_amd.cv2_compat import blur_centers
+    img = np.random.default_rng(2).integers(0, 256, (40, 64), dtype=np.uint8)
+    c = blur_centers(40, 64, 0)
+    assert c.size == 0
+    out, mask = oracle_mod.motion_blur(img, 20, c)
+    assert np.array_equal(out, img) and mask.sum() == 0
+
+
+def test_blur_centers_follow_random_sample():
+    import random
+    from forest_slam_amd.cv2_compat import blur_centers
+    c = blur_centers(600, 960, 10, random.Random(3))
+    assert c.dtype == np.int32 and len(c) == int(600 * 960 * 0.1)
+    assert np.array_equal(c, random.Random(3).sample(range(600 * 960), len(c)))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_gpu_motion_blur_matches_oracle(oracle_mod):
+    import random
+    from forest_slam_amd import _lib
+    for (W, H) in [(960, 600), (333, 211)]:
+        ctx = _lib.Context(W, H, max_batch=3, stages=_lib.STAGE_BF, kp_capacity=64)
+        imgs = np.stack([synthetic_bgr(H, W, s)[..., 1] for s in range(3)])
+        imgs[2] = np.random.default_rng(9).integers(0, 256, (H, W), dtype=np.uint8)
+        t = torch.from_numpy(imgs).cuda()
+        for k, pct in [(10, 1), (15, 0.5), (20, 10), (20, 0), (3, 2)]:
+            cs = [np.asarray(random.Random(b + k).sample(range(H * W), int(H * W * pct / 100)), np.int32)
+                  for b in range(3)]
+            cap = max(1, max(len(c) for c in cs))
+            C = np.zeros((3, cap), np.int32)
+            for b, c in enumerate(cs):
+                C[b, :len(c)] = c
+            n = torch.tensor([len(c) for c in cs], dtype=torch.int32, device="cuda")
+            out, mask = ctx.motion_blur(t, k, torch.from_numpy(C).cuda(), n)
+            out, mask = out.cpu().numpy(), mask.cpu().numpy()
+            for b in range(3):
+                want, wmask = oracle_mod.motion_blur(imgs[b], k, cs[b])
+                assert np.array_equal(mask[b], wmask), (W, H, k, b)
+                assert np.array_equal(out[b], want), (W, H, k, b, int((out[b] != want).sum()))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_gpu_apply_random_motion_blur_shim(oracle_mod):
+    import random
+    from forest_slam_amd import cv2_compat as cv2
+    img = synthetic_bgr(600, 960, 4)[..., 0].copy()
+    got = cv2.apply_random_motion_blur(img, blur_percentage=10, kernel_size=15, rng=random.Random(1))
+    want, _ = oracle_mod.motion_blur(img, 15, cv2.blur_centers(600, 960, 10, random.Random(1)))
+    assert np.array_equal(got, want)
+    # the reference's active call (:194): 0 % blurred -> the image itself
+    assert np.array_equal(cv2.apply_random_motion_blur(img, blur_percentage=0, kernel_size=20, angle=0), img)
+    with pytest.raises(NotImplementedError):
+        cv2.apply_random_motion_blur(img, 10, 15, angle=30)
