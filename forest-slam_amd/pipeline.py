@@ -70,8 +70,11 @@ def _upload(msgs, dev):
 
 
 def run_stereo_bag(path: str, batch: int = 32, nfeatures: int = 500, frame_interval: int = 1, ba_window: int = 0,
-                   device="cuda:0", K_left=K0, dist_left=DIST_L, K_right=K1, dist_right=DIST_R, baseline=BASELINE):
-    """stereo_slam.py's ORB branch over a bag -> (TUM rows f64[n,8], relative T, statuses)."""
+                   device="cuda:0", K_left=K0, dist_left=DIST_L, K_right=K1, dist_right=DIST_R, baseline=BASELINE,
+                   point_map=None):
+    """stereo_slam.py's ORB branch over a bag -> (TUM rows f64[n,8], relative T, statuses).
+    point_map: a ``mapping.PointMap`` that receives every posed frame's points3D in the map
+    frame (stereo_slam.py:308-318)."""
     bag = rosbag.Bag(path)
     pairs = select_stereo_pairs(bag, frame_interval)
     if len(pairs) < 2:
@@ -89,12 +92,21 @@ def run_stereo_bag(path: str, batch: int = 32, nfeatures: int = 500, frame_inter
     L0, R0 = gray(0, 1)
     fe.prime(L0[0], R0[0])
     Ts, sts = [], []
+    cum = np.eye(4)
     for s in range(1, len(pairs), batch):
         e = min(s + batch, len(pairs))
         L, R = gray(s, e)
         T, st = fe.step(L, R)
         Ts.append(T.cpu().numpy())
         sts.append(st.cpu().numpy())
+        if point_map is not None:
+            cums = []
+            for i in range(e - s):  # stereo_slam.py:306, frames the reference skips keep cum
+                if sts[-1][i] != -1:
+                    cum = np.dot(cum, Ts[-1][i])
+                cums.append(cum.copy())
+            keep = torch.from_numpy((sts[-1] != -1).astype(np.int32)).to(dev)
+            point_map.add_frames(fe.P3[:e - s], fe.npts[:e - s] * keep, np.stack(cums))
     T = np.concatenate(Ts)
     st = np.concatenate(sts)
     valid = st != -1

@@ -120,3 +120,20 @@ def test_gpu_voxel_down_sample_matches_oracle(oracle_mod):
             assert np.array_equal(out[:len(want)].cpu().numpy(), want), (len(P), v)
     out, n, st = ctx.voxel_down_sample(torch.zeros((0, 3), dtype=torch.float64, device="cuda"), 0.5)
     assert int(n.item()) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_gpu_point_map_mono_update_matches_oracle(oracle_mod):
+    """mono_slam.py:144-164: cloud -> pose -> voxel_down_sample(0.5) -> appended to the map."""
+    from forest_slam_amd.mapping import PointMap
+    pm = PointMap(100_000)
+    want = []
+    for k in range(3):
+        cloud, T = _cloud(20_000, 40 + k, spread=10.0), _pose(50 + k)
+        pm.add_cloud(cloud, T, 0.5)
+        o64, _ = oracle_mod.map_transform(cloud, T)
+        want.append(oracle_mod.voxel_down_sample(o64, 0.5))
+    want = np.concatenate(want)
+    assert np.array_equal(pm.cloud64(), want)
+    assert np.array_equal(pm.cloud32(), want.astype(np.float32))

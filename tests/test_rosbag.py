@@ -160,17 +160,20 @@ def test_run_stereo_bag_matches_oracle_pipeline(tmp_path, oracle_mod):
             t = rb.Time(1000 + i, 0)
             w.write(pl.LEFT, rb.image_message(bl, t), t)
             w.write(pl.RIGHT, rb.image_message(br, rb.Time(1000 + i, 500)), rb.Time(1000 + i, 500))
+    from forest_slam_amd.mapping import PointMap
+    pmap = PointMap(20000)
     rows, T, st = pl.run_stereo_bag(path, batch=2, nfeatures=300, device="cuda:0", K_left=K, dist_left=pl.DIST_L,
-                                    K_right=K, dist_right=pl.DIST_R, baseline=synth.BASELINE)
+                                    K_right=K, dist_right=pl.DIST_R, baseline=synth.BASELINE, point_map=pmap)
     # oracle: the same bytes through the restated ingest and stereo_slam.py:232-306
     grays = [(oracle_mod.undistort_gray(bl, K, pl.DIST_L), oracle_mod.undistort_gray(br, K, pl.DIST_R))
              for bl, br in frames]
-    Ts, valid = [], []
+    Ts, valid, P3s = [], [], []
     for i in range(1, 6):
         out = oracle_mod.frame_pose(grays[i - 1][0], grays[i - 1][1], grays[i][0], K, pl.DIST_L, synth.BASELINE,
                                     nfeatures=300)
         valid.append(out["T"] is not None)
         Ts.append(out["T"] if out["T"] is not None else np.eye(4))
+        P3s.append(out["P3"])
     assert np.array_equal(st != -1, np.array(valid))
     for i in range(5):
         if valid[i]:
@@ -179,3 +182,9 @@ def test_run_stereo_bag_matches_oracle_pipeline(tmp_path, oracle_mod):
     ref_rows = ev.tum_rows(np.array([1000 + i + 0.5e-6 for i in range(1, 6)])[np.array(valid)], cum)
     assert np.abs(rows[:, 0] - ref_rows[:, 0]).max() < 1e-6
     assert np.abs(rows[:, 1:4] - ref_rows[:, 1:4]).max() < 1e-3
+    # the map (stereo_slam.py:308-318): posed frames' points3D through their cumulative pose
+    ref_map = np.concatenate([oracle_mod.map_transform(P3s[i], cum[j])[1]
+                              for j, i in enumerate(np.flatnonzero(valid))])
+    got = pmap.cloud32()
+    assert got.shape == ref_map.shape
+    assert np.abs(got - ref_map).max() <= 1e-3 * max(1.0, np.abs(ref_map).max())
