@@ -129,6 +129,31 @@ def pmc_traffic(stage: str):
     return None, None
 
 
+F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense FP64 matrix (spec); the PMC busy-cycle ratio agrees
+
+
+def pmc_mfma(kernel: str = "k_ba_lin"):
+    """MFMA utilisation of the BA Schur kernel from the newest committed MFMA PMC summary
+    (profiles/<round>/mfma_per_kernel.csv, tools/mfma_pmc.sh: SQ_VALU_MFMA_BUSY_CYCLES,
+    SQ_INSTS_VALU_MFMA_MOPS_F64, GRBM_GUI_ACTIVE over this bench command)."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "mfma_per_kernel.csv")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        for row in csv.DictReader(f):
+            if row["kernel"] == kernel:
+                tf = float(row["f64_mfma_tflops"])
+                return {"kernel": kernel, "dtype": "f64", "mfma_util": float(row["mfma_util"]),
+                        "achieved_tflops": tf, "peak_tflops": F64_MFMA_PEAK_TFLOPS,
+                        "frac": round(tf / F64_MFMA_PEAK_TFLOPS, 4),
+                        "flops_per_launch": float(row["avg_f64_mfma_flops"]),
+                        "avg_launch_ms_profiled": float(row["avg_ms"]),
+                        "source": os.path.relpath(files[-1], ROOT)}
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -309,6 +334,7 @@ def main():
                          "traffic_rate_gbs_in_order": round(traffic / avg_launch_io_s / 1e9, 1)
                          if (traffic and avg_launch_io_s > 0) else None},
             "cpu_baseline": cpu,
+            "ba_mfma": pmc_mfma() if args.ba_window else None,
             "ate": ate,
             "stages_ms_per_step": stage_ms,
             "workspace_gb": round(fe.ctx.workspace_bytes / 1e9, 2),
