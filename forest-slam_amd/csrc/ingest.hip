@@ -148,14 +148,15 @@ int ingest_run(fvo_ctx* ctx, const uint8_t* bgr, int batch, int64_t sstride, int
 //   k*k >= 130: dftFilter2D (crossCorr in float32).  Its result is the exact S/k within DFT
 //               rounding; S/k is never closer than 1/(2k) to a rounding boundary except at the
 //               exact ties S = q*k + k/2 (even k), which are taken half to even (unpinned).
-// One kernel: block = 256 columns x 32 rows (64 threads x 4 px per row, 4 row groups); the
-// (32+k-1) x (256+k-1) source tile (REFLECT_101 resolved while staging) in LDS; mask and
-// source read as dwords, the mask decides per pixel (only masked pixels are blurred); one
-// 32-bit store per thread and row.
+// k_mb_seed marks the sampled pixels; k_mb_blur (block = 256 columns x 32 rows, 64 threads x
+// 4 px per row, 4 row groups) stages the (32+k-1) x (256+k-1) source tile (REFLECT_101
+// resolved while staging) in LDS, dilates the seeds to the mask in LDS, blurs only masked
+// pixels and writes out + mask with dword stores; k_mb_fix normalises the mask bytes.
 
 namespace {
 
 constexpr int kMbTileW = 256, kMbTileH = 32, kMbMaxK = 31;
+constexpr int kMbTW = kMbTileW + kMbMaxK - 1 + 1, kMbTH = kMbTileH + kMbMaxK - 1;
 
 __device__ __forceinline__ int reflect101(int p, int n) {
   if (n == 1) return 0;
@@ -163,36 +164,50 @@ __device__ __forceinline__ int reflect101(int p, int n) {
   return p;
 }
 
-__global__ __launch_bounds__(256) void k_mb_mask(const int32_t* __restrict__ centers, const int32_t* __restrict__ ncent,
-                                                 int cap, uint8_t* __restrict__ mask, int64_t mstride, int W, int H,
-                                                 int half) {
-  // thread = (center, row of its square); the square is written with byte stores of 1 (races write equal values)
-  const int b = blockIdx.y, side = 2 * half + 1;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int n = min(ncent[b], cap);
-  if (t >= (int64_t)n * side) return;
-  const int c = (int)(t / side), r = (int)(t % side);
+// Seeds: bit 0 of the mask byte at every sampled pixel (one byte store per sample).
+__global__ __launch_bounds__(256) void k_mb_seed(const int32_t* __restrict__ centers, const int32_t* __restrict__ ncent,
+                                                 int cap, uint8_t* __restrict__ mask, int64_t mstride, int npix) {
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= min(ncent[b], cap)) return;
   const int p = centers[(int64_t)b * cap + c];
-  if (p < 0 || p >= W * H) return;  // not a pixel index: ignored
-  const int y = p / W, x = p % W;
-  const int yy = y - half + r;
-  if (yy < 0 || yy >= H) return;
-  const int x0 = max(0, x - half), x1 = min(W, x + half + 1);
-  uint8_t* M = mask + b * mstride + (int64_t)yy * W;
-  for (int xx = x0; xx < x1; ++xx) M[xx] = 1;
+  if (p < 0 || p >= npix) return;  // not a pixel index: ignored
+  mask[b * mstride + p] = 1;
 }
 
-template <bool kDirect>
+// mask byte = bit 1 (the dilated mask written by k_mb_blur) -> 0/1; 4 bytes per thread
+__global__ __launch_bounds__(256) void k_mb_fix(uint8_t* __restrict__ m, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i + 4 <= n) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(m + i);
+    *w = (*w >> 1) & 0x01010101u;
+  } else {
+    for (int64_t j = i; j < n; ++j) m[j] = (m[j] >> 1) & 1;
+  }
+}
+
+// kSeeds: the mask is the (2h+1)^2 dilation of the seed bitmap (= the union of the reference's
+// clipped squares), computed per block in LDS on bitmaps: seed rows (32+2h) x (256+2h) (zero
+// outside the image) gathered by wave ballots, horizontal dilation as 2h+1 shift-ORs of a
+// 64-bit funnel per 32 output columns, vertical as 2h+1 word ORs; each block writes its pixels' mask byte as
+// seed | dilated << 1 (neighbours only read bit 0), k_mb_fix then leaves 0/1.
+// Without seeds the mask is all zero and out = img.
+template <bool kDirect, bool kSeeds>
 __global__ __launch_bounds__(256) void k_mb_blur(const uint8_t* __restrict__ src, int64_t sstride, int spitch,
-                                                 const uint8_t* __restrict__ mask, int64_t mstride,
+                                                 uint8_t* __restrict__ mask, int64_t mstride,
                                                  uint8_t* __restrict__ dst, int64_t dstride, int dpitch, int W, int H,
-                                                 int k, float kf) {
-  // block = 256 columns x kMbTileH rows; thread = 4 consecutive pixels in each of kMbTileH/4 rows
-  __shared__ uint8_t tile[kMbTileH + kMbMaxK - 1][kMbTileW + kMbMaxK - 1 + 1];
+                                                 int k, int h, float kf) {
+  __shared__ uint8_t tile[kMbTH][kMbTW];
+  // seed rows as bitmaps (320 bits = 10 words per tile row), the horizontal dilation (8 words =
+  // 256 output columns per row) and the full dilation of the block's 32 rows
+  __shared__ uint32_t sbits[kSeeds ? kMbTH : 1][10];
+  __shared__ uint32_t hbits[kSeeds ? kMbTH : 1][8];
+  __shared__ uint32_t dbits[kSeeds ? kMbTileH : 1][8];
   const int b = blockIdx.z, a = k / 2;
   const int x0 = blockIdx.x * kMbTileW, y0 = blockIdx.y * kMbTileH;
   const uint8_t* S = src + b * sstride;
-  const int th = min(kMbTileH, H - y0) + k - 1, tw = kMbTileW + k - 1;
+  const int rows = min(kMbTileH, H - y0);
+  const int th = rows + k - 1, tw = kMbTileW + k - 1;
   for (int r = 0; r < th; ++r) {  // row-wise fill: REFLECT_101 row index once per row, coalesced columns
     const uint8_t* Srow = S + (int64_t)reflect101(y0 - a + r, H) * spitch;
     for (int c = threadIdx.x; c < tw; c += 256) {
@@ -200,25 +215,60 @@ __global__ __launch_bounds__(256) void k_mb_blur(const uint8_t* __restrict__ src
       tile[r][c] = gx < W + k ? Srow[reflect101(gx, W)] : 0;
     }
   }
+  uint8_t* Mb = mask + b * mstride;
+  if (kSeeds) {
+    const int sh = rows + 2 * h, sw = kMbTileW + 2 * h;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int r = wave; r < sh; r += 4) {  // ballot per 64 columns: bit c of row r = seed at (y0-h+r, x0-h+c)
+      const int gy = y0 - h + r;
+      const bool rin = gy >= 0 && gy < H;
+#pragma unroll
+      for (int ch = 0; ch < 5; ++ch) {
+        const int c = ch * 64 + lane, gx = x0 - h + c;
+        const bool on = c < sw && rin && gx >= 0 && gx < W && (Mb[(int64_t)gy * W + gx] & 1);
+        const uint64_t bal = __ballot(on);
+        if (lane == 0) {
+          sbits[r][2 * ch] = (uint32_t)bal;
+          sbits[r][2 * ch + 1] = (uint32_t)(bal >> 32);
+        }
+      }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < sh * 8; t += 256) {  // horizontal: out bit c = OR of bits c .. c+2h
+      const int r = t >> 3, w = t & 7;
+      const uint64_t v = (uint64_t)sbits[r][w] | ((uint64_t)sbits[r][w + 1] << 32);
+      uint64_t d = 0;
+      for (int j = 0; j <= 2 * h; ++j) d |= v >> j;
+      hbits[r][w] = (uint32_t)d;
+    }
+    __syncthreads();
+    {  // vertical: rows ly .. ly+2h of the horizontal dilation
+      const int ly = threadIdx.x >> 3, w = threadIdx.x & 7;
+      if (ly < rows) {
+        uint32_t d = 0;
+        for (int i = 0; i <= 2 * h; ++i) d |= hbits[ly + i][w];
+        dbits[ly][w] = d;
+      }
+    }
+  }
   __syncthreads();
   const int lx = (threadIdx.x & 63) * 4, xb = x0 + lx;
   if (xb >= W) return;
   const bool full = xb + 4 <= W;
 #pragma unroll 1
-  for (int ly = threadIdx.x >> 6; ly < kMbTileH; ly += 4) {
+  for (int ly = threadIdx.x >> 6; ly < rows; ly += 4) {
     const int y = y0 + ly;
-    if (y >= H) break;
-    const uint8_t* Mrow = mask + b * mstride + (int64_t)y * W + xb;
     const uint8_t* Srow = S + (int64_t)y * spitch + xb;
+    uint8_t* Mrow = Mb + (int64_t)y * W + xb;
     uint32_t m4 = 0, s4 = 0;
-    if (full && ((((uintptr_t)Mrow) | ((uintptr_t)Srow)) & 3) == 0) {
-      m4 = *reinterpret_cast<const uint32_t*>(Mrow);
+    if (kSeeds) {
+      const uint32_t nib = (dbits[ly][lx >> 5] >> (lx & 31)) & 0xfu;
+      m4 = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
+    }
+    if (full && (((uintptr_t)Srow) & 3) == 0) {
       s4 = *reinterpret_cast<const uint32_t*>(Srow);
     } else {
-      for (int q = 0; q < 4 && xb + q < W; ++q) {
-        m4 |= (uint32_t)Mrow[q] << (8 * q);
-        s4 |= (uint32_t)Srow[q] << (8 * q);
-      }
+      for (int q = 0; q < 4 && xb + q < W; ++q) s4 |= (uint32_t)Srow[q] << (8 * q);
     }
     uint32_t packed = s4;
     if (m4) {
@@ -242,11 +292,25 @@ __global__ __launch_bounds__(256) void k_mb_blur(const uint8_t* __restrict__ src
         packed = (packed & ~(0xffu << (8 * q))) | (v << (8 * q));
       }
     }
+    // mask byte: seed bit | dilated << 1 (k_mb_fix), or 0 without seeds
+    const uint32_t mo = m4 << 1;
     uint8_t* D = dst + b * dstride + (int64_t)y * dpitch + xb;
     if (full && (((uintptr_t)D) & 3) == 0) {
       *reinterpret_cast<uint32_t*>(D) = packed;
     } else {
       for (int q = 0; q < 4 && xb + q < W; ++q) D[q] = (uint8_t)(packed >> (8 * q));
+    }
+    if (kSeeds) {  // only this block writes these bytes; neighbours read bit 0, which is kept
+      if (full && (((uintptr_t)Mrow) & 3) == 0) {
+        uint32_t* M4 = reinterpret_cast<uint32_t*>(Mrow);
+        *M4 = (*M4 & 0x01010101u) | mo;
+      } else {
+        for (int q = 0; q < 4 && xb + q < W; ++q) Mrow[q] = (uint8_t)((Mrow[q] & 1) | ((mo >> (8 * q)) & 0xff));
+      }
+    } else if (full && (((uintptr_t)Mrow) & 3) == 0) {
+      *reinterpret_cast<uint32_t*>(Mrow) = 0;
+    } else {
+      for (int q = 0; q < 4 && xb + q < W; ++q) Mrow[q] = 0;
     }
   }
 }
@@ -258,24 +322,34 @@ int motion_blur_run(fvo_ctx* ctx, const uint8_t* img, int batch, int64_t sstride
                     int64_t dstride, int dpitch, hipStream_t s) {
   const int W = ctx->cfg.width, H = ctx->cfg.height;
   const int64_t mstride = (int64_t)W * H;
-  const int half = ksize / 2, side = 2 * half + 1;
-  FVO_HIP(ctx, hipMemsetAsync(mask, 0, (size_t)mstride * batch, s));
-  if (cap > 0) {
-    dim3 mgrid((unsigned)(((int64_t)cap * side + 255) / 256), batch);
-    hipLaunchKernelGGL(k_mb_mask, mgrid, dim3(256), 0, s, centers, ncent, cap, mask, mstride, W, H, half);
+  const int half = ksize / 2;
+  const bool seeds = cap > 0;
+  if (seeds) {
+    FVO_HIP(ctx, hipMemsetAsync(mask, 0, (size_t)mstride * batch, s));
+    hipLaunchKernelGGL(k_mb_seed, dim3((cap + 255) / 256, batch), dim3(256), 0, s, centers, ncent, cap, mask, mstride,
+                       W * H);
     FVO_LAUNCH_CHECK(ctx);
   }
   dim3 grid((W + kMbTileW - 1) / kMbTileW, (H + kMbTileH - 1) / kMbTileH, batch);
   const bool direct = ksize * ksize < 130;
   const float kf = (float)(1.0 / ksize);
+#define FVO_MB(DIR, SEED)                                                                                    \
+  hipLaunchKernelGGL((k_mb_blur<DIR, SEED>), grid, dim3(256), 0, s, img, sstride, spitch, mask, mstride, out, \
+                     dstride, dpitch, W, H, ksize, half, kf)
   FVO_TIMED(ctx, KN_MOTION_BLUR, s, {
-    if (direct)
-      hipLaunchKernelGGL(k_mb_blur<true>, grid, dim3(256), 0, s, img, sstride, spitch, mask, mstride, out, dstride,
-                         dpitch, W, H, ksize, kf);
-    else
-      hipLaunchKernelGGL(k_mb_blur<false>, grid, dim3(256), 0, s, img, sstride, spitch, mask, mstride, out, dstride,
-                         dpitch, W, H, ksize, kf);
+    if (direct) {
+      if (seeds) FVO_MB(true, true); else FVO_MB(true, false);
+    } else {
+      if (seeds) FVO_MB(false, true); else FVO_MB(false, false);
+    }
   });
+#undef FVO_MB
   FVO_LAUNCH_CHECK(ctx);
+  if (seeds) {
+    if (((uintptr_t)mask) & 3) return fvo_fail(ctx, "motion blur: mask must be 4-byte aligned");
+    const int64_t n = mstride * batch;
+    hipLaunchKernelGGL(k_mb_fix, dim3((unsigned)((n / 4 + 256) / 256)), dim3(256), 0, s, mask, n);
+    FVO_LAUNCH_CHECK(ctx);
+  }
   return 0;
 }

@@ -239,7 +239,7 @@ int fvo_undistort_gray(fvo_ctx* ctx, const uint8_t* bgr, int32_t batch, int64_t 
  * S/k (the DFT path's value) otherwise — see csrc/ingest.hip.
  * centers: [batch][centers_cap] int32 flat pixel indices y*W+x (random.sample(range(H*W), n)),
  *          n_centers [batch] device counts (<= centers_cap); centers_cap 0 = no blur (mask empty).
- * mask:    [batch][H][W] u8 device scratch, written (0/1).
+ * mask:    [batch][H][W] u8 device buffer (4-byte aligned), written (0/1).
  * img/out: [batch] u8 images (b*stride, rows pitch bytes apart); out must not alias img. */
 int fvo_motion_blur(fvo_ctx* ctx, const uint8_t* img, int32_t batch, int64_t src_stride, int32_t src_pitch,
                     int32_t ksize, double angle, const int32_t* centers, const int32_t* n_centers, int32_t centers_cap,

@@ -17,7 +17,8 @@ def find(d, pat):
 def ours(name):
     return any(k in name for k in ("k_sg_", "k_bf_", "k_pnp", "k_backproject", "k_brief", "k_blur", "k_angle",
                                    "k_harris", "k_select", "k_nms", "k_fast", "k_resize", "k_copy_level0",
-                                   "k_row_scan", "k_offsets", "k_ba_", "k_em_", "k_ing_", "k_gather"))
+                                   "k_row_scan", "k_offsets", "k_ba_", "k_em_", "k_ing_", "k_gather",
+                                   "k_mb_", "k_map_", "k_vx_", "rocprim"))
 
 
 def short(name):
