@@ -168,6 +168,8 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=4, help="CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-ate", type=int, default=1, help="ATE of the CPU reference path on the ATE frames")
     ap.add_argument("--overlap-sgbm", type=int, default=1, help="SGBM of step k+1 on a side stream during step k")
+    ap.add_argument("--main-priority", type=int, default=0, help="HIP stream priority of the main path (-1 = high)")
+    ap.add_argument("--sgbm-priority", type=int, default=0, help="HIP stream priority of the overlapped SGBM stream")
     ap.add_argument("--ba-max-landmarks", type=int, default=0, help="per-window landmark cap (0 = library default)")
     ap.add_argument("--ba-max-obs", type=int, default=0, help="per-window observation cap (0 = library default)")
     args = ap.parse_args()
@@ -183,6 +185,8 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.main_priority:
+        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=args.main_priority))
 
     import forest_slam_amd.build as fbuild
     from forest_slam_amd import eval as ev
@@ -197,7 +201,8 @@ def main():
     torch.cuda.synchronize()
     ba_caps = {k: v for k, v in (("ba_max_landmarks", args.ba_max_landmarks), ("ba_max_obs", args.ba_max_obs)) if v}
     fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=B, nfeatures=args.nfeatures, device=dev,
-                           ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm), **ba_caps)
+                           ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm),
+                           sgbm_priority=args.sgbm_priority, **ba_caps)
     fe.prime(L_all[0], R_all[0])
     Lb, Rb = L_all[1:].contiguous(), R_all[1:].contiguous()
 

@@ -29,7 +29,7 @@ from . import _lib
 class StereoFrontEnd:
     def __init__(self, width: int, height: int, K: np.ndarray, dist: np.ndarray, baseline: float, batch: int,
                  nfeatures: int = 500, match_right: bool = True, device=None, ba_window: int = 10,
-                 ba_iters: int = 10, overlap_sgbm: bool = False, **params):
+                 ba_iters: int = 10, overlap_sgbm: bool = False, sgbm_priority: int = 0, **params):
         self.B = batch
         self.K = np.asarray(K, np.float64)
         self.dist = np.resize(np.asarray(dist, np.float64), 5)
@@ -92,7 +92,7 @@ class StereoFrontEnd:
         # when step() is called (resident in HBM, or pass inputs_ready).  Default: SGBM runs
         # in order on the caller's stream.
         self.overlap_sgbm = bool(overlap_sgbm)
-        self.s_sgbm = torch.cuda.Stream(dev) if self.overlap_sgbm else None
+        self.s_sgbm = torch.cuda.Stream(dev, priority=sgbm_priority) if self.overlap_sgbm else None
         self.sg_lastL = e((height, width), torch.uint8)
         self.sg_lastR = e((height, width), torch.uint8)
         self.main_done = [None, None]
