@@ -300,12 +300,15 @@ __global__ __launch_bounds__(256) void k_mb_blur(const uint8_t* __restrict__ src
     } else {
       for (int q = 0; q < 4 && xb + q < W; ++q) D[q] = (uint8_t)(packed >> (8 * q));
     }
-    if (kSeeds) {  // only this block writes these bytes; neighbours read bit 0, which is kept
+    if (kSeeds) {  // only this block writes these bytes; neighbours read bit 0, which is kept (from sbits)
+      const int cb = lx + h;  // seed-tile column of this thread's first pixel, row ly + h
+      const uint64_t sv = (uint64_t)sbits[ly + h][cb >> 5] | ((uint64_t)sbits[ly + h][(cb >> 5) + 1] << 32);
+      const uint32_t sn = (uint32_t)(sv >> (cb & 31)) & 0xfu;
+      const uint32_t sd = (sn & 1u) | ((sn & 2u) << 7) | ((sn & 4u) << 14) | ((sn & 8u) << 21);
       if (full && (((uintptr_t)Mrow) & 3) == 0) {
-        uint32_t* M4 = reinterpret_cast<uint32_t*>(Mrow);
-        *M4 = (*M4 & 0x01010101u) | mo;
+        *reinterpret_cast<uint32_t*>(Mrow) = sd | mo;
       } else {
-        for (int q = 0; q < 4 && xb + q < W; ++q) Mrow[q] = (uint8_t)((Mrow[q] & 1) | ((mo >> (8 * q)) & 0xff));
+        for (int q = 0; q < 4 && xb + q < W; ++q) Mrow[q] = (uint8_t)(((sd | mo) >> (8 * q)) & 0xff);
       }
     } else if (full && (((uintptr_t)Mrow) & 3) == 0) {
       *reinterpret_cast<uint32_t*>(Mrow) = 0;
