@@ -32,12 +32,35 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+RPE_DELTA_M = 5.0
 
 
 def algorithmic_bytes_per_frame(W: int, H: int, N: int) -> int:
     """2WH (L,R u8 in) + 2WH (int16 disparity) + 2N*48 (kp+desc, 2 images)
     + 2*(2N*32 + 4N) (two matchings) + 22N (back-projection) = 4WH + 254N."""
     return 4 * W * H + 254 * N
+
+
+def cpu_threads() -> int:
+    """Threads the CPU legs use: the GPU box's CPU share is 16 (its os.cpu_count() reports the
+    whole machine), so at most 16; this container has 8."""
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def host_cpus() -> dict:
+    """What the host reports (stated beside the thread count used)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"os_cpu_count": os.cpu_count(), "affinity": aff, "model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_baseline(n_frames: int, nfeatures: int, W: int, H: int) -> dict:
@@ -50,7 +73,7 @@ def cpu_baseline(n_frames: int, nfeatures: int, W: int, H: int) -> dict:
     import oracle  # test/baseline infrastructure only
     from concurrent.futures import ThreadPoolExecutor
     from forest_slam_amd import synth
-    cores = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
+    cores = cpu_threads()
     n_mt = max(n_frames, cores * 2)
     rdev = "cuda" if torch.cuda.is_available() else "cpu"  # rendering only; the timed work is host C++
     seq = synth.StereoSequence(seed=0, n_frames=n_mt + 1, W=W, H=H, device=rdev)
@@ -72,7 +95,7 @@ def cpu_baseline(n_frames: int, nfeatures: int, W: int, H: int) -> dict:
         list(ex.map(one, range(n_mt)))
         dtm = time.perf_counter() - t0
     return {"value": n_mt / dtm, "unit": "frames/s", "cores": cores, "kind": "port",
-            "value_1core": n_frames / dt1,
+            "value_1core": n_frames / dt1, "host_cpus": host_cpus(),
             "sample": f"{W}x{H} synthetic stereo frames, nfeatures={nfeatures}: 4 ORB + 2 BF-xcheck + "
                       f"SGBM-3way + back-projection + PnP-RANSAC per frame, oracle/ scalar C++; {n_mt} frames "
                       f"over {cores} threads in {dtm:.1f} s; {n_frames} frames on 1 thread in {dt1:.1f} s"}
@@ -94,7 +117,7 @@ def cpu_reference_ate(L_all, R_all, K, stamps, gt, nfeatures: int) -> dict:
         return oracle.frame_pose(imgs[i - 1][0], imgs[i - 1][1], imgs[i][0], K, synth.DIST_L, synth.BASELINE,
                                  nfeatures)["T"]
 
-    cores = max(1, min(16, os.cpu_count() or 1))
+    cores = cpu_threads()
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=cores) as ex:
         Ts = list(ex.map(one, range(1, len(imgs))))
@@ -111,47 +134,66 @@ KERNEL_SYMBOL = {"sgbm_horiz": "k_sg_horiz", "sgbm_vert": "k_sg_costvert",
                  "pnp_ransac": "k_pnp_hyp", "bf_argmin": "k_bf_argmin"}
 
 
-def pmc_traffic(stage: str):
-    """HBM bytes per launch of the stage's kernel from the newest committed PMC summary
-    (profiles/<round>/pmc_per_kernel.csv, written by profiles/collect.sh from separate
-    FETCH_SIZE / WRITE_SIZE passes of this same bench command; gfx950 corrections applied
-    there).  None when no summary covers the kernel."""
+def shape_key(W: int, H: int, N: int, B: int, K: int) -> str:
+    """Workload key of the committed PMC summaries: counters collected at another shape are
+    never reported for this one."""
+    return f"{W}x{H}_n{N}_b{B}_k{K}"
+
+
+def _pmc_rows(name: str, shape: str):
+    """Rows of the newest profiles/<round>/<name> whose `shape` column equals `shape`."""
     import csv
     import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)), reverse=True):
+        with open(path) as f:
+            rows = [r for r in csv.DictReader(f) if r.get("shape") == shape]
+        if rows:
+            return rows, os.path.relpath(path, ROOT)
+    return [], None
+
+
+def pmc_traffic(stage: str, shape: str):
+    """HBM bytes per launch of the stage's kernel from the newest committed PMC summary of
+    this workload shape (profiles/<round>/pmc_per_kernel.csv, written by profiles/collect.sh
+    from separate FETCH_SIZE / WRITE_SIZE passes of this same bench command; gfx950
+    corrections applied there).  None when no summary covers the kernel at this shape."""
     sym = KERNEL_SYMBOL.get(stage)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_per_kernel.csv")))
-    if not sym or not files:
-        return None, None
-    with open(files[-1]) as f:
-        for row in csv.DictReader(f):
-            if row["kernel"].startswith(sym):
-                return float(row["hbm_bytes_per_dispatch_corrected"]), os.path.relpath(files[-1], ROOT)
+    rows, src = _pmc_rows("pmc_per_kernel.csv", shape)
+    for row in rows:
+        if sym and row["kernel"].startswith(sym):
+            return float(row["hbm_bytes_per_dispatch_corrected"]), src
     return None, None
 
 
 F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense FP64 matrix (spec); the PMC busy-cycle ratio agrees (DESIGN §4.3)
 
 
-def pmc_mfma(kernel: str = "k_ba_lin"):
-    """MFMA utilisation of the BA Schur kernel from the newest committed MFMA PMC summary
-    (profiles/<round>/mfma_per_kernel.csv, tools/mfma_pmc.sh: SQ_VALU_MFMA_BUSY_CYCLES,
-    SQ_INSTS_VALU_MFMA_MOPS_F64, GRBM_GUI_ACTIVE over this bench command)."""
-    import csv
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "mfma_per_kernel.csv")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        for row in csv.DictReader(f):
-            if row["kernel"] == kernel:
-                tf = float(row["f64_mfma_tflops"])
-                return {"kernel": kernel, "dtype": "f64", "mfma_util": float(row["mfma_util"]),
-                        "achieved_tflops": tf, "peak_tflops": F64_MFMA_PEAK_TFLOPS,
-                        "frac": round(tf / F64_MFMA_PEAK_TFLOPS, 4),
-                        "flops_per_launch": float(row["avg_f64_mfma_flops"]),
-                        "avg_launch_ms_profiled": float(row["avg_ms"]),
-                        "source": os.path.relpath(files[-1], ROOT)}
+def pmc_mfma(shape: str, kernel: str = "k_ba_lin"):
+    """MFMA utilisation of the BA Schur kernel from the newest committed MFMA PMC summary of
+    this workload shape (profiles/<round>/mfma_per_kernel.csv, tools/mfma_pmc.sh:
+    SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_MOPS_F64, GRBM_GUI_ACTIVE over this bench
+    command)."""
+    rows, src = _pmc_rows("mfma_per_kernel.csv", shape)
+    for row in rows:
+        if row["kernel"] == kernel:
+            tf = float(row["f64_mfma_tflops"])
+            return {"kernel": kernel, "dtype": "f64", "mfma_util": float(row["mfma_util"]),
+                    "achieved_tflops": tf, "peak_tflops": F64_MFMA_PEAK_TFLOPS,
+                    "frac": round(tf / F64_MFMA_PEAK_TFLOPS, 4),
+                    "flops_per_launch": float(row["avg_f64_mfma_flops"]),
+                    "avg_launch_ms_profiled": float(row["avg_ms"]), "source": src}
     return None
+
+
+def pmc_valu(shape: str):
+    """VALU utilisation per hot kernel from the newest committed
+    profiles/<round>/valu_per_kernel.csv of this shape (tools/valu_pmc.sh)."""
+    rows, src = _pmc_rows("valu_per_kernel.csv", shape)
+    if not rows:
+        return None
+    return {"source": src, "kernels": {r["kernel"]: {"valu_busy": float(r["valu_busy"]),
+                                                     "valu_insts_per_launch": float(r["avg_SQ_INSTS_VALU"])}
+                                       for r in rows}}
 
 
 def main():
@@ -204,19 +246,19 @@ def main():
                            ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm),
                            sgbm_priority=args.sgbm_priority, **ba_caps)
     fe.prime(L_all[0], R_all[0])
-    Lb, Rb = L_all[1:].contiguous(), R_all[1:].contiguous()
-
-    map_exchange = dist is not None and args.ba_window > 0
-    if map_exchange:
-        from forest_slam_amd import dist as fdist
-        lm_out = (torch.empty((int(fe.ctx.cfg.ba_max_landmarks), 3), dtype=torch.float64, device=dev),
-                  torch.empty((1,), dtype=torch.int32, device=dev))
+    # Steps walk the rendered frames forward (1..B) then backward (B-1..0) and so on, so every
+    # frame pair the front end sees -- including the carried pair across a step boundary -- is
+    # a real pair of adjacent frames (ping-pong instead of re-feeding frames 1..B after B).
+    fwd = (L_all[1:].contiguous(), R_all[1:].contiguous())
+    bwd = (L_all[:B].flip(0).contiguous(), R_all[:B].flip(0).contiguous())
+    from forest_slam_amd import dist as fdist
+    rank_step = fdist.SequenceRank(fe)  # front-end step + (world > 1, local BA) the RCCL map exchange
+    nstep = [0]
 
     def step():
-        T, _ = fe.step(Lb, Rb)
-        if map_exchange:  # the multi-sequence map: refined poses + latest keyframe window (RCCL)
-            xyz, cnt = fe.ctx.ba_landmarks(B - 1, out=lm_out)
-            fdist.exchange_window_map(T, xyz, cnt)
+        Lb, Rb = fwd if nstep[0] % 2 == 0 else bwd
+        nstep[0] += 1
+        rank_step.step(Lb, Rb)
 
     for _ in range(max(args.warmup, 1)):
         step()
@@ -268,7 +310,8 @@ def main():
     frames_per_launch = B  # every kernel of the step processes the whole batch in one launch
     bpf = algorithmic_bytes_per_frame(W, H, args.nfeatures)
     achieved = bpf * frames_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(dom)
+    shape = shape_key(W, H, args.nfeatures, B, args.ba_window)
+    traffic, traffic_src = pmc_traffic(dom, shape)
     traffic_rate = traffic / avg_launch_s / 1e9 if (traffic and avg_launch_s > 0) else None
 
     ate = None
@@ -283,9 +326,17 @@ def main():
         r = ev.ate(gt, rows)
         ate = {"rmse_m": round(r["rmse"], 4), "frames": int(aseq.n), "poses": r["n"],
                "pnp_failures": int((st == 0).sum()), "skipped": int((st == -1).sum())}
+        # evo RPE (point-distance error ratio, consecutive pairs, Sim(3)); the 200-frame run
+        # covers ~25 m of the 1018_00 path, so delta is 5 m here (the reference's plots: 20 m
+        # over the 113.8 m sequence)
+        rp = ev.rpe(gt, rows, delta=RPE_DELTA_M)
+        ate["rpe"] = ({"delta_m": RPE_DELTA_M, "pairs": rp["n"], "rmse_pct": round(rp["rmse"], 3),
+                       "mean_pct": round(rp["mean"], 3), "median_pct": round(rp["median"], 3)} if rp["n"] else None)
         if args.ba_window:
             rows_p, _, _ = vo.run_sequence(afe, La, Ra, aseq.t, use_ba=False)
             ate["rmse_m_pnp_only"] = round(ev.ate(gt, rows_p)["rmse"], 4)
+            rpp = ev.rpe(gt, rows_p, delta=RPE_DELTA_M)
+            ate["rpe_mean_pct_pnp_only"] = round(rpp["mean"], 3) if rpp["n"] else None
             ate["local_ba"] = f"K={args.ba_window}"
         else:
             rows_p = rows
@@ -315,8 +366,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "mixed: u8/i16 integer (FAST, BRIEF, Hamming, SGM), f32 (ORB angle/Harris, back-projection, "
-                     "BA Schur GEMM on MFMA), f64 (PnP, BA)",
+            "dtype": "mixed: u8/u16 integer (FAST, BRIEF, Hamming, SGM), f32 (ORB angle/Harris, back-projection), "
+                     "f64 (PnP, BA incl. its Schur GEMM on f64 MFMA)",
             "data": "synthetic: ray-cast forest stereo along the 1018_00 GT path (seed = rank), "
                     "BotanicGarden bag not available",
             "config": {"workload": f"stereo VO front end, {cfg_name}: {W}x{H}, ORB nfeatures={args.nfeatures}, "
@@ -339,7 +390,9 @@ def main():
                          "traffic_rate_gbs_in_order": round(traffic / avg_launch_io_s / 1e9, 1)
                          if (traffic and avg_launch_io_s > 0) else None},
             "cpu_baseline": cpu,
-            "ba_mfma": pmc_mfma() if args.ba_window else None,
+            "ba_mfma": pmc_mfma(shape) if args.ba_window else None,
+            "valu": pmc_valu(shape),
+            "pmc_shape": shape,
             "ate": ate,
             "stages_ms_per_step": stage_ms,
             "workspace_gb": round(fe.ctx.workspace_bytes / 1e9, 2),

@@ -39,6 +39,8 @@ _L = ctypes.c_int64
 SIGNATURES = {
     "fvo_abi_version": (ctypes.c_int, []),
     "fvo_config_default": (None, [ctypes.POINTER(FvoConfig), _I, _I]),
+    "fvo_config_size": (ctypes.c_int32, []),
+    "fvo_config_offset": (ctypes.c_int32, [ctypes.c_char_p]),
     "fvo_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(FvoConfig), ctypes.POINTER(_P)]),
     "fvo_destroy": (None, [_P]),
     "fvo_last_error": (ctypes.c_char_p, [_P]),
@@ -73,6 +75,16 @@ SIGNATURES = {
 }
 
 
+def check_config_layout(L) -> None:
+    """Refuse a library whose fvo_config layout differs from FvoConfig (size and every
+    field offset), so fvo_config_default can never write past the ctypes struct."""
+    if L.fvo_config_size() != ctypes.sizeof(FvoConfig):
+        raise RuntimeError(f"fvo_config is {L.fvo_config_size()} B in libfvo.so, {ctypes.sizeof(FvoConfig)} B here")
+    for name, _ in FvoConfig._fields_:
+        if L.fvo_config_offset(name.encode()) != getattr(FvoConfig, name).offset:
+            raise RuntimeError(f"fvo_config.{name} offset differs between libfvo.so and the binding")
+
+
 def kernel_names() -> list[str]:
     L = load()
     return [L.fvo_kernel_name(i).decode() for i in range(L.fvo_kernel_count())]
@@ -92,6 +104,7 @@ def load(path: str = LIB_PATH):
             fn.argtypes = args
         if L.fvo_abi_version() != ABI_VERSION:
             raise RuntimeError("libfvo.so ABI version mismatch")
+        check_config_layout(L)
         _lib = L
     return _lib
 

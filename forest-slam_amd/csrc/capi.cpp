@@ -1,5 +1,6 @@
 // extern "C" entry points of libfvo.so (include/fvo.h).  Thin: argument checks, context
 // lifetime, dispatch to the per-stage launchers.  No allocation in the hot calls.
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 
@@ -21,9 +22,29 @@ hipEvent_t fvo_event(fvo_ctx* ctx) {
   return e;
 }
 
+// The ABI layout: 26 int32 / float fields + sgbm_max_batch, no padding (include/fvo.h).
+static_assert(sizeof(fvo_config) == 27 * 4, "fvo_config layout changed: bump FVO_ABI_VERSION");
+static_assert(offsetof(fvo_config, scale_factor) == 16 && offsetof(fvo_config, sgbm_max_batch) == 104,
+              "fvo_config field offsets changed: bump FVO_ABI_VERSION");
+
 extern "C" {
 
 int fvo_abi_version(void) { return FVO_ABI_VERSION; }
+
+int32_t fvo_config_size(void) { return (int32_t)sizeof(fvo_config); }
+
+int32_t fvo_config_offset(const char* f) {
+  if (!f) return -1;
+#define FVO_OFS(name) if (!std::strcmp(f, #name)) return (int32_t)offsetof(fvo_config, name);
+  FVO_OFS(width) FVO_OFS(height) FVO_OFS(max_batch) FVO_OFS(nfeatures) FVO_OFS(scale_factor) FVO_OFS(nlevels)
+  FVO_OFS(edge_threshold) FVO_OFS(first_level) FVO_OFS(wta_k) FVO_OFS(score_type) FVO_OFS(patch_size)
+  FVO_OFS(fast_threshold) FVO_OFS(min_disparity) FVO_OFS(num_disparities) FVO_OFS(block_size) FVO_OFS(P1)
+  FVO_OFS(P2) FVO_OFS(disp12_max_diff) FVO_OFS(pre_filter_cap) FVO_OFS(uniqueness_ratio) FVO_OFS(sgbm_stripes)
+  FVO_OFS(kp_capacity) FVO_OFS(stages) FVO_OFS(ba_window) FVO_OFS(ba_max_landmarks) FVO_OFS(ba_max_obs)
+  FVO_OFS(sgbm_max_batch)
+#undef FVO_OFS
+  return -1;
+}
 
 void fvo_config_default(fvo_config* c, int32_t width, int32_t height) {
   std::memset(c, 0, sizeof(*c));

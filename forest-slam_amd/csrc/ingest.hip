@@ -327,6 +327,9 @@ int motion_blur_run(fvo_ctx* ctx, const uint8_t* img, int batch, int64_t sstride
   const int64_t mstride = (int64_t)W * H;
   const int half = ksize / 2;
   const bool seeds = cap > 0;
+  // k_mb_fix rewrites the mask a dword at a time: refuse a misaligned mask before any launch,
+  // so an error never leaves the mask in its intermediate (seed / dilated bit) encoding
+  if (seeds && (((uintptr_t)mask) & 3)) return fvo_fail(ctx, "motion blur: mask must be 4-byte aligned");
   if (seeds) {
     FVO_HIP(ctx, hipMemsetAsync(mask, 0, (size_t)mstride * batch, s));
     hipLaunchKernelGGL(k_mb_seed, dim3((cap + 255) / 256, batch), dim3(256), 0, s, centers, ncent, cap, mask, mstride,
@@ -349,7 +352,6 @@ int motion_blur_run(fvo_ctx* ctx, const uint8_t* img, int batch, int64_t sstride
 #undef FVO_MB
   FVO_LAUNCH_CHECK(ctx);
   if (seeds) {
-    if (((uintptr_t)mask) & 3) return fvo_fail(ctx, "motion blur: mask must be 4-byte aligned");
     const int64_t n = mstride * batch;
     hipLaunchKernelGGL(k_mb_fix, dim3((unsigned)((n / 4 + 256) / 256)), dim3(256), 0, s, mask, n);
     FVO_LAUNCH_CHECK(ctx);

@@ -5,8 +5,15 @@
 * Frame-pair sharding inside ONE sequence: frame pairs are independent (SURVEY.md F8);
   rank r processes pairs [s_r, e_r) reading images [s_r - 1, e_r) (one-image halo), then
   the relative poses are exchanged with one all-gather and every rank composes the chain
-  left to right in float64 — bit-identical to the single-GPU chain (stereo_slam.py:306).
+  left to right in float64.  For the PnP-only path (ba_window = 0) this is bit-identical to
+  the single-GPU chain (stereo_slam.py:306).  With local BA a window needs the K-1 frames
+  before its last one: ``frame_shard(..., halo=K-1)`` starts the rank's front end K-1 images
+  earlier and ``warmup_pairs`` of its first results (the windows that reach back past the
+  shard start on one GPU but not here) are discarded — the previous rank owns those pairs.
   ``frame_shard`` / ``gather_relative_poses``.
+* ``SequenceRank`` — one rank's step of the multi-sequence run (bench.py, tests): the
+  front-end step, the latest BA window's landmarks (``fvo_ba_landmarks``) and the map
+  exchange (``exchange_window_map``).
 * Keyframe exchange for the multi-sequence map: ``allgather_keyframes`` (poses + landmark
   positions, tens of KB: latency-bound, one collective per window step).
 
@@ -24,13 +31,20 @@ def sequences_for_rank(rank: int, world: int, n_sequences: int) -> list[int]:
     return list(range(rank, n_sequences, world))
 
 
-def frame_shard(n_pairs: int, rank: int, world: int) -> tuple[int, int]:
+def frame_shard(n_pairs: int, rank: int, world: int, halo: int = 0) -> tuple[int, int]:
     """Contiguous shard [start, end) of the frame-pair indices 1..n_pairs (pair i uses
-    images i-1 and i), balanced to within one pair."""
+    images i-1 and i), balanced to within one pair.  ``halo`` > 0 (local BA: K-1) moves the
+    start back by up to that many pairs; the caller drops the first ``start_owned - start``
+    results (``warmup_pairs``)."""
     q, r = divmod(n_pairs, world)
     start = rank * q + min(rank, r)
     end = start + q + (1 if rank < r else 0)
-    return 1 + start, 1 + end
+    return 1 + max(0, start - halo), 1 + end
+
+
+def warmup_pairs(n_pairs: int, rank: int, world: int, halo: int) -> int:
+    """Number of leading results of a halo'd shard that belong to the previous rank."""
+    return frame_shard(n_pairs, rank, world)[0] - frame_shard(n_pairs, rank, world, halo)[0]
 
 
 def gather_relative_poses(T_local: torch.Tensor, status_local: torch.Tensor, n_pairs: int,
@@ -59,15 +73,44 @@ def exchange_window_map(T_step: torch.Tensor, lm_xyz: torch.Tensor, lm_count: to
     BA-refined relative poses of the step (f64 [B,4,4]) and its latest window's landmarks
     (f64 [Lmax,3] + i32 [1] count, fixed size) are all-gathered over RCCL.  Fixed shapes and
     device-side counts: no host synchronisation, the collectives queue behind the step's
-    kernels.  Returns (T [world,B,4,4], xyz [world,Lmax,3], counts [world,1])."""
+    kernels.  Returns (T [world,B,4,4], xyz [world,Lmax,3], counts [world,1]) on the inputs'
+    device.  Under the gloo backend (CPU tests, or GPU ranks sharing one card) the tensors
+    go through host copies."""
     world = dist.get_world_size(group)
-    outT = [torch.empty_like(T_step) for _ in range(world)]
-    outX = [torch.empty_like(lm_xyz) for _ in range(world)]
-    outC = [torch.empty_like(lm_count) for _ in range(world)]
-    dist.all_gather(outT, T_step.contiguous(), group=group)
-    dist.all_gather(outX, lm_xyz.contiguous(), group=group)
-    dist.all_gather(outC, lm_count.contiguous(), group=group)
-    return torch.stack(outT), torch.stack(outX), torch.stack(outC)
+    host = dist.get_backend(group) == "gloo" and T_step.is_cuda
+    dev = T_step.device
+    ins = [t.contiguous().cpu() if host else t.contiguous() for t in (T_step, lm_xyz, lm_count)]
+    outs = []
+    for t in ins:
+        o = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(o, t, group=group)
+        outs.append(torch.stack(o).to(dev) if host else torch.stack(o))
+    return tuple(outs)
+
+
+class SequenceRank:
+    """One rank of the sequence-per-GPU run: ``step`` = the front end's step over the rank's
+    next frames, then the exchange of the refined poses and of the latest BA window's
+    landmarks with every other rank (``exchange_window_map``; skipped for world size 1 or
+    without local BA).  Returns (T, status, gathered) with gathered = None or the
+    (T, xyz, counts) all-gather result."""
+
+    def __init__(self, frontend, group=None):
+        self.fe = frontend
+        self.group = group
+        self.exchange = dist.is_available() and dist.is_initialized() and frontend.ba_window > 0
+        if self.exchange:
+            dev = frontend.dev
+            self.lm_out = (torch.empty((int(frontend.ctx.cfg.ba_max_landmarks), 3), dtype=torch.float64, device=dev),
+                           torch.empty((1,), dtype=torch.int32, device=dev))
+
+    def step(self, L: torch.Tensor, R: torch.Tensor):
+        T, st = self.fe.step(L, R)
+        gathered = None
+        if self.exchange:
+            xyz, cnt = self.fe.ctx.ba_landmarks(L.shape[0] - 1, out=self.lm_out)
+            gathered = exchange_window_map(T, xyz, cnt, self.group)
+        return T, st, gathered
 
 
 def allgather_keyframes(poses: torch.Tensor, landmarks: torch.Tensor, group=None):

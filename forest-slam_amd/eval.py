@@ -7,6 +7,11 @@
   (``evo_ape tum GT EST -as``), nearest-timestamp association within 0.01 s.
   Pinned in tests against the reference's own result files: ORB_BF_Stereo 1018_00 ->
   1.1565 m, and the colour-bar extents of three evo plots (Appendix B).
+* RPE: evo-equivalent relative pose error, point-distance error ratio (%) for delta = 20 m
+  over consecutive pairs, Sim(3)-aligned (``evo_rpe tum GT EST -as --delta 20 --delta_unit m
+  --pose_relation point_distance_error_ratio``) — the metric of the reference's
+  ``pose_estimation_results/1018_00/1018-00-{Stereo,Mono}-rpe.png``; pinned in tests against
+  the per-pair values and statistics read off those two plots.
 """
 from __future__ import annotations
 
@@ -111,3 +116,50 @@ def chain(rel: np.ndarray, valid: np.ndarray | None = None) -> np.ndarray:
         cum = np.dot(cum, rel[i])
         out.append(cum.copy())
     return np.array(out).reshape(-1, 4, 4)
+
+
+def path_pairs(positions: np.ndarray, delta: float) -> list[tuple[int, int]]:
+    """evo ``filters.filter_pairs_by_path`` (consecutive pairs): walk the trajectory
+    accumulating the travelled distance; every index where it reaches ``delta`` (metres) is a
+    pair boundary and the counter restarts there.  Pairs join consecutive boundaries (the
+    start pose is not a boundary: 4 pairs for the 113.8 m of 1018_00 at delta 20 m)."""
+    ids = []
+    prev = positions[0]
+    acc = 0.0
+    for i, p in enumerate(positions):
+        acc += float(np.linalg.norm(p - prev))
+        prev = p
+        if acc >= delta:
+            ids.append(i)
+            acc = 0.0
+    return list(zip(ids, ids[1:]))
+
+
+def rpe(ref: np.ndarray, est: np.ndarray, delta: float = 20.0, align: str = "sim3", max_diff: float = 0.01,
+        pairs_from_reference: bool = False) -> dict:
+    """RPE w.r.t. the point-distance error ratio (%), evo semantics: associate (as ``ate``),
+    align the estimate (Sim(3) Umeyama by default), pick consecutive pairs (i, j) ``delta``
+    metres of path apart on the aligned estimate (evo's default; the reference's with
+    ``pairs_from_reference``), and per pair
+    ``100 * | |p_ref[j] - p_ref[i]| - |p_est[j] - p_est[i]| | / |p_ref[j] - p_ref[i]|``
+    (the norm of the relative SE(3) translation is the position distance).  ``t`` is the
+    estimate stamp of each pair's second pose, ``t_rel`` that minus the first stamp."""
+    ir, ie = associate(ref[:, 0], est[:, 0], max_diff)
+    P = est[ie, 1:4]
+    Q = ref[ir, 1:4]
+    if align in ("sim3", "se3"):
+        s, R, t = umeyama(P, Q, align == "sim3")
+        P = (s * (R @ P.T)).T + t
+    pairs = path_pairs(Q if pairs_from_reference else P, delta)
+    if not pairs:
+        return dict(values=np.zeros(0), t=np.zeros(0), t_rel=np.zeros(0), n=0, rmse=float("nan"),
+                    mean=float("nan"), median=float("nan"), pairs=[])
+    i, j = np.array(pairs).T
+    dr = np.linalg.norm(Q[j] - Q[i], axis=1)
+    de = np.linalg.norm(P[j] - P[i], axis=1)
+    nz = dr > 0
+    e = np.abs(dr - de)[nz] / dr[nz] * 100.0
+    ts = est[ie, 0]
+    return dict(values=e, t=ts[j[nz]], t_rel=ts[j[nz]] - ts[0], n=int(len(e)), rmse=float(np.sqrt(np.mean(e ** 2))),
+                mean=float(e.mean()), median=float(np.median(e)), std=float(e.std()), min=float(e.min()),
+                max=float(e.max()), pairs=pairs)

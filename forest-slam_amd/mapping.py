@@ -35,12 +35,23 @@ class PointMap:
             raise RuntimeError(f"PointMap overflow: {n} points for capacity {self.capacity}")
         return n
 
-    def add_frames(self, points: torch.Tensor, n_points: torch.Tensor, cum: np.ndarray | torch.Tensor):
+    def add_frames(self, points: torch.Tensor, n_points: torch.Tensor, cum: np.ndarray | torch.Tensor,
+                   check: bool = False):
         """points f32 [B,cap,3] (device), n_points i32 [B] (device; 0 for frames the reference
-        skips), cum f64 [B,4,4] (each frame's cumulative pose, stereo_slam.py:306)."""
+        skips), cum f64 [B,4,4] (each frame's cumulative pose, stereo_slam.py:306).
+
+        The device counter keeps counting points past ``capacity`` (they are not written), so
+        an overflow is detected exactly by the next ``len()``; ``check=True`` synchronises
+        and raises right here instead, before another batch is appended."""
         T = torch.as_tensor(np.asarray(cum, np.float64) if not isinstance(cum, torch.Tensor) else cum,
                             dtype=torch.float64).to(self.dev)
         self.ctx.map_transform(points, n_points, T, self.count, self.xyz64, self.xyz32)
+        if check:
+            len(self)
+
+    def overflowed(self) -> bool:
+        """True once more points were appended than the map holds (host sync)."""
+        return int(self.count.item()) > self.capacity
 
     def add_cloud(self, points, cum, voxel_size: float = 0.5):
         """mono_slam.py:144-164: points f32 [n,3] (PointCloud2 x/y/z), pose cum f64 [4,4]."""

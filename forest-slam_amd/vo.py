@@ -26,6 +26,12 @@ import torch
 from . import _lib
 
 
+# step() status codes: 1 pose valid, 0 RANSAC failed, -1 skipped (< 6 points, the reference's
+# guard at stereo_slam.py:292), STATUS_KP_OVERFLOW: an image of the pair had more ORB keypoints
+# than the context's kp_capacity (no result; raise kp_capacity).
+STATUS_KP_OVERFLOW = -3
+
+
 class StereoFrontEnd:
     def __init__(self, width: int, height: int, K: np.ndarray, dist: np.ndarray, baseline: float, batch: int,
                  nfeatures: int = 500, match_right: bool = True, device=None, ba_window: int = 10,
@@ -174,6 +180,10 @@ class StereoFrontEnd:
         rv, tv, T, st, _ = ctx.pnp_ransac(P3, p2, npts, self.K, self.dist,
                                           out=(self.rvec[:n], self.tvec[:n], self.T[:n], self.status[:n],
                                                self.inl[:n]))
+        # ORB writes -(needed) when a frame has more keypoints than kp_capacity (its outputs
+        # are then unspecified): mark the frame STATUS_KP_OVERFLOW instead of letting it pass
+        # as a "fewer than 6 points" skip (device-side, no host sync)
+        st.masked_fill_((cnt[:n] < 0) | (self.q_cnt[:n] < 0), STATUS_KP_OVERFLOW)
         out = T
         if self.ba_window:
             out = self._local_ba(n, kp, cnt, m, nm, disp, T)
@@ -211,6 +221,13 @@ class StereoFrontEnd:
         return Tba
 
 
+def _check_overflow(st: np.ndarray):
+    bad = np.nonzero(st == STATUS_KP_OVERFLOW)[0]
+    if len(bad):
+        raise RuntimeError(f"ORB keypoint capacity exceeded on frame pair(s) {bad[:8].tolist()}: "
+                           "create the front end with a larger kp_capacity")
+
+
 def run_sequence(frontend: StereoFrontEnd, L_all: torch.Tensor, R_all: torch.Tensor, stamps=None,
                  use_ba: bool = True):
     """Process a whole sequence (images on device) -> (TUM rows, relative poses, statuses).
@@ -228,6 +245,7 @@ def run_sequence(frontend: StereoFrontEnd, L_all: torch.Tensor, R_all: torch.Ten
         sts.append(st.cpu().numpy())
     T = np.concatenate(Ts) if Ts else np.zeros((0, 4, 4))
     st = np.concatenate(sts) if sts else np.zeros((0,), np.int32)
+    _check_overflow(st)
     # status -1 = fewer than 6 points: the reference skips the frame (no pose, no TUM row,
     # stereo_slam.py:292); status 0 = RANSAC failure: identity T (the reference would chain
     # whatever solvePnPRansac left in rvec/tvec), row emitted.
@@ -247,7 +265,8 @@ class MonoFrontEnd:
     the host (``eval.chain``); translations are unit-norm (mono is scale-free).
 
     ``step`` status per frame: 1 pose valid; 0 RANSAC found no model, -1 fewer than 5
-    matches, -2 five matches with several solutions — the cases where the reference's
+    matches, -2 five matches with several solutions, -3 (STATUS_KP_OVERFLOW) keypoint
+    capacity exceeded — the cases where the reference's
     cv2.recoverPose would raise; T is the identity there."""
 
     def __init__(self, width: int, height: int, K: np.ndarray, batch: int, nfeatures: int = 500, device=None,
@@ -316,6 +335,7 @@ class MonoFrontEnd:
                                       out=(self.E[:n], self.mask[:n], self.status[:n]))
         _, _, T, _ = ctx.recover_pose(E, p0, p1, npts, self.focal, self.pp, e_status=st,
                                       out=(self.R[:n], self.t[:n], self.T[:n], self.ngood[:n]))
+        st.masked_fill_((cnt[:n] < 0) | (self.q_cnt[:n] < 0), STATUS_KP_OVERFLOW)
         self.last_kp.copy_(kp[n - 1])
         self.last_desc.copy_(desc[n - 1])
         self.last_cnt.copy_(cnt[n - 1:n])
@@ -338,6 +358,7 @@ def run_mono_sequence(frontend: MonoFrontEnd, imgs: torch.Tensor, stamps=None, f
         sts.append(st.cpu().numpy())
     T = np.concatenate(Ts) if Ts else np.zeros((0, 4, 4))
     st = np.concatenate(sts) if sts else np.zeros((0,), np.int32)
+    _check_overflow(st)
     cum = ev.chain(T, np.ones(len(T), bool))
     rows = ev.tum_rows(np.asarray(stamps)[sel[1:]], cum)
     return rows, T, st

@@ -15,7 +15,8 @@
  *   fvo_pnp_ransac          <- cv2.solvePnPRansac(P, p, K0, dist_l, reprojectionError=1.0,
  *                              confidence=0.99, iterationsCount=1000, SOLVEPNP_ITERATIVE)
  *                              + cv2.Rodrigues + T assembly, stereo_slam.py:292-303
- *   fvo_ba_window           <- (new) windowed bundle adjustment, no reference counterpart
+ *   fvo_ba_windows          <- (new) windowed local bundle adjustment, no reference counterpart
+ *                              (+ fvo_keypoint_stereo, fvo_ba_landmarks)
  *   fvo_gather_matches      <- mkpts0 = kpts0[valid], mkpts1 = kpts1[matches[valid]]
  *                              mono_slam.py:106-108 (stereo_slam.py:235-238 for the BF DMatch list)
  *   fvo_find_essential      <- cv2.findEssentialMat(mkpts0, mkpts1, focal=K0[0,0], pp=(K0[0,2], K0[1,2]),
@@ -108,6 +109,12 @@ typedef struct fvo_config {
 
 /* Fill `cfg` with the reference's parameters for a width x height image. */
 void fvo_config_default(fvo_config* cfg, int32_t width, int32_t height);
+
+/* Layout of fvo_config as this library was compiled: sizeof, and offsetof(field) in bytes
+ * (-1 for an unknown name).  A binding that declares the struct itself (ctypes, cffi, cgo)
+ * checks its declaration against these before calling fvo_config_default / fvo_create. */
+int32_t fvo_config_size(void);
+int32_t fvo_config_offset(const char* field);
 
 int fvo_create(int device, const fvo_config* cfg, fvo_ctx** out);
 void fvo_destroy(fvo_ctx* ctx);

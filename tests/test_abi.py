@@ -56,3 +56,41 @@ def test_context_fails_loudly_without_gpu():
     from forest_slam_amd import _lib
     with pytest.raises(RuntimeError):
         _lib.Context(960, 600)
+
+
+def test_config_layout_matches_binding():
+    """the ctypes FvoConfig must match the compiled struct exactly (size and
+    every field offset), or fvo_config_default writes past the Python object."""
+    from forest_slam_amd import _lib
+    L = _lib.load()
+    assert L.fvo_config_size() == ctypes.sizeof(_lib.FvoConfig) == 27 * 4
+    for name, _ in _lib.FvoConfig._fields_:
+        assert L.fvo_config_offset(name.encode()) == getattr(_lib.FvoConfig, name).offset, name
+    assert L.fvo_config_offset(b"no_such_field") == -1
+    # every field the header declares is in the binding (and nothing else)
+    src = open(os.path.join(ROOT, "include", "fvo.h")).read()
+    body = src[src.index("typedef struct fvo_config {"):src.index("} fvo_config;")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    declared = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*(?:,|;)", body.split("{", 1)[1])
+    assert declared == [n for n, _ in _lib.FvoConfig._fields_]
+
+
+def test_integration_raw_binding_snippet_runs_to_create():
+    """The raw ctypes binding printed in INTEGRATION.md, executed verbatim up to its device
+    calls: layout asserts pass, fvo_config_default fills the reference constants without
+    overrunning the struct, and fvo_create returns a status (no GPU here: < 0, cleanly)."""
+    import forest_slam_amd.build as b
+    b.build()
+    md = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    block = re.search(r"```python\n(import ctypes\n.*?)```", md, flags=re.S).group(1)
+    code = block.split("# --- device calls")[0]
+    code = code.replace('"forest-slam_amd/libfvo.so"', repr(os.path.join(ROOT, "forest-slam_amd", "libfvo.so")))
+    ns = {}
+    exec(compile(code, "INTEGRATION.md", "exec"), ns)
+    cfg = ns["cfg"]
+    assert (cfg.width, cfg.height, cfg.nfeatures, cfg.num_disparities, cfg.P2, cfg.sgbm_max_batch) == \
+        (960, 600, 500, 96, 1568, 0)
+    if gpu_available():
+        assert ns["rc"] == 0
+    else:
+        assert ns["rc"] < 0 and not ns["ctx"].value

@@ -67,3 +67,45 @@ def test_chain_is_left_to_right_and_skips_invalid():
     assert np.allclose(out[1], A @ A)
     out = ev.chain(np.stack([A, Bm, A]))
     assert np.allclose(out[2], np.dot(np.dot(A, Bm), A))
+
+
+# Values read off the reference's evo RPE plots (pose_estimation_results/1018_00/
+# 1018-00-Stereo-rpe.png and 1018-00-Mono-rpe.png: "RPE w.r.t. point distance error ratio (%)
+# for delta = 20.0 (m) using consecutive pairs (with Sim(3) Umeyama alignment)"): per-pair
+# (seconds from start, RPE %) vertices of the grey curve and the rmse / mean / median lines.
+# The plot reading resolution is ~0.05 % and ~0.3 s.
+RPE_PLOTS = {
+    "1018_00_SuperPoint_SuperGlue_Stereo": dict(
+        t=[35.5, 49.8, 65.2, 79.3], v=[4.62, 0.37, 0.51, 1.14], rmse=2.40, mean=1.65, median=0.82),
+    "1018_00_SuperPoint_SuperGlue_Mono": dict(
+        t=[29.8, 44.7, 59.6, 74.5, 89.4], v=[6.85, 2.80, 6.03, 5.82, 0.35], rmse=5.00, mean=4.36, median=5.82),
+}
+
+
+@pytest.mark.parametrize("est", sorted(RPE_PLOTS))
+def test_rpe_matches_reference_plots(est):
+    """evo RPE restatement (eval.rpe) reproduces the reference's two RPE plots: the pair
+    count, each pair's time and error ratio, and the summary lines."""
+    from forest_slam_amd import eval as ev
+    want = RPE_PLOTS[est]
+    r = ev.rpe(_load("1018_00_Ground_Truth"), _load(est), delta=20.0)
+    assert r["n"] == len(want["v"])
+    assert np.allclose(r["t_rel"], want["t"], atol=0.35)
+    assert np.allclose(r["values"], want["v"], atol=0.06)
+    for k in ("rmse", "mean", "median"):
+        assert abs(r[k] - want[k]) < 0.06, (k, r[k])
+
+
+def test_rpe_orb_bf_stereo_and_properties():
+    """The ORB+BF stereo result (the reference CPU path; no RPE plot is published for it):
+    4 pairs over the 113.8 m path; identical trajectories give 0 %; a pure scale error of the
+    estimate is removed by the Sim(3) alignment but not by the SE(3) one."""
+    from forest_slam_amd import eval as ev
+    gt, est = _load("1018_00_Ground_Truth"), _load("1018_00_ORB_BF_Stereo")
+    r = ev.rpe(gt, est)
+    assert r["n"] == 4 and 3.9 < r["mean"] < 4.1
+    assert ev.rpe(gt, gt)["rmse"] < 1e-9
+    scaled = gt.copy()
+    scaled[:, 1:4] *= 0.5
+    assert ev.rpe(gt, scaled)["rmse"] < 1e-6
+    assert abs(ev.rpe(gt, scaled, align="se3")["mean"] - 50.0) < 1e-6

@@ -1,0 +1,129 @@
+"""Front-end behaviour on the GPU: keypoint-capacity overflow reporting, frame-pair sharding
+with local BA (K-1 halo), and the multi-rank step (two ranks sharing one card, gloo)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")]
+
+W, H = 320, 200
+
+
+def _frames(seed, n, start=0):
+    from forest_slam_amd import synth
+    seq = synth.StereoSequence(seed=seed, n_frames=n, W=W, H=H, device="cuda", start=start)
+    L, R = seq.frames(range(n))
+    torch.cuda.synchronize()
+    return seq, L, R
+
+
+def _fe(seq, batch, **kw):
+    from forest_slam_amd import synth, vo
+    kw.setdefault("nfeatures", 300)
+    return vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=batch, num_disparities=64, **kw)
+
+
+def test_keypoint_overflow_is_a_status_not_a_skip():
+    """a frame with more ORB keypoints than kp_capacity gets STATUS_KP_OVERFLOW
+    (and run_sequence raises) instead of passing as a "fewer than 6 points" skip."""
+    from forest_slam_amd import vo
+    seq, L, R = _frames(31, 3)
+    fe = _fe(seq, 2, ba_window=0, kp_capacity=64)
+    fe.prime(L[0], R[0])
+    _, st = fe.step(L[1:3], R[1:3])
+    assert (st.cpu().numpy() == vo.STATUS_KP_OVERFLOW).all()
+    with pytest.raises(RuntimeError, match="capacity"):
+        vo.run_sequence(_fe(seq, 2, ba_window=0, kp_capacity=64), L, R)
+    ok = _fe(seq, 2, ba_window=0)
+    ok.prime(L[0], R[0])
+    _, st = ok.step(L[1:3], R[1:3])
+    assert (st.cpu().numpy() != vo.STATUS_KP_OVERFLOW).all()
+
+
+def test_frame_shards_with_ba_halo_equal_single_run():
+    """dist.frame_shard(halo=K-1): each shard's front end starts K-1 frames early and drops
+    warmup_pairs results; the concatenated BA-refined transforms equal one run over the
+    whole sequence bit for bit."""
+    from forest_slam_amd import dist as fd
+    Kw, n, world = 4, 13, 3
+    seq, L, R = _frames(32, n, start=120)
+    fe = _fe(seq, 4, ba_window=Kw)
+    fe.prime(L[0], R[0])
+    full = []
+    for s in range(1, n, 4):
+        T, _ = fe.step(L[s:s + 4], R[s:s + 4])
+        full.append(T.cpu().numpy().copy())
+    full = np.concatenate(full)
+    parts = []
+    for r in range(world):
+        s, e = fd.frame_shard(n - 1, r, world, halo=Kw - 1)
+        drop = fd.warmup_pairs(n - 1, r, world, Kw - 1)
+        f = _fe(seq, 3, ba_window=Kw)
+        f.prime(L[s - 1], R[s - 1])
+        got = []
+        for a in range(s, e, 3):
+            b = min(a + 3, e)
+            T, _ = f.step(L[a:b], R[a:b])
+            got.append(T.cpu().numpy().copy())
+        parts.append(np.concatenate(got)[drop:])
+    assert np.array_equal(np.concatenate(parts), full)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from forest_slam_amd import dist as fd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)  # both ranks share the one card of the box
+    seq, L, R = _frames(40 + rank, 7, start=60 * rank)
+    fe = _fe(seq, 3, ba_window=3)
+    sr = fd.SequenceRank(fe)
+    assert sr.exchange
+    fe.prime(L[0], R[0])
+    res = []
+    for s in (1, 4):
+        T, st, (Tg, Xg, Cg) = sr.step(L[s:s + 3], R[s:s + 3])
+        xyz, cnt = fe.ctx.ba_landmarks(2)
+        torch.cuda.synchronize()
+        c = int(cnt.item())
+        res.append(dict(T=T.cpu().numpy(), xyz=xyz[:c].cpu().numpy(), Tg=Tg.cpu().numpy(), Xg=Xg.cpu().numpy(),
+                        Cg=Cg.cpu().numpy()))
+    out[rank] = res
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_exchange_window_maps():
+    """the bench's multi-rank step (dist.SequenceRank: front-end step ->
+    fvo_ba_landmarks -> exchange_window_map) with two ranks on the box's one GPU (gloo
+    exchanging host copies).  Each rank's gathered poses / landmarks equal what the other
+    rank computed."""
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rank_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for step in range(2):
+        for r in range(2):
+            g = out[r][step]
+            for o in range(2):
+                mine = out[o][step]
+                assert np.array_equal(g["Tg"][o], mine["T"])
+                c = int(g["Cg"][o][0])
+                assert c == len(mine["xyz"]) and c > 0
+                assert np.array_equal(g["Xg"][o][:c], mine["xyz"])

@@ -137,3 +137,19 @@ def test_gpu_point_map_mono_update_matches_oracle(oracle_mod):
     want = np.concatenate(want)
     assert np.array_equal(pm.cloud64(), want)
     assert np.array_equal(pm.cloud32(), want.astype(np.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_gpu_point_map_overflow_is_reported():
+    """an append past the capacity is surfaced (check=True raises at once,
+    overflowed() / len() report it) instead of silently dropping later batches."""
+    from forest_slam_amd.mapping import PointMap
+    pm = PointMap(capacity=100, device="cuda:0")
+    P = torch.from_numpy(_cloud(80, 3)).cuda().reshape(1, 80, 3)
+    T = np.eye(4)[None]
+    pm.add_frames(P, torch.tensor([80], dtype=torch.int32, device="cuda"), T, check=True)
+    assert len(pm) == 80 and not pm.overflowed()
+    with pytest.raises(RuntimeError, match="overflow"):
+        pm.add_frames(P, torch.tensor([80], dtype=torch.int32, device="cuda"), T, check=True)
+    assert pm.overflowed()
