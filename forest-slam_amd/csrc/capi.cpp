@@ -80,8 +80,8 @@ void fvo_config_default(fvo_config* c, int32_t width, int32_t height) {
 static void release(fvo_ctx* c) {
   void* ptrs[] = {c->pyr,        c->blur,      c->score,     c->rowcnt,   c->rowoff,  c->cand,     c->hel,
                   c->ncand,      c->nsel1,     c->nsel2,     c->koff,     c->scratch, c->rt.xofs,  c->rt.xc1,
-                  c->rt.yofs,    c->rt.yc1,    c->umax,      c->bf_sidx,  c->bf_sdist, c->bf_tidx, c->sg_cost,
-                  c->sg_L,       c->sg_V,      c->sg_raw,    c->sg_d2,    c->pnp_hyp,  c->pnp_good,
+                  c->rt.yofs,    c->rt.yc1,    c->umax,      c->bf_sidx,  c->bf_sdist, c->bf_tidx, c->sg_ckpt,
+                  c->sg_V,      c->sg_raw,    c->sg_d2,    c->pnp_hyp,  c->pnp_good,
                   c->pnp_sub,    c->pnp_subsets, c->pnp_models, c->pnp_state, c->ba_ws, c->keepbits,
                   c->em_x, c->em_subsets, c->em_models, c->em_good, c->em_nmod, c->em_state};
   for (void* p : ptrs)
@@ -345,7 +345,7 @@ const char* fvo_kernel_name(int id) {
   static const char* names[KN_COUNT] = {
       "orb_copy_level0", "orb_resize", "orb_fast_score", "orb_nms_count", "orb_row_scan", "orb_nms_compact",
       "orb_select_fast", "orb_harris", "orb_select_harris", "orb_offsets", "orb_angle", "orb_blur", "orb_brief",
-      "bf_argmin", "bf_finish", "sgbm_hsum", "sgbm_vert", "sgbm_horiz", "sgbm_median", "backproject",
+      "bf_argmin", "bf_finish", "sgbm_vert", "sgbm_rows", "sgbm_median", "backproject",
       "pnp_ransac", "ba_stereo", "ba_build", "ba_solve", "gather_matches", "essential_ransac", "recover_pose", "ingest_undistort_gray", "motion_blur", "map_transform", "voxel_down_sample"};
   return (id >= 0 && id < KN_COUNT) ? names[id] : "";
 }

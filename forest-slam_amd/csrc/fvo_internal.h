@@ -39,7 +39,7 @@ struct ResizeTab {
 enum FvoKernel {
   KN_ORB_COPY, KN_ORB_RESIZE, KN_ORB_FAST, KN_ORB_NMS_COUNT, KN_ORB_ROW_SCAN, KN_ORB_COMPACT, KN_ORB_SELECT1,
   KN_ORB_HARRIS, KN_ORB_SELECT2, KN_ORB_OFFSETS, KN_ORB_ANGLE, KN_ORB_BLUR, KN_ORB_BRIEF, KN_BF_ARGMIN,
-  KN_BF_FINISH, KN_SG_HSUM, KN_SG_VERT, KN_SG_HORIZ, KN_SG_MEDIAN, KN_BACKPROJECT, KN_PNP, KN_BA_STEREO,
+  KN_BF_FINISH, KN_SG_VERT, KN_SG_ROWS, KN_SG_MEDIAN, KN_BACKPROJECT, KN_PNP, KN_BA_STEREO,
   KN_BA_BUILD, KN_BA_SOLVE, KN_GATHER, KN_ESSENTIAL, KN_RECOVER, KN_INGEST, KN_MOTION_BLUR, KN_MAP_XFORM, KN_VOXEL, KN_COUNT
 };
 
@@ -79,9 +79,8 @@ struct fvo_ctx {
   int32_t* bf_sdist = nullptr;
   int32_t* bf_tidx = nullptr;
   // SGBM workspace
-  uint16_t* sg_cost = nullptr;  // LV = left->right pass + V, [B][HG][width1][16][D] (16-row groups)
-  uint16_t* sg_L = nullptr;     // cost C, same layout
-  uint16_t* sg_V = nullptr;     // top-down pass V, same layout
+  uint16_t* sg_V = nullptr;     // top-down pass V, [B][HG][width1][16][D] (16-row bands, the one volume)
+  uint32_t* sg_ckpt = nullptr;  // [B][HG][nck][256 lanes][ckw] left->right path checkpoints
   int16_t* sg_raw = nullptr;    // [B][W][H] pre-median disparity (transposed)
   uint32_t* sg_d2 = nullptr;    // [B][W][H] right-view key (cost << 16 | 0xFFFF - x1), pseudo LR check
   hipStream_t sg_s2 = nullptr;  // second stream for chunked (pipelined) SGBM batches

@@ -258,17 +258,13 @@ def sgbm_ref(oracle_mod, frames):
     return [oracle_mod.sgbm(L, R) for L, R in frames]
 
 
-@pytest.mark.parametrize("g,cb,hg,pf,chunks", [(4, 64, 4, 1, 1), (4, 32, 4, 2, 2), (8, 32, 8, 1, 1), (8, 16, 8, 2, 3),
-                                                (8, 32, 4, 4, 2)])
-def test_sgbm_variants_bit_exact(frames, sgbm_ref, monkeypatch, g, cb, hg, pf, chunks):
-    """Every SGBM launch variant (lanes per column and columns per block of the cost pass,
-    horizontal prefetch depth, batch chunks pipelined over two streams) is bit-identical to
-    the oracle."""
+@pytest.mark.parametrize("g,cb,chunks", [(4, 64, 1), (4, 32, 2), (8, 32, 1), (8, 16, 3)])
+def test_sgbm_variants_bit_exact(frames, sgbm_ref, monkeypatch, g, cb, chunks):
+    """Every SGBM launch variant (lanes per column and columns per block of the V pass,
+    batch chunks pipelined over two streams) is bit-identical to the oracle."""
     from forest_slam_amd import _lib
     monkeypatch.setenv("FVO_SG_G", str(g))
     monkeypatch.setenv("FVO_SG_CB", str(cb))
-    monkeypatch.setenv("FVO_SG_HG", str(hg))
-    monkeypatch.setenv("FVO_SG_PF", str(pf))
     monkeypatch.setenv("FVO_SG_CHUNKS", str(chunks))
     ctx = _lib.Context(960, 600, max_batch=len(frames))
     L = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
@@ -279,3 +275,22 @@ def test_sgbm_variants_bit_exact(frames, sgbm_ref, monkeypatch, g, cb, hg, pf, c
     for i, want in enumerate(sgbm_ref):
         bad = np.argwhere(d[i] != want)
         assert len(bad) == 0, f"pair {i}: {len(bad)} px differ, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("W,H,nd", [(333, 217, 64), (200, 120, 96), (1024, 100, 128), (500, 77, 96)])
+def test_sgbm_ragged_geometries_bit_exact(oracle_mod, W, H, nd):
+    """Image widths that leave a partial 16-column chunk / 8-column segment and heights that
+    leave a partial 16-row band (the row kernel's edge cases), every supported D."""
+    from forest_slam_amd import _lib
+    rng = np.random.default_rng(W * 7 + H)
+    import forest_slam_amd.synth as synth
+    seq = synth.StereoSequence(seed=W % 13, n_frames=1, W=W, H=H, device="cpu")
+    L, R = (x.numpy() for x in seq.frame(0))
+    Ln = np.clip(L.astype(np.int32) + rng.integers(-3, 4, L.shape), 0, 255).astype(np.uint8)
+    ctx = _lib.Context(W, H, max_batch=2, num_disparities=nd, stages=_lib.STAGE_SGBM)
+    d = ctx.sgbm(torch.from_numpy(np.stack([L, Ln])).cuda(), torch.from_numpy(np.stack([R, R])).cuda())
+    torch.cuda.synchronize()
+    for i, img in enumerate((L, Ln)):
+        want = oracle_mod.sgbm(img, R, num_disp=nd)
+        bad = np.argwhere(d[i].cpu().numpy() != want)
+        assert len(bad) == 0, f"{W}x{H}/{nd} image {i}: {len(bad)} px differ, first {bad[:5]}"
