@@ -81,7 +81,7 @@ static void release(fvo_ctx* c) {
   void* ptrs[] = {c->pyr,        c->blur,      c->score,     c->rowcnt,   c->rowoff,  c->cand,     c->hel,
                   c->ncand,      c->nsel1,     c->nsel2,     c->koff,     c->scratch, c->rt.xofs,  c->rt.xc1,
                   c->rt.yofs,    c->rt.yc1,    c->umax,      c->bf_sidx,  c->bf_sdist, c->bf_tidx, c->sg_ckpt,
-                  c->sg_V,      c->sg_raw,    c->sg_d2,    c->pnp_hyp,  c->pnp_good,
+                  c->sg_V,      c->sg_C,      c->sg_raw,    c->pnp_hyp,  c->pnp_good,
                   c->pnp_sub,    c->pnp_subsets, c->pnp_models, c->pnp_state, c->ba_ws, c->keepbits,
                   c->em_x, c->em_subsets, c->em_models, c->em_good, c->em_nmod, c->em_state};
   for (void* p : ptrs)

@@ -79,10 +79,10 @@ struct fvo_ctx {
   int32_t* bf_sdist = nullptr;
   int32_t* bf_tidx = nullptr;
   // SGBM workspace
-  uint16_t* sg_V = nullptr;     // top-down pass V, [B][HG][width1][16][D] (16-row bands, the one volume)
-  uint32_t* sg_ckpt = nullptr;  // [B][HG][nck][256 lanes][ckw] left->right path checkpoints
-  int16_t* sg_raw = nullptr;    // [B][W][H] pre-median disparity (transposed)
-  uint32_t* sg_d2 = nullptr;    // [B][W][H] right-view key (cost << 16 | 0xFFFF - x1), pseudo LR check
+  uint16_t* sg_C = nullptr;     // 7x7 cost C, [B][HG][width1][16][D] (16-row bands)
+  uint16_t* sg_V = nullptr;     // top-down path V, same layout
+  uint32_t* sg_ckpt = nullptr;  // [B][4-row blocks][nck][64 lanes][ckw] left->right path checkpoints
+  int16_t* sg_raw = nullptr;    // [B][H][W] pre-median disparity
   hipStream_t sg_s2 = nullptr;  // second stream for chunked (pipelined) SGBM batches
   hipEvent_t sg_fork = nullptr, sg_join = nullptr;
   // pose workspace

@@ -2,31 +2,28 @@
 // get_disparity_map (ros_ws/src/stereo_slam.py:108-117): numDisparities 96, minDisparity 0,
 // blockSize 7, P1 392, P2 1568, 3-way aggregation, 4 fixed stripes, then medianBlur(3).
 //
-// One cost-volume-sized buffer crosses HBM per pair: V, the top-down path, u16
-// [HG][x1][16][d] (16-row bands interleaved per column, so a band's 16 rows at one column
-// are 16*D*2 contiguous bytes; x1 = x - max(maxD,0) in [0,width1), d in [0,D)).  The 7x7
-// cost C is never stored: both kernels recompute it from L2-resident image rows.
+// Two cost-volume-sized buffers cross HBM per pair, written once and read by the row pass:
+// the 7x7 cost C and the top-down path V, u16 [HG4][x1][4][d] (4-row groups interleaved per
+// column, so the 4 rows of a group at one column are 4*D*2 contiguous bytes and a wave of the
+// row pass streams contiguous memory; x1 = x - max(maxD,0) in [0,width1), d in [0,D)).
 // Kernels
 //   k_sg_costvert<D,CB,G> block of CB columns (G lanes per column, D/G disparities per lane)
 //                  marching down a stripe: BT pixel cost of both channels in one u16x2 word
 //                  from LDS-staged rows, 7x7 box sum (7-column sum from LDS, 7-row running
 //                  sum over a VGPR shift register, rows clamped to the stripe's first row and to
 //                  H-1 -- the overlap rule of OpenCV's 4 stripes), fused with the top->down
-//                  path; stores V
-//   k_sg_rows<D>   block per 16-row band (16 lanes per row, D/16 disparities per lane):
-//                  recomputes C in chunks of 16 columns (BT costs of the 22 rows the band's
-//                  7-row windows touch, staged image rows -> LDS, per-(column, d-pair) 7-row
-//                  running sums -> LDS; 7-column sliding sum in registers), runs the
-//                  left->right path storing its state every 16 columns (checkpoints), then
-//                  sweeps right->left: per 16-column segment C cached in VGPRs, the left->right
-//                  path recomputed from its checkpoint, the right->left path, S = L + R + V,
-//                  first-minimum WTA, integer sub-pixel, right-view keys (atomicMin), and the
-//                  pseudo left-right check per row
+//                  path; stores C and V
+//   k_sg_rows<D>   wave per 4 rows (16 lanes per row, D/16 disparities per lane): left->right
+//                  path over C storing its state every 8 columns (checkpoints), then segments
+//                  of 8 columns right->left: the left->right path recomputed over the segment
+//                  from its checkpoint, the right->left path, S = L + R + V, first-minimum WTA,
+//                  integer sub-pixel, right-view keys by LDS atomicMin, the pseudo left-right
+//                  check -- the L + V volume the forward pass would otherwise store and re-read
+//                  never exists
 //   k_sg_median    3x3 median (replicated border) -> int16 disparity*16
 // Path states are packed u16x2 VGPRs (v_pk_add/sub/min_u16, v_alignbit for d-1 / d+1);
 // neighbours across lanes come from DPP.  Integer arithmetic only; bit-identical to
-// oracle/sgbm_ref.cpp.  For an output row the stripe's row clamp never binds (the overlap
-// ov >= 5 > 3), so k_sg_rows uses the plain image clamp; V carries the stripe semantics.
+// oracle/sgbm_ref.cpp.
 #include <algorithm>
 #include <cstdlib>
 
@@ -43,7 +40,8 @@ __device__ __forceinline__ u16x2 splat(uint32_t s) { return as_v((s & 0xFFFFu) |
 
 struct SgParams {
   int W, H, D, minD, minX1, width1, P1, P2, ftzero, disp12, ss, ov, nstripes;
-  int HG;  // row groups of 16 (volume layout)
+  int HG;   // row groups of 16
+  int HG4;  // row groups of 4 (volume layout)
 };
 
 // SGM recurrence for one packed pair k of a lane's disparity run, in place.  `old_km1`
@@ -160,7 +158,7 @@ __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q
 // arithmetic as k_sg_hsum + k_sg_vert (order-independent sums).
 template <int D, int CB, int G>
 __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
-                                                    int64_t stride, int pitch, SgParams p,
+                                                    int64_t stride, int pitch, SgParams p, uint16_t* __restrict__ Cvol,
                                                     uint16_t* __restrict__ Vvol) {
   constexpr int DQ = D / G, PQ = DQ / 2, NV2 = DQ / 4;
   constexpr int NT = G * CB;                // threads: G lanes per column
@@ -317,7 +315,7 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
   const u16x2 P1 = splat(p.P1);
   const int x1 = c0 + col;
   const int64_t plane = (int64_t)p.width1 * D;
-  const int64_t colofs = (int64_t)b * p.HG * 16 * plane + (int64_t)x1 * 16 * D + q * DQ;
+  const int64_t colofs = (int64_t)b * p.HG4 * 4 * plane + (int64_t)x1 * 4 * D + q * DQ;
   for (int y = start; y < end; ++y) {
     if (y > start) {  // window [y-3, y+3] clamped to [start, H-1]: out clamp(y-4), in clamp(y+3)
       uint32_t nw[PQ];
@@ -339,10 +337,14 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
     }
     minPrev = hstepG<PQ, G>(st, crun, q, P1, minPrev, p.P2);
     if (y >= first_out && x1 < p.width1) {
-      const int64_t yo = (int64_t)(y >> 4) * 16 * plane + (y & 15) * D;
+      const int64_t yo = (int64_t)(y >> 2) * 4 * plane + (y & 3) * D;
+      uint2* cp = reinterpret_cast<uint2*>(Cvol + colofs + yo);
       uint2* vp = reinterpret_cast<uint2*>(Vvol + colofs + yo);
 #pragma unroll
-      for (int i = 0; i < NV2; ++i) vp[i] = make_uint2(st[2 * i], st[2 * i + 1]);
+      for (int i = 0; i < NV2; ++i) {
+        cp[i] = make_uint2(crun[2 * i], crun[2 * i + 1]);
+        vp[i] = make_uint2(st[2 * i], st[2 * i + 1]);
+      }
     }
   }
 }
@@ -388,307 +390,113 @@ __device__ __forceinline__ void vadd(uint32_t* a, const uint32_t* b) {
   for (int k = 0; k < PQ; ++k) a[k] = as_u(as_v(a[k]) + as_v(b[k]));
 }
 
-// Block per (16-row band, pair); 16 lanes per row, D/16 disparities per lane.  The band's
-// rows y0..y0+15 need BT pixel costs of the 22 rows y0-3..y0+18 (clamped).  C is produced
-// in chunks of 16 columns: per half of the 22 rows the image rows are staged to LDS, then
-// the (Sobel, intensity) channel words, then the BT (value, min, max) triples; every thread
-// runs TPT (column, d-pair) tasks down the 22 rows keeping a 7-row running sum, whose 16
-// outputs (the 7-row sums "col7" of the band's rows) land in sC7.  Each row's lanes keep
-// the last 8 col7 values in VGPRs and slide C = C + col7(x+3) - col7(x-4) along x.
-// Sweep 1 (left->right) runs the L path and stores its state (+ minimum) at the columns
-// x = W1-14-16k' -- the left neighbours of sweep 2's segments.  Sweep 2 walks the reflected
-// columns x' = W1-1-x in the same chunks: C of the segment into VGPRs, the segment's V
-// loaded, L recomputed forward from its checkpoint, then the R path, S = L + R + V and the
-// WTA per column.  The reflected C slide equals the direct one (the box sum is symmetric,
-// borders clamp the same way).
+// Wave per 4 rows (one block), 16 lanes per row, D/16 disparities per lane.  Sweep 1 walks
+// the row left->right over C (prefetched PF columns ahead) running the L path and storing
+// its state (+ minimum) every SEG columns -- at x = W1-9-SEG*s, the left neighbour of sweep
+// 2's segment s.  Sweep 2 walks segments of SEG columns right->left (double-buffered C and V
+// loads one segment ahead): L recomputed forward over the segment from its checkpoint, then
+// the R path, S = L + R + V, first-minimum WTA as one u32 min of (S << 7 | d) across the
+// row's lanes, integer sub-pixel, and the right-view key (cost << 16 | 0xFFFF - x1) lowered
+// by an LDS atomicMin -- the serial rule "replace iff disp2cost > cost" of sgbm_ref.cpp (the
+// smallest cost wins, among equal costs the largest x1, the first one the scan visits).  The
+// pseudo left-right check then runs on the LDS row and writes the row-major raw disparity.
 template <int D>
-__global__ __launch_bounds__(256, 2) void k_sg_rows(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
-                                                    int64_t stride, int pitch, SgParams p,
-                                                    const uint16_t* __restrict__ Vvol, uint32_t* __restrict__ ckpt,
-                                                    int nck, int16_t* __restrict__ rawT, uint32_t* __restrict__ keyT) {
-  constexpr int DQ = D / 16, PQ = DQ / 2;
-  constexpr int NT = 256, NR = 16, HALF = 11, CH = 16, SEG = 8;
-  constexpr int NRC = CH + D - 1;          // right pixels of a chunk row
-  constexpr int NIR = HALF + 2;            // staged image rows per half (at most)
-  constexpr int NRB = NRC + 4, NLB = CH + 4;
-  constexpr int NCR = NRC + 2, NCL = CH + 2;
-  constexpr int DP = D / 2;                // d-pairs (packed words) per column
-  constexpr int TPT = CH * DP / NT;        // (column, d-pair) tasks per thread
+__global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvol, const uint16_t* __restrict__ Vvol,
+                                                SgParams p, uint32_t* __restrict__ ckpt, int nck,
+                                                int16_t* __restrict__ raw) {
+  constexpr int DQ = D / 16, PQ = DQ / 2, SEG = 8, PF = 8;
   constexpr int CKW = PQ + 1 <= 4 ? 4 : 8;
-  static_assert((CH * DP) % NT == 0, "task split");
-  __shared__ uint8_t sImg[NIR][NRB + NLB];
-  __shared__ uint32_t sCh[HALF][NCR + NCL];
-  __shared__ uint32_t sTr[3][HALF][NRC + CH];
-  __shared__ uint32_t sC7[CH][NR][DP];
-
-  const int tid = threadIdx.x, lane = tid & 63, q = lane & 15;
-  const int r = (tid >> 6) * 4 + (lane >> 4);
-  const int band = blockIdx.x, b = blockIdx.y;
+  constexpr int XS = 2 * D;  // u32 words per column of a 4-row group
+  extern __shared__ uint32_t smem[];
+  const int lane = threadIdx.x, q = lane & 15, r = lane >> 4;
+  const int y = blockIdx.x * 4 + r, b = blockIdx.y;
   const int H = p.H, W = p.W, W1 = p.width1;
-  const int y0 = band * NR, y = y0 + r;
   const bool rowok = y < H;
-  const uint8_t* Lb = Limg + b * stride;
-  const uint8_t* Rb = Rimg + b * stride;
-  const bool aligned = ((((uintptr_t)Lb) | ((uintptr_t)Rb) | (uintptr_t)pitch) & 3) == 0;
-  const int ft = p.ftzero;
-  auto clip = [ft](int v) { return min(max(v, -ft), ft) + ft; };
-  const u16x2 P1 = splat(p.P1);
+  const int yy = min(y, H - 1);  // rows past H walk the last row's volumes (never output)
+  uint32_t* key = smem + r * W;
+  int16_t* sraw = reinterpret_cast<int16_t*>(smem + 4 * W) + r * W;
   const int INVALID = (p.minD - 1) * 16;
-  const int64_t colT = (int64_t)b * W * H + y;
-  if (rowok)
-    for (int x = q; x < W; x += 16) {
-      rawT[colT + (int64_t)x * H] = (int16_t)INVALID;
-      keyT[colT + (int64_t)x * H] = 0xFFFFFFFFu;
-    }
-
-  // ---- col7 of the 16 columns c_i = clamp(base + dir*i, 0, W1-1) -> sC7[i]
-  auto produce = [&](int base, int dir) {
-    const int ca = min(max(base, 0), W1 - 1), cb = min(max(base + dir * (CH - 1), 0), W1 - 1);
-    const int clo = min(ca, cb), nl = max(ca, cb) - clo + 1, nr = nl + D - 1;
-    const int xl0 = clo + p.minX1, xr0 = xl0 - (D - 1) - p.minD;
-    uint32_t hist[TPT][7], rs[TPT];
+  for (int x = q; x < W; x += 16) {
+    key[x] = 0xFFFFFFFFu;
+    sraw[x] = (int16_t)INVALID;
+  }
+  const int64_t rowofs = (((int64_t)b * p.HG4 + (yy >> 2)) * W1 * (4 * D) + (yy & 3) * D + q * DQ) / 2;
+  const uint32_t* Cr = reinterpret_cast<const uint32_t*>(Cvol) + rowofs;
+  const uint32_t* Vr = reinterpret_cast<const uint32_t*>(Vvol) + rowofs;
+  const u16x2 P1 = splat(p.P1);
+  const int64_t ckbase = ((int64_t)b * gridDim.x + blockIdx.x) * nck;
+  auto ld = [&](const uint32_t* base, int x, uint32_t* out) {
 #pragma unroll
-    for (int t = 0; t < TPT; ++t) rs[t] = 0;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const int ya = y0 - 3 + HALF * hh;  // first pc row of the half (unclamped)
-      const int yc0 = min(max(ya, 0), H - 1), yc1 = min(max(ya + HALF - 1, 0), H - 1);
-      const int rlo = max(yc0 - 1, 0), nir = min(yc1 + 1, H - 1) - rlo + 1;
-      // S0: image bytes; staged row i = image row rlo + i; byte j <-> x = x0 - 2 + j (clamped).
-      // Dword loads from 4-byte aligned columns (the row's 4-aligned cover of the window),
-      // all issued before the first LDS store; words that reach past an image border (or
-      // unaligned rows) take the clamped byte path.
-      {
-        const int ar = (xr0 - 2) & ~3, al = (xl0 - 2) & ~3;
-        const int nwr = ((xr0 - 2 + NRB + 3) & ~3) - ar >> 2, nwl = ((xl0 - 2 + NLB + 3) & ~3) - al >> 2;
-        const int nw = nwr + nwl;
-        constexpr int MAXW = (NRB + 3) / 4 + 1 + (NLB + 3) / 4 + 1;
-        constexpr int PERT = (NIR * MAXW + NT - 1) / NT;
-        uint32_t wv[PERT];
-#pragma unroll
-        for (int t = 0; t < PERT; ++t) {
-          const int i = tid + NT * t;
-          wv[t] = 0;
-          if (i < nir * nw) {
-            const int rr = i / nw, k = i % nw;
-            const bool right = k < nwr;
-            const int x = right ? ar + 4 * k : al + 4 * (k - nwr);
-            const uint8_t* row = (right ? Rb : Lb) + (int64_t)(rlo + rr) * pitch;
-            if (aligned && x >= 0 && x + 3 < W) {
-              wv[t] = *reinterpret_cast<const uint32_t*>(row + x);
-            } else {
-#pragma unroll
-              for (int bb = 0; bb < 4; ++bb) wv[t] |= (uint32_t)row[min(max(x + bb, 0), W - 1)] << (8 * bb);
-            }
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < PERT; ++t) {
-          const int i = tid + NT * t;
-          if (i < nir * nw) {
-            const int rr = i / nw, k = i % nw;
-            const bool right = k < nwr;
-            const int j0 = right ? ar + 4 * k - (xr0 - 2) : al + 4 * (k - nwr) - (xl0 - 2);  // byte index of the word
-            const int lim = right ? NRB : NLB, off = right ? 0 : NRB;
-#pragma unroll
-            for (int bb = 0; bb < 4; ++bb) {
-              const int j = j0 + bb;
-              if (j >= 0 && j < lim) sImg[rr][off + j] = (uint8_t)(wv[t] >> (8 * bb));
-            }
-          }
-        }
-      }
-      __syncthreads();
-      // S1: channel words of pixels x0 - 1 + k; borders (x < 1, x >= W-1) read ftzero
-      for (int i = tid; i < HALF * (NCR + NCL); i += NT) {
-        const int pl = i / (NCR + NCL), k = i % (NCR + NCL);
-        const bool right = k < NCR;
-        const int kk = right ? k : k - NCR;
-        if (kk >= (right ? nr : nl) + 2) continue;
-        const int yc = min(max(ya + pl, 0), H - 1);
-        const int x = (right ? xr0 : xl0) - 1 + kk, jj = kk + 1, off = right ? 0 : NRB;
-        uint32_t wv = (uint32_t)clip(0) * 0x10001u;
-        if (x >= 1 && x < W - 1) {
-          const uint8_t* r0 = &sImg[max(yc - 1, 0) - rlo][off];
-          const uint8_t* r1 = &sImg[yc - rlo][off];
-          const uint8_t* r2 = &sImg[min(yc + 1, H - 1) - rlo][off];
-          const int sb = (r1[jj + 1] - r1[jj - 1]) * 2 + r0[jj + 1] - r0[jj - 1] + r2[jj + 1] - r2[jj - 1];
-          wv = (uint32_t)clip(sb) | ((uint32_t)r1[jj] << 16);
-        }
-        sCh[pl][right ? kk : NCR + kk] = wv;
-      }
-      __syncthreads();
-      // S2: BT triples (u, min, max) of pixels x0 + k; at x = 0 / W-1 the half is u itself
-      for (int i = tid; i < HALF * (NRC + CH); i += NT) {
-        const int pl = i / (NRC + CH), k = i % (NRC + CH);
-        const bool right = k < NRC;
-        const int kk = right ? k : k - NRC;
-        if (kk >= (right ? nr : nl)) continue;
-        const int x = (right ? xr0 : xl0) + kk;
-        const uint32_t* ch = &sCh[pl][right ? 0 : NCR];
-        const u16x2 u = as_v(ch[kk + 1]);
-        u16x2 hl = (u + as_v(ch[kk])) >> 1, hr = (u + as_v(ch[kk + 2])) >> 1;
-        if (x == 0) hl = u;
-        if (x == W - 1) hr = u;
-        const int o = right ? kk : NRC + kk;
-        sTr[0][pl][o] = as_u(u);
-        sTr[1][pl][o] = as_u(vmin(vmin(hl, hr), u));
-        sTr[2][pl][o] = as_u(__builtin_elementwise_max(__builtin_elementwise_max(hl, hr), u));
-      }
-      __syncthreads();
-      // tasks: BT cost of both d of the pair, 7-row running sum, outputs for rows pr - 6
-#pragma unroll
-      for (int t = 0; t < TPT; ++t) {
-        const int task = tid + NT * t, ci = task / DP, dp = task % DP;
-        const int kl = min(max(base + dir * ci, 0), W1 - 1) - clo;
-        const uint32_t* tl = &sTr[0][0][NRC + kl];
-        const uint32_t* tr = &sTr[0][0][kl + (D - 2) - 2 * dp];
-        uint32_t* out = &sC7[ci][0][dp];
-#pragma unroll
-        for (int pl = 0; pl < HALF; ++pl) {
-          const int pr = HALF * hh + pl;
-          constexpr int PL = NRC + CH, PLN = HALF * (NRC + CH);
-          const u16x2 u = as_v(tl[pl * PL]), u0 = as_v(tl[PLN + pl * PL]), u1 = as_v(tl[2 * PLN + pl * PL]);
-          uint32_t w = 0;
-#pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2) {
-            const int o = pl * PL + 1 - h2;
-            const u16x2 v = as_v(tr[o]), v0 = as_v(tr[PLN + o]), v1 = as_v(tr[2 * PLN + o]);
-            const u16x2 cA =
-                __builtin_elementwise_max(__builtin_elementwise_sub_sat(u, v1), __builtin_elementwise_sub_sat(v0, u));
-            const u16x2 cB =
-                __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, u1), __builtin_elementwise_sub_sat(u0, v));
-            const uint32_t m = as_u(vmin(cA, cB));
-            w |= ((m & 0xFFFFu) + (m >> 18)) << (16 * h2);
-          }
-          rs[t] = as_u(as_v(rs[t]) + as_v(w));
-          if (pr >= 6) {
-            out[(pr - 6) * DP] = rs[t];
-            rs[t] = as_u(as_v(rs[t]) - as_v(hist[t][(pr + 1) % 7]));  // drop pc row pr - 6
-          }
-          hist[t][pr % 7] = w;
-          if (pl % 3 == 2) __builtin_amdgcn_sched_barrier(0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    __syncthreads();
-  };
-  auto col7 = [&](int j, uint32_t* e) {
-#pragma unroll
-    for (int k = 0; k < PQ; ++k) e[k] = sC7[j][r][q * PQ + k];
+    for (int k = 0; k < PQ; ++k) out[k] = base[(int64_t)x * XS + k];
   };
 
-  uint32_t hist[8][PQ], C[PQ], st[PQ];
+  // ---- sweep 1: left -> right, checkpoints.  Loads are unconditional (clamped columns) so
+  // the compiler's vmcnt waits stay precise; the checkpoint of each 8-column block is picked
+  // by a register select and stored once per block (slot nck-1 is a dummy for blocks that
+  // hold none).
+  uint32_t st[PQ], cb[PF][PQ], ck[PQ + 1];
   uint32_t minPrev = 0;
 #pragma unroll
   for (int k = 0; k < PQ; ++k) st[k] = 0;
-  const int nchunk = (W1 + 2) / CH + 1;  // chunks until 16k - 3 >= W1
-  const int64_t ckbase = ((int64_t)b * p.HG + band) * nck;
-
-  // ---- sweep 1: left -> right path, checkpoints
-  for (int k = 0; k < nchunk; ++k) {
-    produce(CH * k, 1);
-    if (k == 0) {  // columns -4..-1 clamp to column 0
-      uint32_t e[PQ];
-      col7(0, e);
 #pragma unroll
-      for (int i = 4; i < 8; ++i)
+  for (int j = 0; j < PF; ++j) ld(Cr, min(j, W1 - 1), cb[j]);
+  static_assert(PF == SEG, "one checkpoint per prefetch block");
+  const int jck = (W1 - 9) & (SEG - 1);  // position of the checkpoint column in every block
+  for (int x0 = 0; x0 < W1; x0 += PF) {
+    const bool full = x0 + PF <= W1;
 #pragma unroll
-        for (int kk = 0; kk < PQ; ++kk) hist[i][kk] = e[kk];
+    for (int j = 0; j < PF; ++j) {
+      const int x = x0 + j;
+      uint32_t c[PQ];
 #pragma unroll
-      for (int kk = 0; kk < PQ; ++kk) C[kk] = as_u(as_v(e[kk]) * (unsigned short)4);
+      for (int k = 0; k < PQ; ++k) c[k] = cb[j][k];
+      ld(Cr, min(x + PF, W1 - 1), cb[j]);
+      if (full || x < W1) minPrev = step16<PQ>(st, c, q, P1, minPrev, p.P2);
+      const bool here = j == jck;
+#pragma unroll
+      for (int k = 0; k < PQ; ++k) ck[k] = here ? st[k] : ck[k];
+      ck[PQ] = here ? minPrev : ck[PQ];
     }
+    const int rem = W1 - 9 - (x0 + jck);
+    const int slot = rem >= 0 && x0 + jck < W1 ? rem / SEG : nck - 1;
+    uint32_t* cp = ckpt + ((ckbase + slot) * 64 + lane) * CKW;
+    uint32_t v[CKW];
 #pragma unroll
-    for (int j = 0; j < CH; ++j) {
-      const int x = CH * k - 3 + j;
-      if (x >= W1) break;
-      uint32_t e[PQ];
-      col7(j, e);
-      if (x < 0) {  // chunk 0, columns 0..2 only enter the window
-        vadd<PQ>(C, e);
+    for (int kk = 0; kk < CKW; ++kk) v[kk] = kk <= PQ ? ck[kk] : 0u;
 #pragma unroll
-        for (int kk = 0; kk < PQ; ++kk) hist[j & 7][kk] = e[kk];
-        continue;
-      }
-#pragma unroll
-      for (int kk = 0; kk < PQ; ++kk) {
-        C[kk] = as_u(as_v(C[kk]) + as_v(e[kk]) - as_v(hist[(j + 1) & 7][kk]));
-        hist[j & 7][kk] = e[kk];
-      }
-      minPrev = step16<PQ>(st, C, q, P1, minPrev, p.P2);
-      const int rem = W1 - 6 - x;
-      if (rem >= 0 && (rem & (SEG - 1)) == 0) {
-        uint32_t* cp = ckpt + ((ckbase + rem / SEG) * NT + tid) * CKW;
-        uint32_t v[CKW];
-#pragma unroll
-        for (int kk = 0; kk < CKW; ++kk) v[kk] = kk < PQ ? st[kk] : minPrev;
-#pragma unroll
-        for (int kk = 0; kk < CKW; kk += 4) *reinterpret_cast<uint4*>(cp + kk) = make_uint4(v[kk], v[kk + 1], v[kk + 2], v[kk + 3]);
-      }
-    }
+    for (int kk = 0; kk < CKW; kk += 4) *reinterpret_cast<uint4*>(cp + kk) = make_uint4(v[kk], v[kk + 1], v[kk + 2], v[kk + 3]);
   }
-  // the checkpoints are re-read by this same thread (its own stores, through its CU)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // ---- sweep 2: reflected columns x' = W1-1-x
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the checkpoints, re-read below by the lanes that stored them
+
+  // ---- sweep 2: segments s of reflected columns x' = SEG*s + i (x1 = W1-1-x'), right to left
+  const int nseg = (W1 + SEG - 1) / SEG;
   uint32_t Rst[PQ];
   uint32_t minR = 0;
 #pragma unroll
   for (int k = 0; k < PQ; ++k) Rst[k] = 0;
-  const int64_t vrow = ((int64_t)b * p.HG + band) * W1;
-  const uint16_t* Vr = Vvol + (int64_t)r * D + q * DQ;
-  for (int k = 0; k < nchunk; ++k) {
-    produce(W1 - 1 - CH * k, -1);
-    if (k == 0) {
-      uint32_t e[PQ];
-      col7(0, e);
+  uint32_t Cs[2][SEG][PQ], Vs[2][SEG][PQ];
+  auto ldseg = [&](int sg, uint32_t (*cs)[PQ], uint32_t (*vs)[PQ]) {
 #pragma unroll
-      for (int i = 4; i < 8; ++i)
-#pragma unroll
-        for (int kk = 0; kk < PQ; ++kk) hist[i][kk] = e[kk];
-#pragma unroll
-      for (int kk = 0; kk < PQ; ++kk) C[kk] = as_u(as_v(e[kk]) * (unsigned short)4);
+    for (int i = 0; i < SEG; ++i) {
+      const int x1 = max(W1 - 1 - (SEG * sg + i), 0);
+      ld(Cr, x1, cs[i]);
+      ld(Vr, x1, vs[i]);
     }
-    const int jlo = k == 0 ? 3 : 0, jhi = min(CH - 1, W1 + 2 - CH * k);  // valid j: x' in [0, W1)
+  };
+  ldseg(0, Cs[0], Vs[0]);
+  for (int s0 = 0; s0 < nseg; s0 += 2) {
 #pragma unroll
-    for (int sg = 0; sg < CH / SEG; ++sg) {  // segments of SEG reflected columns, right to left
-      uint32_t Cs[SEG][PQ], Ls[SEG][PQ], Vs[SEG][PQ];
-#pragma unroll
-      for (int i = 0; i < SEG; ++i) {
-        const int j = SEG * sg + i;
-        if (j > jhi) break;
-        uint32_t e[PQ];
-        col7(j, e);
-        if (j < jlo) {
-          vadd<PQ>(C, e);
-#pragma unroll
-          for (int kk = 0; kk < PQ; ++kk) hist[j & 7][kk] = e[kk];
-          continue;
-        }
-#pragma unroll
-        for (int kk = 0; kk < PQ; ++kk) {
-          C[kk] = as_u(as_v(C[kk]) + as_v(e[kk]) - as_v(hist[(j + 1) & 7][kk]));
-          hist[j & 7][kk] = e[kk];
-          Cs[i][kk] = C[kk];
-        }
-        const int x1 = W1 - 1 - (CH * k - 3 + j);
-        const uint32_t* vp = reinterpret_cast<const uint32_t*>(Vr + (vrow + x1) * (16 * D));
-#pragma unroll
-        for (int kk = 0; kk < PQ; ++kk) Vs[i][kk] = vp[kk];
-      }
-      const int ilo = max(jlo - SEG * sg, 0), ihi = min(jhi - SEG * sg, SEG - 1);  // valid i
-      if (ihi < ilo) continue;  // uniform: the segment lies past the last column
-      // left -> right over the segment (i descending) from its checkpoint: the path state at
-      // the real column left of the segment, x' = CH*k - 3 + SEG*(sg+1)
-      uint32_t lst[PQ];
-      uint32_t lmin = 0;
-      const int xpn = CH * k - 3 + SEG * (sg + 1);
-      if (xpn >= W1) {  // the segment starts at x = 0
-#pragma unroll
-        for (int kk = 0; kk < PQ; ++kk) lst[kk] = 0;
-      } else {
-        const uint32_t* cp = ckpt + ((ckbase + (W1 - 6 - (W1 - 1 - xpn)) / SEG) * NT + tid) * CKW;
+    for (int h = 0; h < 2; ++h) {
+      const int sg = s0 + h;  // may be nseg (an empty segment: every step below is skipped)
+      ldseg(sg + 1, Cs[h ^ 1], Vs[h ^ 1]);
+      const int ihi = min(SEG - 1, W1 - 1 - SEG * sg);  // valid i: x' < W1
+      // L over the segment (i descending = real x ascending) from the checkpoint at the real
+      // column left of it, x' = SEG*(sg+1); zero state when the segment starts at x = 0
+      uint32_t lst[PQ], Ls[SEG][PQ];
+      const bool zero = SEG * (sg + 1) > W1 - 1;
+      {
+        const uint32_t* cp = ckpt + ((ckbase + (zero ? nck - 1 : sg)) * 64 + lane) * CKW;
         uint32_t v[CKW];
 #pragma unroll
         for (int kk = 0; kk < CKW; kk += 4) {
@@ -696,28 +504,27 @@ __global__ __launch_bounds__(256, 2) void k_sg_rows(const uint8_t* __restrict__ 
           v[kk] = w4.x; v[kk + 1] = w4.y; v[kk + 2] = w4.z; v[kk + 3] = w4.w;
         }
 #pragma unroll
-        for (int kk = 0; kk < PQ; ++kk) lst[kk] = v[kk];
-        lmin = v[PQ];
+        for (int kk = 0; kk < PQ; ++kk) lst[kk] = zero ? 0u : v[kk];
+        minPrev = zero ? 0u : v[PQ];
       }
+      uint32_t lmin = minPrev;
 #pragma unroll
       for (int i = SEG - 1; i >= 0; --i) {
-        if (i > ihi || i < ilo) continue;
-        lmin = step16<PQ>(lst, Cs[i], q, P1, lmin, p.P2);
+        if (i <= ihi) lmin = step16<PQ>(lst, Cs[h][i], q, P1, lmin, p.P2);
 #pragma unroll
         for (int kk = 0; kk < PQ; ++kk) Ls[i][kk] = lst[kk];
       }
-      // right -> left, S = L + R + V, first-minimum WTA, sub-pixel, right-view key
 #pragma unroll
       for (int i = 0; i < SEG; ++i) {
-        if (i > ihi || i < ilo) continue;
-        const int x1 = W1 - 1 - (CH * k - 3 + SEG * sg + i);
-        minR = step16<PQ>(Rst, Cs[i], q, P1, minR, p.P2);
+        if (i > ihi) break;
+        const int x1 = W1 - 1 - (SEG * sg + i);
+        minR = step16<PQ>(Rst, Cs[h][i], q, P1, minR, p.P2);
         // first minimum over d as one u32 min of (S << 7 | d) across the row's lanes
         uint32_t Sw[PQ];
         uint32_t kmin = 0xFFFFFFFFu;
 #pragma unroll
         for (int kk = 0; kk < PQ; ++kk) {
-          Sw[kk] = as_u(as_v(Ls[i][kk]) + as_v(Rst[kk]) + as_v(Vs[i][kk]));
+          Sw[kk] = as_u(as_v(Ls[i][kk]) + as_v(Rst[kk]) + as_v(Vs[h][i][kk]));
           const uint32_t d0 = (uint32_t)(q * DQ + 2 * kk);
           kmin = min(kmin, ((Sw[kk] & 0xFFFFu) << 7) | d0);
           kmin = min(kmin, ((Sw[kk] >> 16) << 7) | (d0 + 1));
@@ -726,11 +533,11 @@ __global__ __launch_bounds__(256, 2) void k_sg_rows(const uint8_t* __restrict__ 
         kmin = min(kmin, qperm<kQX2>(kmin));
         kmin = min(kmin, rdpp<kRHalfMirror>(kmin));
         kmin = min(kmin, rdpp<kRMirror>(kmin));
-        const int best = (int)(kmin >> 7), bd = (int)(kmin & 127u);
-        // S[bd-1] << 16 | S[bd+1] from the lanes that hold them (OR across the row)
+        const int best = (int)(kmin >> 7), d = (int)(kmin & 127u);
+        // S[d-1] << 16 | S[d+1] from the lanes that hold them (OR across the row)
         uint32_t nb = 0;
         {
-          const int im = bd - 1 - q * DQ, ip = bd + 1 - q * DQ;
+          const int im = d - 1 - q * DQ, ip = d + 1 - q * DQ;
           uint32_t wm = 0, wp = 0;
 #pragma unroll
           for (int kk = 0; kk < PQ; ++kk) {
@@ -744,12 +551,11 @@ __global__ __launch_bounds__(256, 2) void k_sg_rows(const uint8_t* __restrict__ 
         nb |= qperm<kQX2>(nb);
         nb |= rdpp<kRHalfMirror>(nb);
         nb |= rdpp<kRMirror>(nb);
-        const int sm1 = (int)(nb >> 16), sp1 = (int)(nb & 0xFFFFu);
-        if (q == 0 && rowok) {
-          const int d = bd;
+        if (q == 0) {
+          const int sm1 = (int)(nb >> 16), sp1 = (int)(nb & 0xFFFFu);
           const int x2 = x1 + p.minX1 - d - p.minD;
           if (x2 >= 0 && x2 < W && best < 0x7FFF)  // disp2cost starts at SHRT_MAX
-            atomicMin(&keyT[colT + (int64_t)x2 * H], ((uint32_t)best << 16) | (uint32_t)(0xFFFF - x1));
+            atomicMin(&key[x2], ((uint32_t)best << 16) | (uint32_t)(0xFFFF - x1));
           int dd;
           if (0 < d && d < D - 1) {
             const int denom2 = max(sm1 + sp1 - 2 * best, 1);
@@ -757,47 +563,46 @@ __global__ __launch_bounds__(256, 2) void k_sg_rows(const uint8_t* __restrict__ 
           } else {
             dd = d * 16;
           }
-          rawT[colT + (int64_t)(x1 + p.minX1) * H] = (int16_t)(dd + p.minD * 16);
+          sraw[x1 + p.minX1] = (int16_t)(dd + p.minD * 16);
         }
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // ---- pseudo left-right consistency check, the row's columns split over its 16 lanes; the
-  // keys are read from L2 (the atomics were performed there)
+  __syncthreads();  // one wave: orders the LDS atomics / raw stores before the check below
   if (!rowok) return;
+  // ---- pseudo left-right consistency check on the LDS row, then the row-major raw row
   auto disp2 = [&](int x2) -> int {
-    const uint32_t kv = __hip_atomic_load(keyT + colT + (int64_t)x2 * H, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t kv = key[x2];
     return kv == 0xFFFFFFFFu ? INVALID : (int)(0xFFFFu - (kv & 0xFFFFu)) + p.minX1 - x2;
   };
-  for (int x = p.minX1 + q; x < p.minX1 + W1; x += 16) {
-    const int64_t ix = colT + (int64_t)x * H;
-    const int d1 = rawT[ix];
-    if (d1 == INVALID) continue;
-    const int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
-    const int _x = x - _d, x_ = x - d_;
-    if (0 <= x_ && x_ < W && 0 <= _x && _x < W) {
-      const int a = disp2(x_), cc = disp2(_x);
-      if (a >= p.minD && abs(a - d_) > p.disp12 && cc >= p.minD && abs(cc - _d) > p.disp12) rawT[ix] = (int16_t)INVALID;
+  int16_t* out = raw + ((int64_t)b * H + y) * W;
+  for (int x = q; x < W; x += 16) {
+    int d1 = sraw[x];
+    if (d1 != INVALID && x >= p.minX1 && x < p.minX1 + W1) {
+      const int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
+      const int _x = x - _d, x_ = x - d_;
+      if (0 <= x_ && x_ < W && 0 <= _x && _x < W) {
+        const int a = disp2(x_), cc = disp2(_x);
+        if (a >= p.minD && abs(a - d_) > p.disp12 && cc >= p.minD && abs(cc - _d) > p.disp12) d1 = INVALID;
+      }
     }
+    out[x] = (int16_t)d1;
   }
 }
 
 // ------------------------------------------------------------------ median 3x3
-__global__ void k_sg_median(const int16_t* __restrict__ rawT, int16_t* __restrict__ out, int W, int H) {
-  int y = blockIdx.x * blockDim.x + threadIdx.x;  // rows contiguous in the transposed input
-  int x = blockIdx.y, b = blockIdx.z;
-  if (y >= H) return;
-  const int16_t* s = rawT + (int64_t)b * W * H;
+__global__ void k_sg_median(const int16_t* __restrict__ raw, int16_t* __restrict__ out, int W, int H) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, b = blockIdx.z;
+  if (x >= W) return;
+  const int16_t* s = raw + (int64_t)b * W * H;
   int v[9];
   int k = 0;
 #pragma unroll
   for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
     for (int dx = -1; dx <= 1; ++dx) {
-      int yy = min(max(y + dy, 0), H - 1), xx = min(max(x + dx, 0), W - 1);
-      v[k++] = s[(int64_t)xx * H + yy];
+      const int yy = min(max(y + dy, 0), H - 1), xx = min(max(x + dx, 0), W - 1);
+      v[k++] = s[(int64_t)yy * W + xx];
     }
   // Paeth's 19-compare median-of-9 network
 #define SG_S(a, b) { int t_ = min(v[a], v[b]); v[b] = max(v[a], v[b]); v[a] = t_; }
@@ -808,6 +613,10 @@ __global__ void k_sg_median(const int16_t* __restrict__ rawT, int16_t* __restric
   out[((int64_t)b * H + y) * W + x] = (int16_t)v[4];
 }
 
+// Experiment / tuning knobs (read per launch): FVO_SG_G lanes per column in the cost pass
+// (4 or 8), FVO_SG_CB columns per cost-pass block (G=4: 32/64; G=8: 16/32), FVO_SG_CHUNKS
+// batch chunks alternated over the caller's stream and a second stream (the cost pass of
+// one chunk overlaps the row pass of the other).  All variants are bit-identical.
 int env_int(const char* name, int def) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : def;
@@ -831,32 +640,30 @@ SgParams make_params(const fvo_config& c) {
   p.ss = (int)std::ceil(c.height / (double)p.nstripes);
   p.ov = (c.block_size / 2 + 1) + (int)std::ceil(0.1 * p.ss);
   p.HG = (c.height + 15) / 16;
+  p.HG4 = (c.height + 3) / 4;
   return p;
 }
 
-// Experiment / tuning knobs (read per launch): FVO_SG_G lanes per column in the V pass
-// (4 or 8), FVO_SG_CB columns per V-pass block (G=4: 32/64; G=8: 16/32), FVO_SG_CHUNKS batch
-// chunks alternated over the caller's stream and a second stream (the V pass of one chunk
-// overlaps the row pass of the other).  All variants are bit-identical.
-
-// Checkpoints of the left->right path per (pair, band): at x = W1-6-8k, k < nck.
-int sg_nck(const SgParams& p) { return p.width1 / 8 + 2; }
+// Checkpoints of the left->right path per (pair, 4-row block): at x = W1-9-8s, s < nck.
+int sg_nck(const SgParams& p) { return p.width1 / 8 + 2; }  // + a dummy slot
 int sg_ckw(int D) { return D / 32 + 1 <= 4 ? 4 : 8; }
+int sg_nblk(const SgParams& p) { return (p.H + 3) / 4; }
 
 template <int D>
 void launch_chunk(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_t* R, int nb, int64_t stride,
-                  int pitch, uint16_t* V, uint32_t* ck, int16_t* raw, uint32_t* key, int16_t* disp, int cb, int g,
+                  int pitch, uint16_t* C, uint16_t* V, uint32_t* ck, int16_t* raw, int16_t* disp, int cb, int g,
                   hipStream_t s) {
   const dim3 gcv((p.width1 + cb - 1) / cb, p.nstripes, nb);
   FVO_TIMED(ctx, KN_SG_VERT, s, {
-    if (g == 8 && cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 8>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, V);
-    else if (g == 8) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 16, 8>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, V);
-    else if (cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 4>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, V);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 64, 4>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, V);
+    if (g == 8 && cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 8>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, C, V);
+    else if (g == 8) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 16, 8>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, C, V);
+    else if (cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 4>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, C, V);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 64, 4>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, C, V);
   });
-  FVO_TIMED(ctx, KN_SG_ROWS, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_rows<D>), dim3(p.HG, nb), dim3(256), 0, s, L, R,
-                                                   stride, pitch, p, V, ck, sg_nck(p), raw, key));
-  FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.H + 255) / 256, p.W, nb), dim3(256), 0, s,
+  const size_t lds = (size_t)4 * p.W * (sizeof(uint32_t) + sizeof(int16_t));
+  FVO_TIMED(ctx, KN_SG_ROWS, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_rows<D>), dim3(sg_nblk(p), nb), dim3(64), lds, s,
+                                                   C, V, p, ck, sg_nck(p), raw));
+  FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.W + 255) / 256, p.H, nb), dim3(256), 0, s,
                                                      raw, disp, p.W, p.H));
 }
 
@@ -865,8 +672,8 @@ void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_
                  int pitch, int16_t* disp, hipStream_t s) {
   const int g = env_int("FVO_SG_G", 8), cb = env_int("FVO_SG_CB", g == 8 ? 32 : 64);
   const int nch = std::max(1, std::min(env_int("FVO_SG_CHUNKS", 1), batch));
-  const int64_t vol = (int64_t)p.HG * 16 * p.width1 * D, img = (int64_t)p.H * p.W;
-  const int64_t ckp = (int64_t)p.HG * sg_nck(p) * 256 * sg_ckw(D);
+  const int64_t vol = (int64_t)p.HG4 * 4 * p.width1 * D, img = (int64_t)p.H * p.W;
+  const int64_t ckp = (int64_t)sg_nblk(p) * sg_nck(p) * 64 * sg_ckw(D);
   if (nch > 1) {
     (void)hipEventRecord(ctx->sg_fork, s);
     (void)hipStreamWaitEvent(ctx->sg_s2, ctx->sg_fork, 0);
@@ -875,8 +682,8 @@ void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_
     const int b0 = (int)((int64_t)batch * k / nch), b1 = (int)((int64_t)batch * (k + 1) / nch);
     if (b1 <= b0) continue;
     hipStream_t sk = (k & 1) ? ctx->sg_s2 : s;
-    launch_chunk<D>(ctx, p, L + b0 * stride, R + b0 * stride, b1 - b0, stride, pitch, ctx->sg_V + b0 * vol,
-                    ctx->sg_ckpt + b0 * ckp, ctx->sg_raw + b0 * img, ctx->sg_d2 + b0 * img, disp + b0 * img, cb, g,
+    launch_chunk<D>(ctx, p, L + b0 * stride, R + b0 * stride, b1 - b0, stride, pitch, ctx->sg_C + b0 * vol,
+                    ctx->sg_V + b0 * vol, ctx->sg_ckpt + b0 * ckp, ctx->sg_raw + b0 * img, disp + b0 * img, cb, g,
                     sk);
   }
   if (nch > 1) {
@@ -899,12 +706,14 @@ int sgbm_init(fvo_ctx* ctx) {
   const int64_t B = c.sgbm_max_batch > 0 ? std::min(c.sgbm_max_batch, c.max_batch) : c.max_batch;
   const int64_t plane = (int64_t)p.width1 * p.D;
   int rc;
-  // sg_V: V [B][HG][width1][16][D] u16 (the one volume); sg_ckpt: path checkpoints
-  const int64_t vol = (int64_t)p.HG * 16 * plane;
-  const int64_t ckp = (int64_t)p.HG * sg_nck(p) * 256 * sg_ckw(p.D);
-  if ((rc = fvo_alloc(ctx, &ctx->sg_V, B * vol)) || (rc = fvo_alloc(ctx, &ctx->sg_ckpt, B * ckp)) ||
-      (rc = fvo_alloc(ctx, &ctx->sg_raw, B * p.H * p.W)) || (rc = fvo_alloc(ctx, &ctx->sg_d2, B * p.H * p.W)))
+  // sg_C: cost C, sg_V: top-down path V, each [B][HG4][width1][4][D] u16; sg_ckpt: the
+  // left->right path checkpoints; sg_raw: pre-median disparity [B][H][W]
+  const int64_t vol = (int64_t)p.HG4 * 4 * plane;
+  const int64_t ckp = (int64_t)sg_nblk(p) * sg_nck(p) * 64 * sg_ckw(p.D);
+  if ((rc = fvo_alloc(ctx, &ctx->sg_C, B * vol)) || (rc = fvo_alloc(ctx, &ctx->sg_V, B * vol)) ||
+      (rc = fvo_alloc(ctx, &ctx->sg_ckpt, B * ckp)) || (rc = fvo_alloc(ctx, &ctx->sg_raw, B * p.H * p.W)))
     return rc;
+  if ((size_t)4 * p.W * 6 > 160 * 1024) return fvo_fail(ctx, "SGBM: image too wide for the row kernel's LDS rows");
   FVO_HIP(ctx, hipStreamCreateWithFlags(&ctx->sg_s2, hipStreamNonBlocking));
   FVO_HIP(ctx, hipEventCreateWithFlags(&ctx->sg_fork, hipEventDisableTiming));
   FVO_HIP(ctx, hipEventCreateWithFlags(&ctx->sg_join, hipEventDisableTiming));
