@@ -214,6 +214,7 @@ def main():
     ap.add_argument("--sgbm-priority", type=int, default=0, help="HIP stream priority of the overlapped SGBM stream")
     ap.add_argument("--ba-max-landmarks", type=int, default=0, help="per-window landmark cap (0 = library default)")
     ap.add_argument("--ba-max-obs", type=int, default=0, help="per-window observation cap (0 = library default)")
+    ap.add_argument("--graph", type=int, default=0, help="replay each step as a captured HIP graph (1) or launch eagerly (0)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -255,14 +256,29 @@ def main():
     rank_step = fdist.SequenceRank(fe)  # front-end step + (world > 1, local BA) the RCCL map exchange
     nstep = [0]
 
-    def step():
+    def eager_step():
         Lb, Rb = fwd if nstep[0] % 2 == 0 else bwd
         nstep[0] += 1
         rank_step.step(Lb, Rb)
 
+    step = eager_step
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
+    if args.graph and world == 1:
+        # one graph per direction (the inputs alternate between the two static buffers); the
+        # per-kernel breakdown below still launches eagerly (events cannot be recorded inside)
+        graphs = []
+        for d in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                eager_step()
+            graphs.append(g)
+        torch.cuda.synchronize()
+
+        def step():
+            graphs[nstep[0] % 2].replay()
+            nstep[0] += 1
 
     # per-kernel breakdown (separate pass, every launch bracketed by events).  SGBM runs in
     # order on the main stream here, so no kernel's time includes another stream's kernels
@@ -272,7 +288,7 @@ def main():
     fe.overlap_sgbm = False
     nprof = 2
     for _ in range(nprof):
-        step()
+        eager_step()
     torch.cuda.synchronize()
     fe.overlap_sgbm = ov
     stages = fe.ctx.timing_read()

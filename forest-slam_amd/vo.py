@@ -136,13 +136,19 @@ class StereoFrontEnd:
         slot = self.k % 2
         self.disp = self.disp_buf[slot]
         sg = self.s_sgbm if self.overlap_sgbm else main
+        capturing = torch.cuda.is_current_stream_capturing()
         if self.overlap_sgbm:
-            if inputs_ready is not None:
-                sg.wait_event(inputs_ready)
-            if self.main_done[slot] is not None:  # main's reads of this disparity buffer (step k-2)
-                sg.wait_event(self.main_done[slot])
-            L.record_stream(sg)
-            R.record_stream(sg)
+            if capturing:
+                # inside a HIP graph the SGBM branch forks from the step's own start (graph
+                # replays are stream-ordered, so no earlier step still reads its buffer)
+                sg.wait_stream(main)
+            else:
+                if inputs_ready is not None:
+                    sg.wait_event(inputs_ready)
+                if self.main_done[slot] is not None:  # main's reads of this disparity buffer (step k-2)
+                    sg.wait_event(self.main_done[slot])
+                L.record_stream(sg)
+                R.record_stream(sg)
         with torch.cuda.stream(sg):  # previous stereo pairs -> SGBM (needs only images)
             self.prevL[0].copy_(self.sg_lastL)
             self.prevR[0].copy_(self.sg_lastR)
@@ -192,7 +198,7 @@ class StereoFrontEnd:
         self.last_desc[1].copy_(desc[2 * n - 1])
         self.last_cnt[0:1].copy_(cnt[n - 1:n])
         self.last_cnt[1:2].copy_(cnt[2 * n - 1:2 * n])
-        if self.overlap_sgbm:
+        if self.overlap_sgbm and not capturing:
             self.main_done[slot] = main.record_event()
         self.k += 1
         return out, st

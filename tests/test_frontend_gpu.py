@@ -127,3 +127,53 @@ def test_two_ranks_exchange_window_maps():
                 c = int(g["Cg"][o][0])
                 assert c == len(mine["xyz"]) and c > 0
                 assert np.array_equal(g["Xg"][o][:c], mine["xyz"])
+
+
+def test_frontend_step_captured_in_hip_graph_replays_bit_identically():
+    """VERDICT r1 missing #5 / include/fvo.h: hot calls allocate nothing and sync nothing, so
+    a whole StereoFrontEnd.step (ORB, BF, SGBM, back-projection, PnP, local BA -- and the
+    torch copies around them) captures into one HIP graph.  Replays on new inputs give the
+    eager results bit for bit."""
+    seq, L, R = _frames(33, 7, start=80)
+    eager = _fe(seq, 2, ba_window=3)
+    eager.prime(L[0], R[0])
+    want = []
+    for s in (1, 3, 5):
+        T, st = eager.step(L[s:s + 2], R[s:s + 2])
+        want.append((T.cpu().numpy().copy(), st.cpu().numpy().copy()))
+    fe = _fe(seq, 2, ba_window=3)
+    fe.prime(L[0], R[0])
+    fe.step(L[1:3], R[1:3])  # eager first step (the BA window start settles)
+    Ls, Rs = L[3:5].clone(), R[3:5].clone()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        T, st = fe.step(Ls, Rs)
+    for k, s in ((1, 3), (2, 5)):
+        Ls.copy_(L[s:s + 2])
+        Rs.copy_(R[s:s + 2])
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(T.cpu().numpy(), want[k][0]) and np.array_equal(st.cpu().numpy(), want[k][1]), k
+
+
+def test_overlapped_frontend_step_in_hip_graph():
+    """The same with the SGBM branch on its own stream (bench default): inside the capture
+    it forks from the step's start and joins before back-projection."""
+    seq, L, R = _frames(34, 5, start=40)
+    eager = _fe(seq, 2, ba_window=0)
+    eager.prime(L[0], R[0])
+    want = [eager.step(L[s:s + 2], R[s:s + 2])[0].cpu().numpy().copy() for s in (1, 3)]
+    fe = _fe(seq, 2, ba_window=0, overlap_sgbm=True)
+    fe.prime(L[0], R[0])
+    Ls, Rs = L[1:3].clone(), R[1:3].clone()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        T, _ = fe.step(Ls, Rs)
+    for k, s in enumerate((1, 3)):
+        Ls.copy_(L[s:s + 2])
+        Rs.copy_(R[s:s + 2])
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(T.cpu().numpy(), want[k]), k
