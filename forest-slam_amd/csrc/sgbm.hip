@@ -392,7 +392,7 @@ __device__ __forceinline__ void vadd(uint32_t* a, const uint32_t* b) {
 
 // Wave per 4 rows (one block), 16 lanes per row, D/16 disparities per lane.  Sweep 1 walks
 // the row left->right over C (prefetched PF columns ahead) running the L path and storing
-// its state (+ minimum) every SEG columns -- at x = W1-9-SEG*s, the left neighbour of sweep
+// its state (+ minimum) every SEG columns -- at x = W1-1-SEG*(s+1), the left neighbour of sweep
 // 2's segment s.  Sweep 2 walks segments of SEG columns right->left (double-buffered C and V
 // loads one segment ahead): L recomputed forward over the segment from its checkpoint, then
 // the R path, S = L + R + V, first-minimum WTA as one u32 min of (S << 7 | d) across the
@@ -404,7 +404,7 @@ template <int D>
 __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvol, const uint16_t* __restrict__ Vvol,
                                                 SgParams p, uint32_t* __restrict__ ckpt, int nck,
                                                 int16_t* __restrict__ raw) {
-  constexpr int DQ = D / 16, PQ = DQ / 2, SEG = 8, PF = 8;
+  constexpr int DQ = D / 16, PQ = DQ / 2, SEG = 8, PF = 16;
   constexpr int CKW = PQ + 1 <= 4 ? 4 : 8;
   constexpr int XS = 2 * D;  // u32 words per column of a 4-row group
   extern __shared__ uint32_t smem[];
@@ -434,14 +434,14 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
   // the compiler's vmcnt waits stay precise; the checkpoint of each 8-column block is picked
   // by a register select and stored once per block (slot nck-1 is a dummy for blocks that
   // hold none).
-  uint32_t st[PQ], cb[PF][PQ], ck[PQ + 1];
+  uint32_t st[PQ], cb[PF][PQ], ck[PF / SEG][PQ + 1];
   uint32_t minPrev = 0;
 #pragma unroll
   for (int k = 0; k < PQ; ++k) st[k] = 0;
 #pragma unroll
   for (int j = 0; j < PF; ++j) ld(Cr, min(j, W1 - 1), cb[j]);
-  static_assert(PF == SEG, "one checkpoint per prefetch block");
-  const int jck = (W1 - 9) & (SEG - 1);  // position of the checkpoint column in every block
+  static_assert(PF % SEG == 0, "whole checkpoints per prefetch block");
+  const int jck = (W1 - 1 - SEG) & (SEG - 1);  // checkpoint columns of a block: jck + SEG*m
   for (int x0 = 0; x0 < W1; x0 += PF) {
     const bool full = x0 + PF <= W1;
 #pragma unroll
@@ -452,21 +452,24 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
       for (int k = 0; k < PQ; ++k) c[k] = cb[j][k];
       ld(Cr, min(x + PF, W1 - 1), cb[j]);
       if (full || x < W1) minPrev = step16<PQ>(st, c, q, P1, minPrev, p.P2);
-      const bool here = j == jck;
+      const bool here = (j & (SEG - 1)) == jck;
+      uint32_t* ckm = ck[j / SEG];
 #pragma unroll
-      for (int k = 0; k < PQ; ++k) ck[k] = here ? st[k] : ck[k];
-      ck[PQ] = here ? minPrev : ck[PQ];
+      for (int k = 0; k < PQ; ++k) ckm[k] = here ? st[k] : ckm[k];
+      ckm[PQ] = here ? minPrev : ckm[PQ];
     }
-    const int rem = W1 - 9 - (x0 + jck);
-    const int slot = rem >= 0 && x0 + jck < W1 ? rem / SEG : nck - 1;
-    uint32_t* cp = ckpt + ((ckbase + slot) * 64 + lane) * CKW;
-    uint32_t v[CKW];
 #pragma unroll
-    for (int kk = 0; kk < CKW; ++kk) v[kk] = kk <= PQ ? ck[kk] : 0u;
+    for (int m = 0; m < PF / SEG; ++m) {
+      const int xc = x0 + SEG * m + jck, rem = W1 - 1 - SEG - xc;
+      const int slot = rem >= 0 && xc < W1 ? rem / SEG : nck - 1;
+      uint32_t* cp = ckpt + ((ckbase + slot) * 64 + lane) * CKW;
+      uint32_t v[CKW];
 #pragma unroll
-    for (int kk = 0; kk < CKW; kk += 4) *reinterpret_cast<uint4*>(cp + kk) = make_uint4(v[kk], v[kk + 1], v[kk + 2], v[kk + 3]);
+      for (int kk = 0; kk < CKW; ++kk) v[kk] = kk <= PQ ? ck[m][kk] : 0u;
+#pragma unroll
+      for (int kk = 0; kk < CKW; kk += 4) *reinterpret_cast<uint4*>(cp + kk) = make_uint4(v[kk], v[kk + 1], v[kk + 2], v[kk + 3]);
+    }
   }
-
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the checkpoints, re-read below by the lanes that stored them
 
   // ---- sweep 2: segments s of reflected columns x' = SEG*s + i (x1 = W1-1-x'), right to left
