@@ -191,9 +191,11 @@ def pmc_valu(shape: str):
     rows, src = _pmc_rows("valu_per_kernel.csv", shape)
     if not rows:
         return None
-    return {"source": src, "kernels": {r["kernel"]: {"valu_busy": float(r["valu_busy"]),
-                                                     "valu_insts_per_launch": float(r["avg_SQ_INSTS_VALU"])}
-                                       for r in rows}}
+    hot = ("k_sg_rows", "k_sg_costvert", "k_fast_nms", "k_bf_argmin", "k_pnp_hyp", "k_ba_lin", "k_blur", "k_brief")
+    return {"source": src, "metric": "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles)",
+            "kernels": {r["kernel"]: {"valu_util": float(r["valu_util"]),
+                                      "valu_insts_per_launch": float(r["avg_SQ_INSTS_VALU"])}
+                        for r in rows if r["kernel"].startswith(hot)}}
 
 
 def main():

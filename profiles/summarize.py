@@ -1,7 +1,8 @@
 """Summarise rocprofv3 CSV output for the libfvo kernels (kernel names from the anonymous
 namespace of forest-slam_amd/csrc/*.hip).  Writes kernel_stats.csv (rocprof's own stats,
 filtered), pmc_per_kernel.csv (avg FETCH_SIZE / WRITE_SIZE per dispatch, raw and gfx950-
-corrected) into the output directory."""
+corrected) into the output directory; every row carries the workload shape key (bench.py
+shape_key) so counters are never reported for another shape."""
 import csv
 import glob
 import os
@@ -27,17 +28,18 @@ def short(name):
     return (m.group(1) + (m.group(2) or "")) if m else name
 
 
-def main(trace, fetch, write, out):
+def main(trace, fetch, write, out, shape):
     os.makedirs(out, exist_ok=True)
     st = find(trace, "*kernel_stats.csv")
     if st:
         rows = list(csv.DictReader(open(st)))
         keep = [r for r in rows if ours(r["Name"])]
         with open(os.path.join(out, "kernel_stats.csv"), "w", newline="") as f:
-            w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
+            w = csv.DictWriter(f, fieldnames=list(rows[0].keys()) + ["shape"])
             w.writeheader()
             for r in keep:
                 r["Name"] = short(r["Name"])
+                r["shape"] = shape
                 w.writerow(r)
     pmc = defaultdict(lambda: {"FETCH_SIZE": [], "WRITE_SIZE": []})
     for d, ctr in ((fetch, "FETCH_SIZE"), (write, "WRITE_SIZE")):
@@ -49,16 +51,16 @@ def main(trace, fetch, write, out):
                 pmc[short(r["Kernel_Name"])][ctr].append(float(r["Counter_Value"]))
     with open(os.path.join(out, "pmc_per_kernel.csv"), "w", newline="") as f:
         w = csv.writer(f)
-        w.writerow(["kernel", "dispatches", "avg_FETCH_SIZE_kB", "avg_WRITE_SIZE_kB",
+        w.writerow(["kernel", "shape", "dispatches", "avg_FETCH_SIZE_kB", "avg_WRITE_SIZE_kB",
                     "hbm_bytes_per_dispatch_corrected"])
         for k, v in sorted(pmc.items()):
             fe = sum(v["FETCH_SIZE"]) / max(len(v["FETCH_SIZE"]), 1)
             wr = sum(v["WRITE_SIZE"]) / max(len(v["WRITE_SIZE"]), 1)
             # gfx950: FETCH_SIZE reports 1/2 of wide coalesced read bytes (x2); units of kB (x1024)
-            w.writerow([k, max(len(v["FETCH_SIZE"]), len(v["WRITE_SIZE"])), round(fe, 1), round(wr, 1),
+            w.writerow([k, shape, max(len(v["FETCH_SIZE"]), len(v["WRITE_SIZE"])), round(fe, 1), round(wr, 1),
                         int((2 * fe + wr) * 1024)])
     print("summaries written to", out)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])

@@ -21,7 +21,7 @@ def short(name):
     return (m.group(1) + (m.group(2) or "")) if m else name
 
 
-def main(d, out):
+def main(d, out, shape):
     cc = find(d, "*counter_collection.csv")
     kt = find(d, "*kernel_trace.csv")
     dur = {}
@@ -40,7 +40,7 @@ def main(d, out):
             per[k]["_time_s"] += dur.get(r.get("Dispatch_Id"), 0.0)
     with open(os.path.join(out, "mfma_per_kernel.csv"), "w", newline="") as f:
         w = csv.writer(f)
-        w.writerow(["kernel", "dispatches", "avg_ms", "avg_MFMA_BUSY_CYCLES", "avg_GRBM_GUI_ACTIVE",
+        w.writerow(["kernel", "shape", "dispatches", "avg_ms", "avg_MFMA_BUSY_CYCLES", "avg_GRBM_GUI_ACTIVE",
                     "mfma_util", "avg_f64_mfma_flops", "f64_mfma_tflops"])
         for k, v in sorted(per.items()):
             n = len(disp[k])
@@ -49,10 +49,10 @@ def main(d, out):
             gui = v.get("GRBM_GUI_ACTIVE", 0.0) / n
             util = busy / (gui / 8 * 1024) if gui else None
             fl = v.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0) / n * 512
-            w.writerow([k, n, round(t * 1e3, 4), round(busy), round(gui), None if util is None else round(util, 5),
+            w.writerow([k, shape, n, round(t * 1e3, 4), round(busy), round(gui), None if util is None else round(util, 5),
                         round(fl), round(fl / t / 1e12, 3) if t else None])
     print(open(os.path.join(out, "mfma_per_kernel.csv")).read())
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3])

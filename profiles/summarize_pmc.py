@@ -1,9 +1,10 @@
 """Generic per-kernel summary of one rocprofv3 --pmc pass (any counter set) joined with the
 same pass's kernel-trace durations -> CSV: kernel, shape, dispatches, avg_ms, avg_<counter>...
-plus, when the SQ counters are present, derived VALU figures:
-  valu_busy  = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
-               (SQ_ACTIVE_INST_* count quad-cycles; GRBM_GUI_ACTIVE is summed over 8 XCDs)
-  valu_issue = SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) / (1024 x GRBM_GUI_ACTIVE / 8)
+plus, when the SQ counters are present, the VALU utilisation:
+  valu_util = SQ_INSTS_VALU x 2 cycles (a wave64 VALU instruction on a SIMD-32) /
+              (1024 SIMDs x GRBM_GUI_ACTIVE / 8)   (GRBM_GUI_ACTIVE is summed over 8 XCDs)
+  i.e. the fraction of the SIMDs' cycles spent issuing vector instructions (1.0 = every
+  SIMD issues one wave64 VALU instruction every 2 cycles for the kernel's whole duration).
     usage: python profiles/summarize_pmc.py <rocprof dir> <out.csv> <shape> [kernel-prefix ...]"""
 import csv
 import glob
@@ -45,7 +46,7 @@ def main(d, out, shape, prefixes):
             disp[k].add(did)
             per[k]["_t"] += dur.get(did, 0.0)
     ctrs = sorted(ctrs)
-    cols = ["kernel", "shape", "dispatches", "avg_ms"] + [f"avg_{c}" for c in ctrs] + ["valu_busy", "valu_issue"]
+    cols = ["kernel", "shape", "dispatches", "avg_ms"] + [f"avg_{c}" for c in ctrs] + ["valu_util"]
     with open(out, "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(cols)
@@ -54,9 +55,8 @@ def main(d, out, shape, prefixes):
             avg = {c: v.get(c, 0.0) / n for c in ctrs}
             gui = avg.get("GRBM_GUI_ACTIVE", 0.0)
             cyc = gui / 8 * 1024 if gui else None
-            busy = round(avg["SQ_ACTIVE_INST_VALU"] * 4 / cyc, 4) if cyc and "SQ_ACTIVE_INST_VALU" in avg else None
-            issue = round(avg["SQ_INSTS_VALU"] * 2 / cyc, 4) if cyc and "SQ_INSTS_VALU" in avg else None
-            w.writerow([k, shape, n, round(v["_t"] / n * 1e3, 4)] + [round(avg[c], 1) for c in ctrs] + [busy, issue])
+            util = round(avg["SQ_INSTS_VALU"] * 2 / cyc, 4) if cyc and "SQ_INSTS_VALU" in avg else None
+            w.writerow([k, shape, n, round(v["_t"] / n * 1e3, 4)] + [round(avg[c], 1) for c in ctrs] + [util])
     print(open(out).read())
 
 
