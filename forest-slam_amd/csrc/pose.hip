@@ -208,6 +208,68 @@ __device__ void dsvd_ws(const double* A, double* W, double* U, double* V, double
   }
 }
 
+// Right singular vector of the smallest singular value of the symmetric 12x12 DLT matrix
+// (packed upper triangle LLp, identical on every lane) -- column 11 of dsvd_ws<12,12>'s V --
+// by the same cyclic one-sided Jacobi, parallel over rows: lane i < 12 holds row i of the
+// working matrix and of V, the three column dot products of a rotation are 16-lane sums.
+// Only the summation order of those dot products differs from the serial dsvd_ws.
+// Returns the vector on every lane.
+__device__ void dlt12_null(const double* LLp, double* out) {
+  const int lane = threadIdx.x & 63, i = lane & 15;
+  const bool act = i < 12;
+  double u[12], v[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    u[j] = 0.0;
+    v[j] = (act && j == i) ? 1.0 : 0.0;
+  }
+  // row i of the symmetric matrix from the packed upper triangle (compile-time indices only)
+#pragma unroll
+  for (int a = 0, k = 0; a < 12; ++a)
+#pragma unroll
+    for (int b = a; b < 12; ++b, ++k) {
+      if (i == a) u[b] = LLp[k];
+      if (i == b) u[a] = LLp[k];
+    }
+  auto red = [](double x) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) x += __shfl_xor(x, o, 16);
+    return x;
+  };
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0;
+#pragma unroll
+    for (int p = 0; p < 11; ++p)
+#pragma unroll
+      for (int q = p + 1; q < 12; ++q) {
+        const double a = red(u[p] * u[p]), bb = red(u[q] * u[q]), g = red(u[p] * u[q]);
+        if (g == 0.0 || fabs(g) <= 1e-300) continue;
+        const double rel = fabs(g) / sqrt(a * bb);
+        off = fmax(off, rel);
+        if (rel < 1e-15) continue;
+        const double zeta = (bb - a) / (2.0 * g);
+        const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
+        const double up = u[p], uq = u[q], vp = v[p], vq = v[q];
+        u[p] = c * up - sn * uq;
+        u[q] = sn * up + c * uq;
+        v[p] = c * vp - sn * vq;
+        v[q] = sn * vp + c * vq;
+      }
+    if (off < 1e-15) break;
+  }
+  // the smallest column norm, the last one in dsvd_ws's stable descending order
+  double wmin = 0.0, vm = 0.0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    const double w = sqrt(red(u[j] * u[j]));
+    if (j == 0 || w <= wmin) { wmin = w; vm = v[j]; }
+  }
+  const int base = lane & ~15;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) out[k] = __shfl(vm, base + k, 64);
+}
+
 // SPD 6x6 solve by Cholesky for the LM step (JtJ with the (1 + lambda) diagonal).  Returns
 // false when a pivot is not clearly positive (pivot^2 below 1e-12 of the largest diagonal
 // entry): the caller then takes OpenCV's DECOMP_SVD path (dsolve), which also handles the
@@ -824,19 +886,11 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
   }
   for (int k = 0; k < 78; ++k) LLp[k] = wsum_d(LLp[k]);
   double param[6] = {0, 0, 0, 0, 0, 0};
+  double RRt[12];
+  if (!planar) dlt12_null(LLp, RRt);  // the whole wave
   if (lane == 0) {
     double R[9];
     if (!planar) {
-      double* LL = sh.dlt[0];
-      double* LU = sh.dlt[3];
-      double* LV = sh.dlt[4];
-      double LW[12];
-      int k = 0;
-      for (int a = 0; a < 12; ++a)
-        for (int b = a; b < 12; ++b) { LL[a * 12 + b] = LLp[k]; LL[b * 12 + a] = LLp[k]; ++k; }
-      dsvd_ws<12, 12>(LL, LW, LU, LV, sh.dlt[1], sh.dlt[2]);
-      double RRt[12];
-      for (int i = 0; i < 12; ++i) RRt[i] = LV[i * 12 + 11];
       double RR[9] = {RRt[0], RRt[1], RRt[2], RRt[4], RRt[5], RRt[6], RRt[8], RRt[9], RRt[10]};
       double tt[3] = {RRt[3], RRt[7], RRt[11]};
       if (ddet3(RR) < 0) {
