@@ -216,6 +216,8 @@ def main():
     ap.add_argument("--sgbm-priority", type=int, default=0, help="HIP stream priority of the overlapped SGBM stream")
     ap.add_argument("--ba-max-landmarks", type=int, default=0, help="per-window landmark cap (0 = library default)")
     ap.add_argument("--ba-max-obs", type=int, default=0, help="per-window observation cap (0 = library default)")
+    ap.add_argument("--sgbm-cus", type=str, default="", help="CUs of the overlapped SGBM stream: 'first:N', "
+                    "'every:K' (all but every K-th CU) or '' (all)")
     ap.add_argument("--graph", type=int, default=0, help="replay each step as a captured HIP graph (1) or launch eagerly (0)")
     args = ap.parse_args()
 
@@ -245,9 +247,16 @@ def main():
     L_all, R_all = seq.frames(range(B + 1))
     torch.cuda.synchronize()
     ba_caps = {k: v for k, v in (("ba_max_landmarks", args.ba_max_landmarks), ("ba_max_obs", args.ba_max_obs)) if v}
+    sgbm_cus = None
+    if args.sgbm_cus:
+        from forest_slam_amd import _lib
+        ncu = _lib.load().fvo_device_cu_count()
+        kind, k = args.sgbm_cus.split(":")
+        k = int(k)
+        sgbm_cus = list(range(k)) if kind == "first" else [c for c in range(ncu) if c % k != k - 1]
     fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=B, nfeatures=args.nfeatures, device=dev,
                            ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm),
-                           sgbm_priority=args.sgbm_priority, **ba_caps)
+                           sgbm_priority=args.sgbm_priority, sgbm_cus=sgbm_cus, **ba_caps)
     fe.prime(L_all[0], R_all[0])
     # Steps walk the rendered frames forward (1..B) then backward (B-1..0) and so on, so every
     # frame pair the front end sees -- including the carried pair across a step boundary -- is

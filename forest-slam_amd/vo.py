@@ -35,7 +35,8 @@ STATUS_KP_OVERFLOW = -3
 class StereoFrontEnd:
     def __init__(self, width: int, height: int, K: np.ndarray, dist: np.ndarray, baseline: float, batch: int,
                  nfeatures: int = 500, match_right: bool = True, device=None, ba_window: int = 10,
-                 ba_iters: int = 10, overlap_sgbm: bool = False, sgbm_priority: int = 0, **params):
+                 ba_iters: int = 10, overlap_sgbm: bool = False, sgbm_priority: int = 0, sgbm_cus=None,
+                 **params):
         self.B = batch
         self.K = np.asarray(K, np.float64)
         self.dist = np.resize(np.asarray(dist, np.float64), 5)
@@ -98,7 +99,12 @@ class StereoFrontEnd:
         # when step() is called (resident in HBM, or pass inputs_ready).  Default: SGBM runs
         # in order on the caller's stream.
         self.overlap_sgbm = bool(overlap_sgbm)
-        self.s_sgbm = torch.cuda.Stream(dev, priority=sgbm_priority) if self.overlap_sgbm else None
+        # sgbm_cus: the compute units the overlapped SGBM stream may use (None = all); the
+        # others stay free for the latency-bound pose / BA kernels of the caller's stream
+        if self.overlap_sgbm and sgbm_cus is not None:
+            self.s_sgbm = _lib.cu_masked_stream(sgbm_cus, dev)
+        else:
+            self.s_sgbm = torch.cuda.Stream(dev, priority=sgbm_priority) if self.overlap_sgbm else None
         self.sg_lastL = e((height, width), torch.uint8)
         self.sg_lastR = e((height, width), torch.uint8)
         self.main_done = [None, None]

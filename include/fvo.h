@@ -274,6 +274,15 @@ int64_t fvo_voxel_workspace_bytes(int64_t n_points);
 int fvo_voxel_down_sample(fvo_ctx* ctx, const double* points, int64_t n_points, double voxel_size, void* workspace,
                           int64_t workspace_bytes, double* out, int32_t* n_out, int32_t* status, fvo_stream stream);
 
+/* Stream helpers for partitioning the GPU between concurrent stages: a HIP stream whose
+ * kernels run only on the CUs set in cu_mask (bit i of word i/32 = CU i, `words` words), e.g.
+ * the overlapped SGBM stream leaving CUs free for the latency-bound pose / BA kernels of the
+ * other stream.  fvo_stream_destroy releases it. */
+int fvo_stream_create_cu_mask(const uint32_t* cu_mask, int32_t words, fvo_stream* out);
+int fvo_stream_destroy(fvo_stream stream);
+/* Number of compute units of the current device. */
+int fvo_device_cu_count(void);
+
 /* Test hook: KeyPointsFilter::retainBest on `n` float responses (device memory) with the
  * product's selection kernel.  idx_out [n] receives the surviving original indices in
  * OpenCV's output order, *n_out the survivor count.  Allocates (stream-ordered). */
