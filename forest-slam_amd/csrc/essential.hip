@@ -122,81 +122,6 @@ __device__ void null_space_5x9(const double* Q, double* basis) {
   }
 }
 
-// 10x20 constraint matrix (row-major) from E = xX + yY + zZ + W (oracle coeff_matrix).
-__device__ void coeff_matrix(const double* basis, double* A) {
-  double L[9][4];
-#pragma unroll
-  for (int i = 0; i < 9; ++i)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) L[i][k] = basis[k * 9 + i];
-  for (int r = 0; r < 200; ++r) A[r] = 0.0;
-  {
-    constexpr int cof[3][5] = {{0, 4, 8, 5, 7}, {1, 3, 8, 5, 6}, {2, 3, 7, 4, 6}};
-    constexpr double sgn[3] = {1.0, -1.0, 1.0};
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      double q[10], t[10];
-      mul_ll(L[cof[c][1]], L[cof[c][2]], q);
-      mul_ll(L[cof[c][3]], L[cof[c][4]], t);
-#pragma unroll
-      for (int k = 0; k < 10; ++k) q[k] -= t[k];
-      madd_ql(q, L[cof[c][0]], sgn[c], A);
-    }
-  }
-  double EEt[9][10];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-#pragma unroll
-      for (int k = 0; k < 10; ++k) EEt[i * 3 + j][k] = 0.0;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        double q[10];
-        mul_ll(L[i * 3 + k], L[j * 3 + k], q);
-#pragma unroll
-        for (int m = 0; m < 10; ++m) EEt[i * 3 + j][m] += q[m];
-      }
-    }
-  double Mq[9][10];
-#pragma unroll
-  for (int i = 0; i < 9; ++i)
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      double tr = EEt[0][k] + EEt[4][k] + EEt[8][k];
-      Mq[i][k] = 2.0 * EEt[i][k] - ((i % 4 == 0) ? tr : 0.0);
-    }
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) madd_ql(Mq[i * 3 + k], L[k * 3 + j], 1.0, A + (1 + i * 3 + j) * 20);
-}
-
-__device__ bool reduce_10x20(double* A, double* R) {
-  for (int c = 0; c < 10; ++c) {
-    int p = c;
-    double best = fabs(A[c * 20 + c]);
-    for (int r = c + 1; r < 10; ++r)
-      if (fabs(A[r * 20 + c]) > best) { best = fabs(A[r * 20 + c]); p = r; }
-    if (!(best > 0.0)) return false;
-    if (p != c)
-      for (int k = 0; k < 20; ++k) { double t = A[c * 20 + k]; A[c * 20 + k] = A[p * 20 + k]; A[p * 20 + k] = t; }
-    double inv = 1.0 / A[c * 20 + c];
-    for (int k = c; k < 20; ++k) A[c * 20 + k] *= inv;
-    for (int r = 0; r < 10; ++r) {
-      if (r == c) continue;
-      double f = A[r * 20 + c];
-      if (f == 0.0) continue;
-      for (int k = c; k < 20; ++k) A[r * 20 + k] -= f * A[c * 20 + k];
-    }
-  }
-  for (int r = 0; r < 10; ++r)
-    for (int k = 0; k < 10; ++k) R[r * 10 + k] = A[r * 20 + 10 + k];
-  return true;
-}
-
 template <int NA, int NB>
 __device__ __forceinline__ void pmul(const double* a, const double* b, double* c) {
 #pragma unroll
@@ -259,37 +184,6 @@ __device__ __forceinline__ Cx cdiv(Cx a, Cx b) {
   return {(a.re * b.re + a.im * b.im) * t, (-a.re * b.im + a.im * b.re) * t};
 }
 
-// solvePoly (Durand-Kerner), oracle solve_poly.
-__device__ int solve_poly(const double* c, Cx* roots) {
-  int n = 10;
-  while (n > 1 && fabs(c[n]) <= DBL_EPSILON) --n;
-  Cx p{1, 0}, r{1, 1};
-  for (int i = 0; i < n; ++i) {
-    roots[i] = p;
-    p = cmul(p, r);
-  }
-  for (int iter = 0; iter < 300; ++iter) {
-    double maxDiff = 0;
-    for (int i = 0; i < n; ++i) {
-      p = roots[i];
-      Cx num{c[n], 0}, den{c[n], 0};
-      for (int j = 0; j < n; ++j) {
-        num = cmul(num, p);
-        num.re += c[n - j - 1];
-        if (j != i) {
-          Cx d{p.re - roots[j].re, p.im - roots[j].im};
-          if (d.re != 0 || d.im != 0) den = cmul(den, d);
-        }
-      }
-      num = cdiv(num, den);
-      roots[i] = {p.re - num.re, p.im - num.im};
-      maxDiff = fmax(maxDiff, sqrt(num.re * num.re + num.im * num.im));
-    }
-    if (maxDiff <= 0) break;
-  }
-  return n;
-}
-
 __device__ __forceinline__ void null3(const double* B, double* v) {
   constexpr int pr[3][2] = {{0, 1}, {0, 2}, {1, 2}};
   v[0] = 0.0; v[1] = 0.0; v[2] = 0.0;
@@ -309,75 +203,6 @@ __device__ __forceinline__ void null3(const double* B, double* v) {
   if (nrm > 0.0)
 #pragma unroll
     for (int i = 0; i < 3; ++i) v[i] /= nrm;
-}
-
-// EMEstimatorCallback::runKernel; x1/x2 interleaved (x, y) x 5.  Returns the model count.
-__device__ int five_point(const double* x1, const double* x2, double* models) {
-  double Q[45];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    double a = x1[2 * i], b = x1[2 * i + 1], c = x2[2 * i], d = x2[2 * i + 1];
-    double* q = Q + i * 9;
-    q[0] = a * c; q[1] = b * c; q[2] = c;
-    q[3] = a * d; q[4] = b * d; q[5] = d;
-    q[6] = a; q[7] = b; q[8] = 1.0;
-  }
-  double basis[36], A[200], R[100];
-  null_space_5x9(Q, basis);
-  coeff_matrix(basis, A);
-  if (!reduce_10x20(A, R)) return 0;
-  double b[39];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const double* a1 = R + (2 * i + 4) * 10;
-    const double* a2 = R + (2 * i + 5) * 10;
-    double r1[13], r2[13];
-#pragma unroll
-    for (int k = 0; k < 13; ++k) { r1[k] = 0.0; r2[k] = 0.0; }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { r1[1 + k] = a1[k]; r1[5 + k] = a1[3 + k]; }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) r1[9 + k] = a1[6 + k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { r2[k] = a2[k]; r2[4 + k] = a2[3 + k]; }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) r2[8 + k] = a2[6 + k];
-#pragma unroll
-    for (int k = 0; k < 13; ++k) b[i * 13 + k] = r1[k] - r2[k];
-  }
-  double c[11];
-  det_poly(b, c);
-  Cx roots[10];
-  int nr = solve_poly(c, roots);
-  int count = 0;
-  for (int i = 0; i < nr; ++i) {
-    if (fabs(roots[i].im) > 1e-10) continue;
-    double z1 = roots[i].re, z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
-    double bz[9];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const double* br = b + j * 13;
-      bz[j * 3 + 0] = br[0] * z3 + br[1] * z2 + br[2] * z1 + br[3];
-      bz[j * 3 + 1] = br[4] * z3 + br[5] * z2 + br[6] * z1 + br[7];
-      bz[j * 3 + 2] = br[8] * z4 + br[9] * z3 + br[10] * z2 + br[11] * z1 + br[12];
-    }
-    double v[3];
-    null3(bz, v);
-    if (fabs(v[2]) < 1e-10) continue;
-    double x = v[0] / v[2], y = v[1] / v[2];
-    double* e = models + count * 9;
-    double n2 = 0.0;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      e[k] = basis[k] * x + basis[9 + k] * y + basis[18 + k] * z1 + basis[27 + k];
-      n2 += e[k] * e[k];
-    }
-    double nrm = sqrt(n2);
-#pragma unroll
-    for (int k = 0; k < 9; ++k) e[k] /= nrm;
-    ++count;
-  }
-  return count;
 }
 
 // computeError of one point (float, as EMEstimatorCallback writes it).
@@ -619,42 +444,345 @@ __global__ void k_em_prep(const float* __restrict__ p0all, const float* __restri
   }
 }
 
-// One lane per RANSAC iteration: 5-point models + inlier count of each over all points.
-__global__ __launch_bounds__(64) void k_em_hyp(const double* __restrict__ xn, int cap, float thr2, int maxIters,
-                                               int it_lo, const int16_t* __restrict__ sub,
-                                               const EmState* __restrict__ state, double* __restrict__ models,
-                                               int32_t* __restrict__ good, int8_t* __restrict__ nmod) {
-  extern __shared__ __attribute__((aligned(16))) double sx[];  // [n][4]
+// ---- the 5-point solver in three launches over the RANSAC subsets of one iteration range
+// (each a different mapping of the same arithmetic as five_point(), operation for operation):
+//   k_em_coef   lane per subset: 5x9 epipolar rows, null-space basis (Householder), the 10x20
+//               cubic-constraint matrix, row by row -> workspace.
+//   k_em_elim   16-lane group per subset: Gauss-Jordan on the 10x20 matrix with a row per lane
+//               (pivot = first maximum found by a group butterfly, rows swapped by relabelling,
+//               pivot row broadcast by shuffles), then B(z) and det B(z) -> workspace.
+//   k_em_hyp    lane per subset: Durand-Kerner on det B(z) with the roots in registers (300
+//               iterations unless the roots stop moving -- OpenCV's rule, so almost always
+//               300), the models, then every model of the wave scored over the points in LDS
+//               with the (subset, model) pairs spread evenly over the lanes.
+// Before: one lane ran five_point() whole (1.9 KB of scratch per lane for the 10x20 matrix and
+// the root array, 1 wave per SIMD) -- 13 ms per 64 frames.
+constexpr int EM_WS = 288;  // doubles per subset: basis 36 | A 200 | b 39 | det 11 | ok
+constexpr int EMW_BASIS = 0, EMW_A = 36, EMW_B = 236, EMW_C = 275, EMW_OK = 286;
+
+__device__ __forceinline__ bool em_active(const EmState& st, int it, int maxIters) {
+  return st.n >= 5 && it < maxIters && it < st.niters;
+}
+
+// coeff_matrix, one row at a time (each row's accumulation order unchanged).
+__device__ void coeff_rows(const double* basis, double* __restrict__ A) {
+  double L[9][4];
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) L[i][k] = basis[k * 9 + i];
+  {
+    constexpr int cof[3][5] = {{0, 4, 8, 5, 7}, {1, 3, 8, 5, 6}, {2, 3, 7, 4, 6}};
+    constexpr double sgn[3] = {1.0, -1.0, 1.0};
+    double row[20];
+#pragma unroll
+    for (int k = 0; k < 20; ++k) row[k] = 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      double q[10], t[10];
+      mul_ll(L[cof[c][1]], L[cof[c][2]], q);
+      mul_ll(L[cof[c][3]], L[cof[c][4]], t);
+#pragma unroll
+      for (int k = 0; k < 10; ++k) q[k] -= t[k];
+      madd_ql(q, L[cof[c][0]], sgn[c], row);
+    }
+#pragma unroll
+    for (int k = 0; k < 20; ++k) A[k] = row[k];
+  }
+  // EEt[ij] = sum_k L[i*3+k] L[j*3+k] (k ascending from zero); only the three diagonal
+  // entries feed the trace, and row block i needs EEt[i*3+0..2]
+  auto eet = [&](int i, int j, double* e) {
+#pragma unroll
+    for (int m = 0; m < 10; ++m) e[m] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double q[10];
+      mul_ll(L[i * 3 + k], L[j * 3 + k], q);
+#pragma unroll
+      for (int m = 0; m < 10; ++m) e[m] += q[m];
+    }
+  };
+  double tr[10];
+  {
+    double e0[10], e4[10], e8[10];
+    eet(0, 0, e0);
+    eet(1, 1, e4);
+    eet(2, 2, e8);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) tr[k] = e0[k] + e4[k] + e8[k];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    double Mq[3][10];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double e[10];
+      eet(i, k, e);
+      const int ii = i * 3 + k;
+#pragma unroll
+      for (int m = 0; m < 10; ++m) Mq[k][m] = 2.0 * e[m] - ((ii % 4 == 0) ? tr[m] : 0.0);
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      double row[20];
+#pragma unroll
+      for (int k = 0; k < 20; ++k) row[k] = 0.0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) madd_ql(Mq[k], L[k * 3 + j], 1.0, row);
+#pragma unroll
+      for (int k = 0; k < 20; ++k) A[(1 + i * 3 + j) * 20 + k] = row[k];
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void k_em_coef(const double* __restrict__ xn, int cap, int maxIters, int it_lo,
+                                                const int16_t* __restrict__ sub, const EmState* __restrict__ state,
+                                                double* __restrict__ ws) {
   const int b = blockIdx.y;
   const int it = it_lo + blockIdx.x * 64 + threadIdx.x;
   const EmState st = state[b];
-  const int n = st.n;
-  if (n < 5 || it_lo + (int)blockIdx.x * 64 >= min(st.niters, maxIters)) return;
+  if (!em_active(st, it, maxIters)) return;
   const double* x = xn + (int64_t)b * cap * 4;
-  for (int i = threadIdx.x; i < 4 * n; i += 64) sx[i] = x[i];
-  __syncthreads();
-  if (it >= maxIters || it >= st.niters) return;
   const int16_t* sb = sub + ((int64_t)b * maxIters + it) * 5;
-  double s1[10], s2[10];
+  double Q[45];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    int j = sb[i];
-    s1[2 * i] = sx[4 * j];
-    s1[2 * i + 1] = sx[4 * j + 1];
-    s2[2 * i] = sx[4 * j + 2];
-    s2[2 * i + 1] = sx[4 * j + 3];
+    const int j = sb[i];
+    const double a = x[4 * j], bb = x[4 * j + 1], c = x[4 * j + 2], d = x[4 * j + 3];
+    double* q = Q + i * 9;
+    q[0] = a * c; q[1] = bb * c; q[2] = c;
+    q[3] = a * d; q[4] = bb * d; q[5] = d;
+    q[6] = a; q[7] = bb; q[8] = 1.0;
   }
-  const int64_t slot = (int64_t)b * maxIters + it;
-  double* mo = models + slot * 90;
-  int nm = five_point(s1, s2, mo);
-  nmod[slot] = (int8_t)nm;
-  for (int k = 0; k < nm; ++k) {
+  double* w = ws + ((int64_t)b * maxIters + it) * EM_WS;
+  double basis[36];
+  null_space_5x9(Q, basis);
+#pragma unroll
+  for (int k = 0; k < 36; ++k) w[EMW_BASIS + k] = basis[k];
+  coeff_rows(basis, w + EMW_A);
+}
+
+// reduce_10x20 with logical row r held by the group lane whose `pos` is r.
+__global__ __launch_bounds__(64) void k_em_elim(int maxIters, int it_lo, const EmState* __restrict__ state,
+                                                double* __restrict__ ws) {
+  __shared__ double sR[4][6][10];  // rows 4..9 of the reduced right half, per group
+  const int b = blockIdx.y, g = threadIdx.x >> 4, l = threadIdx.x & 15;
+  const int it = it_lo + blockIdx.x * 4 + g;
+  const EmState st = state[b];
+  const bool active = em_active(st, it, maxIters);  // uniform over the group
+  double* w = ws + ((int64_t)b * maxIters + (active ? it : 0)) * EM_WS;
+  const bool has = active && l < 10;
+  double row[20];
+#pragma unroll
+  for (int k = 0; k < 20; ++k) row[k] = has ? w[EMW_A + l * 20 + k] : 0.0;
+  int pos = l;
+  bool ok = active;
+#pragma unroll
+  for (int c = 0; c < 10; ++c) {
+    if (ok) {
+      // pivot: the first (lowest logical row) maximum of |A[r][c]| over r >= c; a NaN on the
+      // diagonal fails (reduce_10x20's !(best > 0)), NaNs below it never win
+      const bool elig = has && pos >= c;
+      double v = elig && !isnan(row[c]) ? fabs(row[c]) : -1.0;
+      int kp = elig ? pos : 64, kl = l;
+      int nanfail = (has && pos == c && isnan(row[c])) ? 1 : 0;
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        const double ov = __shfl_xor(v, off, 16);
+        const int op = __shfl_xor(kp, off, 16), ol = __shfl_xor(kl, off, 16);
+        nanfail |= __shfl_xor(nanfail, off, 16);
+        if (ov > v || (ov == v && op < kp)) { v = ov; kp = op; kl = ol; }
+      }
+      if (nanfail || !(v > 0.0)) {
+        ok = false;
+      } else {
+        const int p = kp, plane = kl;
+        if (pos == c) pos = p;
+        else if (pos == p) pos = c;
+        if (l == plane) {
+          const double inv = 1.0 / row[c];
+#pragma unroll
+          for (int k = c; k < 20; ++k) row[k] *= inv;
+        }
+        double pr[20];
+#pragma unroll
+        for (int k = c; k < 20; ++k) pr[k] = __shfl(row[k], plane, 16);
+        if (has && l != plane) {
+          const double f = row[c];
+          if (f != 0.0)
+#pragma unroll
+            for (int k = c; k < 20; ++k) row[k] -= f * pr[k];
+        }
+      }
+    }
+  }
+  if (ok && has && pos >= 4)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) sR[g][pos - 4][k] = row[10 + k];
+  __syncthreads();
+  if (!active || l != 0) return;
+  if (!ok) {
+    w[EMW_OK] = 0.0;
+    return;
+  }
+  double bv[39];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double* a1 = sR[g][2 * i];
+    const double* a2 = sR[g][2 * i + 1];
+    double r1[13], r2[13];
+#pragma unroll
+    for (int k = 0; k < 13; ++k) { r1[k] = 0.0; r2[k] = 0.0; }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { r1[1 + k] = a1[k]; r1[5 + k] = a1[3 + k]; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r1[9 + k] = a1[6 + k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { r2[k] = a2[k]; r2[4 + k] = a2[3 + k]; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r2[8 + k] = a2[6 + k];
+#pragma unroll
+    for (int k = 0; k < 13; ++k) bv[i * 13 + k] = r1[k] - r2[k];
+  }
+  double cz[11];
+  det_poly(bv, cz);
+#pragma unroll
+  for (int k = 0; k < 39; ++k) w[EMW_B + k] = bv[k];
+#pragma unroll
+  for (int k = 0; k < 11; ++k) w[EMW_C + k] = cz[k];
+  w[EMW_OK] = 1.0;
+}
+
+// solve_poly with every index static (roots in registers); identical arithmetic.  The stop
+// test uses max |num|^2 instead of max |num|: both are <= 0 exactly when every |num|^2 is 0.
+__device__ int solve_poly_reg(const double* c, Cx* roots) {
+  int n = 10;
+#pragma unroll
+  for (int k = 10; k >= 2; --k)
+    if (n == k && fabs(c[k]) <= DBL_EPSILON) n = k - 1;
+  double cc[11];  // cc[m] = c[n - m]
+#pragma unroll
+  for (int m = 0; m <= 10; ++m) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k <= 10; ++k) v = (n - m == k) ? c[k] : v;
+    cc[m] = v;
+  }
+  {
+    Cx p{1, 0}, r{1, 1};
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      roots[i] = p;
+      p = cmul(p, r);
+    }
+  }
+  for (int iter = 0; iter < 300; ++iter) {
+    double mx = 0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      if (i < n) {
+        const Cx p = roots[i];
+        Cx num{cc[0], 0}, den{cc[0], 0};
+#pragma unroll
+        for (int j = 0; j < 10; ++j) {
+          if (j < n) {
+            num = cmul(num, p);
+            num.re += cc[j + 1];
+            if (j != i) {
+              const Cx d{p.re - roots[j].re, p.im - roots[j].im};
+              if (d.re != 0 || d.im != 0) den = cmul(den, d);
+            }
+          }
+        }
+        num = cdiv(num, den);
+        roots[i] = {p.re - num.re, p.im - num.im};
+        mx = fmax(mx, num.re * num.re + num.im * num.im);
+      }
+    }
+    if (mx <= 0) break;
+  }
+  return n;
+}
+
+__global__ __launch_bounds__(64) void k_em_hyp(const double* __restrict__ xn, int cap, float thr2, int maxIters,
+                                               int it_lo, const EmState* __restrict__ state,
+                                               const double* __restrict__ ws, double* __restrict__ models,
+                                               int32_t* __restrict__ good, int8_t* __restrict__ nmod) {
+  extern __shared__ __attribute__((aligned(16))) double sx[];  // [n][4]
+  __shared__ int mlist[640];                                   // (lane << 4 | model) of the wave's models
+  const int b = blockIdx.y, lane = threadIdx.x;
+  const int it = it_lo + blockIdx.x * 64 + lane;
+  const EmState st = state[b];
+  const int n = st.n;
+  if (n < 5 || it_lo + (int)blockIdx.x * 64 >= min(st.niters, maxIters)) return;  // block-uniform
+  const double* x = xn + (int64_t)b * cap * 4;
+  for (int i = lane; i < 4 * n; i += 64) sx[i] = x[i];
+  const bool active = em_active(st, it, maxIters);
+  const int64_t slot = (int64_t)b * maxIters + (active ? it : 0);
+  const double* w = ws + slot * EM_WS;
+  int count = 0;
+  if (active && w[EMW_OK] != 0.0) {
+    double cz[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) cz[k] = w[EMW_C + k];
+    Cx roots[10];
+    const int nr = solve_poly_reg(cz, roots);
+    double* mo = models + slot * 90;
+    const double* bb = w + EMW_B;
+    const double* basis = w + EMW_BASIS;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      if (i < nr && !(fabs(roots[i].im) > 1e-10)) {
+        const double z1 = roots[i].re, z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
+        double bz[9];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const double* br = bb + j * 13;
+          bz[j * 3 + 0] = br[0] * z3 + br[1] * z2 + br[2] * z1 + br[3];
+          bz[j * 3 + 1] = br[4] * z3 + br[5] * z2 + br[6] * z1 + br[7];
+          bz[j * 3 + 2] = br[8] * z4 + br[9] * z3 + br[10] * z2 + br[11] * z1 + br[12];
+        }
+        double v[3];
+        null3(bz, v);
+        if (!(fabs(v[2]) < 1e-10)) {
+          const double xx = v[0] / v[2], yy = v[1] / v[2];
+          double e[9], n2 = 0.0;
+#pragma unroll
+          for (int k = 0; k < 9; ++k) {
+            e[k] = basis[k] * xx + basis[9 + k] * yy + basis[18 + k] * z1 + basis[27 + k];
+            n2 += e[k] * e[k];
+          }
+          const double nrm = sqrt(n2);
+          double* eo = mo + count * 9;
+#pragma unroll
+          for (int k = 0; k < 9; ++k) eo[k] = e[k] / nrm;
+          ++count;
+        }
+      }
+    }
+    nmod[slot] = (int8_t)count;
+  }
+  // spread the wave's (subset, model) pairs over the lanes: exclusive scan of the counts
+  int off = count;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(off, d, 64);
+    if (lane >= d) off += t;
+  }
+  const int total = __shfl(off, 63, 64);
+  off -= count;
+  for (int k = 0; k < count; ++k) mlist[off + k] = (lane << 4) | k;
+  __syncthreads();
+  for (int m = lane; m < total; m += 64) {
+    const int who = mlist[m] >> 4, k = mlist[m] & 15;
+    const int64_t s2 = (int64_t)b * maxIters + it_lo + blockIdx.x * 64 + who;
+    const double* mE = models + s2 * 90 + k * 9;
     double E[9];
 #pragma unroll
-    for (int q = 0; q < 9; ++q) E[q] = mo[k * 9 + q];
+    for (int q = 0; q < 9; ++q) E[q] = mE[q];
     int g = 0;
     for (int i = 0; i < n; ++i) g += em_error(E, sx[4 * i], sx[4 * i + 1], sx[4 * i + 2], sx[4 * i + 3]) <= thr2;
-    good[slot * 10 + k] = g;
+    good[s2 * 10 + k] = g;
   }
 }
 
@@ -790,7 +918,8 @@ int mono_init(fvo_ctx* ctx) {
   int rc;
   if ((rc = fvo_alloc(ctx, &ctx->em_x, B * ctx->kp_cap * 4)) || (rc = fvo_alloc(ctx, &ctx->em_subsets, it * 5)) ||
       (rc = fvo_alloc(ctx, &ctx->em_models, it * 90)) || (rc = fvo_alloc(ctx, &ctx->em_good, it * 10)) ||
-      (rc = fvo_alloc(ctx, &ctx->em_nmod, it)) || (rc = fvo_alloc(ctx, (EmState**)&ctx->em_state, B)))
+      (rc = fvo_alloc(ctx, &ctx->em_nmod, it)) || (rc = fvo_alloc(ctx, (EmState**)&ctx->em_state, B)) ||
+      (rc = fvo_alloc(ctx, &ctx->em_ws, it * EM_WS)))
     return rc;
   return 0;
 }
@@ -813,23 +942,25 @@ int essential_run(fvo_ctx* ctx, const float* p0, const float* p1, const int32_t*
   const float thr2 = (float)(thr * thr);
   EmState* st = (EmState*)ctx->em_state;
   const size_t shm = (size_t)cap * 4 * sizeof(double);
-  if (shm > 160 * 1024) return fvo_fail(ctx, "essential: point capacity exceeds LDS (cap <= 5120)");
+  if (shm + 640 * sizeof(int) > 160 * 1024) return fvo_fail(ctx, "essential: point capacity exceeds LDS (cap <= 5040)");
   if (shm > 64 * 1024)
     FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_em_hyp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   const int first = std::min(maxIters, 128);
+  auto solve = [&](int lo, int hi) {
+    const int nit = hi - lo;
+    hipLaunchKernelGGL(k_em_coef, dim3((nit + 63) / 64, batch), dim3(64), 0, s, ctx->em_x, cap, maxIters, lo,
+                       ctx->em_subsets, st, ctx->em_ws);
+    hipLaunchKernelGGL(k_em_elim, dim3((nit + 3) / 4, batch), dim3(64), 0, s, maxIters, lo, st, ctx->em_ws);
+    hipLaunchKernelGGL(k_em_hyp, dim3((nit + 63) / 64, batch), dim3(64), shm, s, ctx->em_x, cap, thr2, maxIters, lo,
+                       st, ctx->em_ws, ctx->em_models, ctx->em_good, ctx->em_nmod);
+    hipLaunchKernelGGL(k_em_replay, dim3((batch + 63) / 64), dim3(64), 0, s, batch, maxIters, lo, hi, prob,
+                       ctx->em_good, ctx->em_nmod, st);
+  };
   FVO_TIMED(ctx, KN_ESSENTIAL, s, {
     hipLaunchKernelGGL(k_em_prep, dim3(batch), dim3(256), 0, s, p0, p1, npts, cap, K, maxIters, ctx->em_x,
                        ctx->em_subsets, st);
-    hipLaunchKernelGGL(k_em_hyp, dim3((first + 63) / 64, batch), dim3(64), shm, s, ctx->em_x, cap, thr2, maxIters, 0,
-                       ctx->em_subsets, st, ctx->em_models, ctx->em_good, ctx->em_nmod);
-    hipLaunchKernelGGL(k_em_replay, dim3((batch + 63) / 64), dim3(64), 0, s, batch, maxIters, 0, first, prob,
-                       ctx->em_good, ctx->em_nmod, st);
-    if (maxIters > first) {
-      hipLaunchKernelGGL(k_em_hyp, dim3((maxIters - first + 63) / 64, batch), dim3(64), shm, s, ctx->em_x, cap, thr2,
-                         maxIters, first, ctx->em_subsets, st, ctx->em_models, ctx->em_good, ctx->em_nmod);
-      hipLaunchKernelGGL(k_em_replay, dim3((batch + 63) / 64), dim3(64), 0, s, batch, maxIters, first, maxIters, prob,
-                         ctx->em_good, ctx->em_nmod, st);
-    }
+    solve(0, first);
+    if (maxIters > first) solve(first, maxIters);
     hipLaunchKernelGGL(k_em_final, dim3(batch), dim3(64), 0, s, ctx->em_x, cap, thr2, maxIters, st, ctx->em_models,
                        ctx->em_nmod, E, mask, status);
   });

@@ -104,6 +104,7 @@ struct fvo_ctx {
   double* em_models = nullptr;    // [B][max_iters][10][9] 5-point solutions
   int32_t* em_good = nullptr;     // [B][max_iters][10] inlier counts
   int8_t* em_nmod = nullptr;      // [B][max_iters] solutions per subset
+  double* em_ws = nullptr;        // [B][max_iters][EM_WS] per-subset solver stages (basis, 10x20, B(z), det)
   void* em_state = nullptr;       // [B] EmState
   int32_t em_max_iters = 0;
 };
