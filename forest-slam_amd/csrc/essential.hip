@@ -412,11 +412,12 @@ __global__ void k_gather_matches(const float* __restrict__ kp0, const float* __r
   if (threadIdx.x == 0) npts[b] = n;
 }
 
-// Normalised points (x1, y1, x2, y2) fp64 per point, subsets and RANSAC state per frame.
+// Normalised points (x1, y1, x2, y2) fp64 per point and the RANSAC state per frame (the
+// subsets come from the context's RNG(-1) table, drawn once: ransac_table_init).
 // recoverPose normalises exactly as findEssentialMat does (five-point.cpp), so it reuses this.
 __global__ void k_em_prep(const float* __restrict__ p0all, const float* __restrict__ p1all,
                           const int32_t* __restrict__ npts, int cap, Pinhole K, int maxIters,
-                          double* __restrict__ xn, int16_t* __restrict__ sub, EmState* __restrict__ state) {
+                          double* __restrict__ xn, EmState* __restrict__ state) {
   const int b = blockIdx.x;
   int n = npts[b];
   n = n < 0 ? 0 : (n > cap ? cap : n);
@@ -436,12 +437,6 @@ __global__ void k_em_prep(const float* __restrict__ p0all, const float* __restri
   st.best = -1;
   st.n = n;
   state[b] = st;
-  int16_t* o = sub + (int64_t)b * maxIters * 5;
-  if (n == 5) {
-    for (int i = 0; i < 5; ++i) o[i] = (int16_t)i;  // count == modelPoints: runKernel on all points
-  } else if (n > 5) {
-    fvo_rs::draw_subsets(n, maxIters, o);
-  }
 }
 
 // ---- the 5-point solver in three launches over the RANSAC subsets of one iteration range
@@ -536,18 +531,19 @@ __device__ void coeff_rows(const double* basis, double* __restrict__ A) {
 }
 
 __global__ __launch_bounds__(64) void k_em_coef(const double* __restrict__ xn, int cap, int maxIters, int it_lo,
-                                                const int16_t* __restrict__ sub, const EmState* __restrict__ state,
-                                                double* __restrict__ ws) {
+                                                const int16_t* __restrict__ table, int table_iters,
+                                                const EmState* __restrict__ state, double* __restrict__ ws) {
   const int b = blockIdx.y;
   const int it = it_lo + blockIdx.x * 64 + threadIdx.x;
   const EmState st = state[b];
   if (!em_active(st, it, maxIters)) return;
   const double* x = xn + (int64_t)b * cap * 4;
-  const int16_t* sb = sub + ((int64_t)b * maxIters + it) * 5;
+  // count == modelPoints (5): runKernel on all points; else the subset of row n of the table
+  const int16_t* sb = table + ((int64_t)st.n * table_iters + it) * 5;
   double Q[45];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    const int j = sb[i];
+    const int j = st.n == 5 ? i : sb[i];
     const double a = x[4 * j], bb = x[4 * j + 1], c = x[4 * j + 2], d = x[4 * j + 3];
     double* q = Q + i * 9;
     q[0] = a * c; q[1] = bb * c; q[2] = c;
@@ -760,8 +756,8 @@ __global__ __launch_bounds__(64) void k_em_hyp(const double* __restrict__ xn, in
         }
       }
     }
-    nmod[slot] = (int8_t)count;
   }
+  if (active) nmod[slot] = (int8_t)count;
   // spread the wave's (subset, model) pairs over the lanes: exclusive scan of the counts
   int off = count;
 #pragma unroll
@@ -786,26 +782,44 @@ __global__ __launch_bounds__(64) void k_em_hyp(const double* __restrict__ xn, in
   }
 }
 
-__global__ void k_em_replay(int batch, int maxIters, int it_lo, int it_hi, double conf,
-                            const int32_t* __restrict__ good, const int8_t* __restrict__ nmod,
-                            EmState* __restrict__ state) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= batch) return;
+// RANSACPointSetRegistrator::run's acceptance rule over (iteration, model) in order: one
+// wave per frame loads 64 iterations' counts at a time, then walks them in order with
+// wave-uniform reads (the loop bound niters shrinks as models are accepted).
+__global__ __launch_bounds__(64) void k_em_replay(int maxIters, int it_lo, int it_hi, double conf,
+                                                  const int32_t* __restrict__ good, const int8_t* __restrict__ nmod,
+                                                  EmState* __restrict__ state) {
+  const int b = blockIdx.x, lane = threadIdx.x;
   EmState st = state[b];
   if (st.n < 6) return;
-  for (int it = it_lo; it < it_hi && it < st.niters; ++it) {
-    const int64_t slot = (int64_t)b * maxIters + it;
-    const int nm = nmod[slot];
-    for (int k = 0; k < nm; ++k) {
-      int g = good[slot * 10 + k];
-      if (g > max(st.maxGood, 4)) {
-        st.best = it * 10 + k;
-        st.maxGood = g;
-        st.niters = fvo_rs::update_num_iters(conf, (double)(st.n - g) / st.n, 5, st.niters);
+  for (int base = it_lo; base < it_hi && base < st.niters; base += 64) {
+    const int it = base + lane;
+    int nm = 0, g[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) g[k] = 0;
+    if (it < it_hi && it < st.niters) {
+      const int64_t slot = (int64_t)b * maxIters + it;
+      nm = nmod[slot];
+#pragma unroll
+      for (int k = 0; k < 10; ++k)
+        if (k < nm) g[k] = good[slot * 10 + k];
+    }
+    for (int j = 0; j < 64; ++j) {
+      if (base + j >= it_hi || base + j >= st.niters) break;
+      const int nmj = __builtin_amdgcn_readlane(nm, j);
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        if (k < nmj) {
+          const int gj = __builtin_amdgcn_readlane(g[k], j);
+          if (gj > max(st.maxGood, 4)) {
+            st.best = (base + j) * 10 + k;
+            st.maxGood = gj;
+            st.niters = fvo_rs::update_num_iters(conf, (double)(st.n - gj) / st.n, 5, st.niters);
+          }
+        }
       }
     }
   }
-  state[b] = st;
+  if (lane == 0) state[b] = st;
 }
 
 // E + inlier mask of the accepted model; status 1 ok, 0 no model, -1 n < 5,
@@ -916,7 +930,7 @@ int mono_init(fvo_ctx* ctx) {
   ctx->em_max_iters = 1000;
   const int64_t B = ctx->cfg.max_batch, it = B * ctx->em_max_iters;
   int rc;
-  if ((rc = fvo_alloc(ctx, &ctx->em_x, B * ctx->kp_cap * 4)) || (rc = fvo_alloc(ctx, &ctx->em_subsets, it * 5)) ||
+  if ((rc = fvo_alloc(ctx, &ctx->em_x, B * ctx->kp_cap * 4)) || (rc = ransac_table_init(ctx)) ||
       (rc = fvo_alloc(ctx, &ctx->em_models, it * 90)) || (rc = fvo_alloc(ctx, &ctx->em_good, it * 10)) ||
       (rc = fvo_alloc(ctx, &ctx->em_nmod, it)) || (rc = fvo_alloc(ctx, (EmState**)&ctx->em_state, B)) ||
       (rc = fvo_alloc(ctx, &ctx->em_ws, it * EM_WS)))
@@ -936,7 +950,8 @@ int essential_run(fvo_ctx* ctx, const float* p0, const float* p1, const int32_t*
                   double focal, double cx, double cy, double prob, double threshold, int maxIters, double* E,
                   uint8_t* mask, int32_t* status, hipStream_t s) {
   if (cap > ctx->kp_cap) return fvo_fail(ctx, "essential: cap exceeds the context keypoint capacity");
-  if (maxIters < 1 || maxIters > ctx->em_max_iters) return fvo_fail(ctx, "essential: max_iters out of range");
+  if (maxIters < 1 || maxIters > ctx->em_max_iters || maxIters > ctx->rs_table_iters)
+    return fvo_fail(ctx, "essential: max_iters out of range");
   Pinhole K{focal, cx, cy};
   const double thr = threshold / ((focal + focal) / 2);
   const float thr2 = (float)(thr * thr);
@@ -945,20 +960,21 @@ int essential_run(fvo_ctx* ctx, const float* p0, const float* p1, const int32_t*
   if (shm + 640 * sizeof(int) > 160 * 1024) return fvo_fail(ctx, "essential: point capacity exceeds LDS (cap <= 5040)");
   if (shm > 64 * 1024)
     FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_em_hyp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  // the first chunk's width hardly matters (measured 64..384 subsets: 3.94..4.08 ms per 64
+  // frames): a wave's Durand-Kerner chain (300 iterations) sets the time of each launch
   const int first = std::min(maxIters, 128);
   auto solve = [&](int lo, int hi) {
     const int nit = hi - lo;
     hipLaunchKernelGGL(k_em_coef, dim3((nit + 63) / 64, batch), dim3(64), 0, s, ctx->em_x, cap, maxIters, lo,
-                       ctx->em_subsets, st, ctx->em_ws);
+                       ctx->rs_table, ctx->rs_table_iters, st, ctx->em_ws);
     hipLaunchKernelGGL(k_em_elim, dim3((nit + 3) / 4, batch), dim3(64), 0, s, maxIters, lo, st, ctx->em_ws);
     hipLaunchKernelGGL(k_em_hyp, dim3((nit + 63) / 64, batch), dim3(64), shm, s, ctx->em_x, cap, thr2, maxIters, lo,
                        st, ctx->em_ws, ctx->em_models, ctx->em_good, ctx->em_nmod);
-    hipLaunchKernelGGL(k_em_replay, dim3((batch + 63) / 64), dim3(64), 0, s, batch, maxIters, lo, hi, prob,
-                       ctx->em_good, ctx->em_nmod, st);
+    hipLaunchKernelGGL(k_em_replay, dim3(batch), dim3(64), 0, s, maxIters, lo, hi, prob, ctx->em_good, ctx->em_nmod,
+                       st);
   };
   FVO_TIMED(ctx, KN_ESSENTIAL, s, {
-    hipLaunchKernelGGL(k_em_prep, dim3(batch), dim3(256), 0, s, p0, p1, npts, cap, K, maxIters, ctx->em_x,
-                       ctx->em_subsets, st);
+    hipLaunchKernelGGL(k_em_prep, dim3(batch), dim3(256), 0, s, p0, p1, npts, cap, K, maxIters, ctx->em_x, st);
     solve(0, first);
     if (maxIters > first) solve(first, maxIters);
     hipLaunchKernelGGL(k_em_final, dim3(batch), dim3(64), 0, s, ctx->em_x, cap, thr2, maxIters, st, ctx->em_models,
@@ -976,7 +992,7 @@ int recover_run(fvo_ctx* ctx, const double* E, const int32_t* est, const float* 
   // normalised points (the recoverPose normalisation equals findEssentialMat's)
   FVO_TIMED(ctx, KN_RECOVER, s, {
     hipLaunchKernelGGL(k_em_prep, dim3(batch), dim3(256), 0, s, p0, p1, npts, cap, K, 0, ctx->em_x,
-                       ctx->em_subsets, (EmState*)ctx->em_state);
+                       (EmState*)ctx->em_state);
     hipLaunchKernelGGL(k_em_recover, dim3(batch), dim3(256), 0, s, E, est, ctx->em_x, npts, cap, dist, R, t, T,
                        ngood);
   });

@@ -88,7 +88,8 @@ struct fvo_ctx {
   // pose workspace
   double* pnp_hyp = nullptr;      // [B][cap][2] normalised inlier points (refinement)
   int32_t* pnp_sub = nullptr;     // [B][cap] inlier indices
-  int16_t* pnp_subsets = nullptr; // [cap+1][max_iters][5] RANSAC subsets per point count
+  int16_t* rs_table = nullptr;    // [cap+1][rs_table_iters][5] RNG(-1) RANSAC subsets per point count
+  int32_t rs_table_iters = 0;     //   (shared by PnP and the essential-matrix RANSAC)
   double* pnp_models = nullptr;   // [B][max_iters][6] hypotheses (rvec, tvec)
   int32_t* pnp_good = nullptr;    // [B][max_iters] inlier counts
   void* pnp_state = nullptr;      // [B] PnpState
@@ -100,7 +101,6 @@ struct fvo_ctx {
   int64_t ba_win_bytes = 0;
   // mono (essential matrix) workspace
   double* em_x = nullptr;         // [B][cap][4] normalised (x1, y1, x2, y2)
-  int16_t* em_subsets = nullptr;  // [B][max_iters][5]
   double* em_models = nullptr;    // [B][max_iters][10][9] 5-point solutions
   int32_t* em_good = nullptr;     // [B][max_iters][10] inlier counts
   int8_t* em_nmod = nullptr;      // [B][max_iters] solutions per subset
@@ -147,6 +147,7 @@ int sgbm_init(fvo_ctx* ctx);
 int sgbm_run(fvo_ctx* ctx, const uint8_t* L, const uint8_t* R, int batch, int64_t image_stride, int pitch,
              int16_t* disp, hipStream_t s);
 int pose_init(fvo_ctx* ctx);
+int ransac_table_init(fvo_ctx* ctx);
 int backproject_run(fvo_ctx* ctx, const int16_t* disp, const float* kp0, const float* kp1, const int32_t* matches,
                     const int32_t* nmatch, int batch, int cap, const double* K, double baseline, float* P3, float* p2,
                     int32_t* npts, hipStream_t s);

@@ -1193,12 +1193,21 @@ int pose_init(fvo_ctx* ctx) {
   const int64_t B = ctx->cfg.max_batch, n = B * ctx->kp_cap, it = B * ctx->pnp_max_iters;
   int rc;
   if ((rc = fvo_alloc(ctx, &ctx->pnp_sub, n)) || (rc = fvo_alloc(ctx, &ctx->pnp_hyp, 2 * n)) ||
-      (rc = fvo_alloc(ctx, &ctx->pnp_subsets, (int64_t)(ctx->kp_cap + 1) * ctx->pnp_max_iters * 5)) ||
-      (rc = fvo_alloc(ctx, &ctx->pnp_models, it * 6)) ||
+      (rc = ransac_table_init(ctx)) || (rc = fvo_alloc(ctx, &ctx->pnp_models, it * 6)) ||
       (rc = fvo_alloc(ctx, &ctx->pnp_good, it)) || (rc = fvo_alloc(ctx, (PnpState**)&ctx->pnp_state, B)))
     return rc;
-  hipLaunchKernelGGL(k_pnp_table, dim3((ctx->kp_cap + 1 + 63) / 64), dim3(64), 0, 0, ctx->kp_cap, ctx->pnp_max_iters,
-                     ctx->pnp_subsets);
+  return 0;
+}
+
+// The RNG(-1) subset table shared by PnP and the essential-matrix RANSAC (both draw 5-point
+// subsets with getSubset() from a fresh RNG(-1) per call): built once per context.
+int ransac_table_init(fvo_ctx* ctx) {
+  if (ctx->rs_table) return 0;
+  ctx->rs_table_iters = 1000;
+  int rc;
+  if ((rc = fvo_alloc(ctx, &ctx->rs_table, (int64_t)(ctx->kp_cap + 1) * ctx->rs_table_iters * 5))) return rc;
+  hipLaunchKernelGGL(k_pnp_table, dim3((ctx->kp_cap + 1 + 63) / 64), dim3(64), 0, 0, ctx->kp_cap,
+                     ctx->rs_table_iters, ctx->rs_table);
   FVO_LAUNCH_CHECK(ctx);
   FVO_HIP(ctx, hipDeviceSynchronize());
   return 0;
@@ -1230,12 +1239,12 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
   FVO_TIMED(ctx, KN_PNP, s, {
     hipLaunchKernelGGL(k_pnp_subsets, dim3((batch + 63) / 64), dim3(64), 0, s, npts, batch, cap, maxIters, st);
     hipLaunchKernelGGL(k_pnp_hyp, dim3((first + 63) / 64, batch), dim3(64), shm, s, P3, p2, cap, c, thr2, maxIters, 0,
-                       ctx->pnp_subsets, ctx->pnp_max_iters, st, ctx->pnp_models, ctx->pnp_good);
+                       ctx->rs_table, ctx->rs_table_iters, st, ctx->pnp_models, ctx->pnp_good);
     hipLaunchKernelGGL(k_pnp_replay, dim3((batch + 63) / 64), dim3(64), 0, s, batch, maxIters, 0, first, conf,
                        ctx->pnp_good, st);
     if (maxIters > first) {
       hipLaunchKernelGGL(k_pnp_hyp, dim3((maxIters - first + 63) / 64, batch), dim3(64), shm, s, P3, p2, cap, c, thr2,
-                         maxIters, first, ctx->pnp_subsets, ctx->pnp_max_iters, st, ctx->pnp_models,
+                         maxIters, first, ctx->rs_table, ctx->rs_table_iters, st, ctx->pnp_models,
                          ctx->pnp_good);
       hipLaunchKernelGGL(k_pnp_replay, dim3((batch + 63) / 64), dim3(64), 0, s, batch, maxIters, first, maxIters, conf,
                          ctx->pnp_good, st);
