@@ -130,7 +130,7 @@ def cpu_reference_ate(L_all, R_all, K, stamps, gt, nfeatures: int) -> dict:
 
 # stage name (fvo_kernel_name) -> kernel symbol prefix in rocprofv3 summaries
 KERNEL_SYMBOL = {"sgbm_rows": "k_sg_rows", "sgbm_vert": "k_sg_costvert",
-                 "sgbm_median": "k_sg_median", "orb_fast_score": "k_fast_nms", "orb_blur": "k_blur",
+                 "sgbm_median": "k_sg_median", "orb_fast_score": "k_fast_nms", "orb_brief": "k_brief",
                  "pnp_ransac": "k_pnp_hyp", "bf_argmin": "k_bf_argmin"}
 
 

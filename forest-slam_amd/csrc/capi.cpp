@@ -82,7 +82,7 @@ static void release(fvo_ctx* c) {
                   c->ncand,      c->nsel1,     c->nsel2,     c->koff,     c->scratch, c->rt.xofs,  c->rt.xc1,
                   c->rt.yofs,    c->rt.yc1,    c->umax,      c->bf_sidx,  c->bf_sdist, c->bf_tidx, c->sg_ckpt,
                   c->sg_V,      c->sg_C,      c->sg_raw,    c->pnp_hyp,  c->pnp_good,
-                  c->pnp_sub,    c->rs_table, c->pnp_models, c->pnp_state, c->ba_ws, c->keepbits,
+                  c->pnp_sub,    c->rs_table, c->pnp_models, c->pnp_ws, c->pnp_state, c->ba_ws, c->keepbits,
                   c->em_x, c->em_models, c->em_good, c->em_nmod, c->em_state, c->em_ws};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -398,7 +398,9 @@ int fvo_debug_buffer(fvo_ctx* c, int which, void** ptr, int64_t* bytes) {
   const int64_t B = c->cfg.max_batch;
   switch (which) {
     case 0: *ptr = c->pyr; *bytes = B * c->g.total_px; return 0;
-    case 1: *ptr = c->blur; *bytes = B * c->g.total_px; return 0;
+    case 1:  // computed on request from the last call's pyramid (not part of the hot path)
+      if (orb_blur_debug(c)) return -1;
+      *ptr = c->blur; *bytes = B * c->g.total_px; return 0;
     case 2: *ptr = c->score; *bytes = B * c->g.total_px; return 0;
     case 3: *ptr = c->ncand; *bytes = B * c->g.nlevels * 4; return 0;
     case 4: *ptr = c->nsel1; *bytes = B * c->g.nlevels * 4; return 0;

@@ -60,7 +60,8 @@ struct fvo_ctx {
   int64_t ws_bytes = 0;
   // ORB workspace (per image b < max_batch)
   uint8_t* pyr = nullptr;     // [B][total_px]
-  uint8_t* blur = nullptr;    // [B][total_px]
+  uint8_t* blur = nullptr;    // [B][total_px] debug only (orb_blur_debug), allocated on first use
+  int orb_last_batch = 0;     // images of the last ORB call
   uint8_t* score = nullptr;   // [B][total_px]
   int32_t* rowcnt = nullptr;  // [B][total_rows]
   int32_t* rowoff = nullptr;  // [B][total_rows]
@@ -91,6 +92,7 @@ struct fvo_ctx {
   int16_t* rs_table = nullptr;    // [cap+1][rs_table_iters][5] RNG(-1) RANSAC subsets per point count
   int32_t rs_table_iters = 0;     //   (shared by PnP and the essential-matrix RANSAC)
   double* pnp_models = nullptr;   // [B][max_iters][6] hypotheses (rvec, tvec)
+  double* pnp_ws = nullptr;       // [B][max_iters][PNP_WS] EPnP null space + subset state between launches
   int32_t* pnp_good = nullptr;    // [B][max_iters] inlier counts
   void* pnp_state = nullptr;      // [B] PnpState
   int32_t pnp_max_iters = 0;
@@ -148,6 +150,7 @@ int sgbm_run(fvo_ctx* ctx, const uint8_t* L, const uint8_t* R, int batch, int64_
              int16_t* disp, hipStream_t s);
 int pose_init(fvo_ctx* ctx);
 int ransac_table_init(fvo_ctx* ctx);
+int orb_blur_debug(fvo_ctx* ctx);
 int backproject_run(fvo_ctx* ctx, const int16_t* disp, const float* kp0, const float* kp1, const int32_t* matches,
                     const int32_t* nmatch, int batch, int cap, const double* K, double baseline, float* P3, float* p2,
                     int32_t* npts, hipStream_t s);

@@ -704,41 +704,88 @@ __global__ __launch_bounds__(256) void k_blur(const OrbDev G, const uint8_t* __r
 }
 
 // ------------------------------------------------------------------ rBRIEF
-__global__ void k_brief(const OrbDev G, const uint8_t* __restrict__ blur, const float* __restrict__ kp, const int32_t* __restrict__ counts,
-                        uint8_t* __restrict__ desc, int64_t total, int cap) {
-  int b = blockIdx.y;
-  int n = counts[b];
+// The descriptor reads the blurred level only at its 512 rotated pattern samples, all within
+// 19 px of the keypoint (|pattern| <= 13 * sqrt 2), so the blur is computed for that patch
+// only instead of for the whole pyramid: one wave per keypoint stages the 45 x 45 source patch
+// (REFLECT_101 resolved while staging, as k_blur does) in LDS, lanes 0..38 each stream one
+// column down the 45 rows with the horizontal 7-tap sum from LDS and the vertical 7-tap sum
+// from a register window -- exactly k_blur's integer arithmetic and rounding -- into a 39 x 39
+// blurred patch in LDS, then the samples are compared from it (4 ballots = the 32 bytes).
+constexpr int kBrR = 19, kBrP = 2 * kBrR + 1, kBrS = kBrP + 6;  // sample radius, blurred / source side
+constexpr int kBrSW = kBrS + 3, kBrPW = kBrP + 1;                // LDS row pitches
+
+__global__ __launch_bounds__(256) void k_brief(const OrbDev G, const uint8_t* __restrict__ pyr,
+                                               const float* __restrict__ kp, const int32_t* __restrict__ counts,
+                                               uint8_t* __restrict__ desc, int64_t total, int cap) {
+  __shared__ uint8_t s_src[4][kBrS][kBrSW];
+  __shared__ uint8_t s_blr[4][kBrP][kBrPW];
+  const int b = blockIdx.y;
+  const int n = counts[b];
   if (n < 0) return;
-  int wpb = blockDim.x >> 6, lane = wave_lane();
-  for (int j = blockIdx.x * wpb + (threadIdx.x >> 6); j < n; j += gridDim.x * wpb) {
+  const int wpb = blockDim.x >> 6, lane = wave_lane(), wv = threadIdx.x >> 6;
+  uint8_t(*src)[kBrSW] = s_src[wv];
+  uint8_t(*blr)[kBrPW] = s_blr[wv];
+  for (int j = blockIdx.x * wpb + wv; j < n; j += gridDim.x * wpb) {
     const float* k = kp + ((int64_t)b * cap + j) * FVO_KP_STRIDE;
-    int l = (int)k[5];
-    float scale = 1.f / G.scale[l];
+    const int l = (int)k[5];
+    const float scale = 1.f / G.scale[l];
     float angle = k[3];
     angle *= (float)(3.14159265358979323846 / 180.f);
-    float a = (float)cos((double)angle), bb = (float)sin((double)angle);
-    int cy = (int)rintf(k[1] * scale), cx = (int)rintf(k[0] * scale);
-    int w = G.w[l];
-    const uint8_t* c = blur + b * total + G.off[l] + (int64_t)cy * w + cx;
+    const float a = (float)cos((double)angle), bb = (float)sin((double)angle);
+    const int cy = (int)rintf(k[1] * scale), cx = (int)rintf(k[0] * scale);
+    const int w = G.w[l], h = G.h[l];
+    const uint8_t* im = pyr + b * total + G.off[l];
+    const int sx0 = cx - kBrR - 3, sy0 = cy - kBrR - 3;
+    for (int i = lane; i < kBrS * kBrS; i += 64) {
+      const int r = i / kBrS, c = i - r * kBrS;
+      const int y = reflect101(min(sy0 + r, 2 * (h - 1)), h);
+      const int x = reflect101(min(sx0 + c, 2 * (w - 1)), w);
+      src[r][c] = im[(int64_t)y * w + x];
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < kBrP) {
+      const int c = lane;
+      int win[7] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int r = 0; r < kBrS; ++r) {
+        int hs = 0;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) hs += c_gk[t] * src[r][c + t];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) win[q] = win[q + 1];
+        win[6] = hs;
+        if (r >= 6) {
+          int sv = 0;
+#pragma unroll
+          for (int q = 0; q < 7; ++q) sv += c_gk[q] * win[q];
+          const int v = (sv + 32767 + ((sv >> 16) & 1)) >> 16;  // round half to even, as k_blur
+          blr[r - 6][c] = (uint8_t)min(v, 255);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
     unsigned long long words[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      int pi = q * 64 + lane;
+      const int pi = q * 64 + lane;
       int v[2];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        float px = (float)c_pattern[pi * 4 + 2 * s], py = (float)c_pattern[pi * 4 + 2 * s + 1];
-        float xx = px * a - py * bb;
-        float yy = px * bb + py * a;
-        int ix = (int)rintf(xx), iy = (int)rintf(yy);
-        v[s] = c[iy * w + ix];
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const float px = (float)c_pattern[pi * 4 + 2 * s2], py = (float)c_pattern[pi * 4 + 2 * s2 + 1];
+        const float xx = px * a - py * bb;
+        const float yy = px * bb + py * a;
+        const int ix = (int)rintf(xx), iy = (int)rintf(yy);
+        v[s2] = blr[iy + kBrR][ix + kBrR];
       }
       words[q] = __ballot(v[0] < v[1]);
     }
     if (lane < 4) {
-      unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
-      reinterpret_cast<unsigned long long*>(desc + ((int64_t)b * cap + j) * FVO_DESC_BYTES)[lane] = wv;
+      const unsigned long long wv4 = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+      reinterpret_cast<unsigned long long*>(desc + ((int64_t)b * cap + j) * FVO_DESC_BYTES)[lane] = wv4;
     }
+    __builtin_amdgcn_wave_barrier();  // the next keypoint overwrites this wave's patches
   }
 }
 
@@ -849,7 +896,7 @@ int orb_init(fvo_ctx* ctx) {
   int64_t maxcand = 0;
   for (int l = 0; l < c.nlevels; ++l) maxcand = std::max<int64_t>(maxcand, g.cand_off[l + 1] - g.cand_off[l]);
   ctx->scratch_per = 2 * maxcand;
-  if ((rc = fvo_alloc(ctx, &ctx->pyr, B * g.total_px)) || (rc = fvo_alloc(ctx, &ctx->blur, B * g.total_px)) ||
+  if ((rc = fvo_alloc(ctx, &ctx->pyr, B * g.total_px)) ||
       (rc = fvo_alloc(ctx, &ctx->score, B * g.total_px)) || (rc = fvo_alloc(ctx, &ctx->rowcnt, B * g.total_rows)) ||
       (rc = fvo_alloc(ctx, &ctx->rowoff, B * g.total_rows)) || (rc = fvo_alloc(ctx, &ctx->cand, B * g.cand_total)) ||
       (rc = fvo_alloc(ctx, &ctx->hel, B * g.cand_total)) || (rc = fvo_alloc(ctx, &ctx->ncand, B * c.nlevels)) ||
@@ -925,9 +972,28 @@ int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride
   FVO_TIMED(ctx, KN_ORB_OFFSETS, s, hipLaunchKernelGGL(k_offsets, dim3((batch + 63) / 64), dim3(64), 0, s, ctx->nsel2, ctx->koff, counts, batch, L, cap));
   FVO_TIMED(ctx, KN_ORB_ANGLE, s, hipLaunchKernelGGL(k_angle, dim3(16, L, batch), dim3(256), 0, s, G, ctx->pyr, ctx->hel, ctx->nsel2, ctx->koff, kp,
                      total, g.cand_total, L, cap, c.patch_size));
-  FVO_TIMED(ctx, KN_ORB_BLUR, s, hipLaunchKernelGGL(k_blur, dim3(G.btile0[L], batch), dim3(256), 0, s, G, ctx->pyr, ctx->blur, total));
-  FVO_TIMED(ctx, KN_ORB_BRIEF, s, hipLaunchKernelGGL(k_brief, dim3(64, batch), dim3(256), 0, s, G, ctx->blur, kp, counts, desc, total, cap));
+  FVO_TIMED(ctx, KN_ORB_BRIEF, s, hipLaunchKernelGGL(k_brief, dim3(64, batch), dim3(256), 0, s, G, ctx->pyr, kp, counts, desc, total, cap));
+  ctx->orb_last_batch = batch;
   FVO_LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+// Debug hook (fvo_debug_buffer 1): the blurred pyramid of the last fvo_orb_detect_compute
+// call, which the hot path no longer materialises (k_brief blurs each keypoint's patch).
+int orb_blur_debug(fvo_ctx* ctx) {
+  if (!ctx->pyr) return fvo_fail(ctx, "orb stage not enabled");
+  const OrbGeom& g = ctx->g;
+  if (!ctx->blur) {
+    int rc = fvo_alloc(ctx, &ctx->blur, (int64_t)ctx->cfg.max_batch * g.total_px);
+    if (rc) return rc;
+  }
+  if (ctx->orb_last_batch > 0) {
+    const OrbDev G = make_dev(g);
+    hipLaunchKernelGGL(k_blur, dim3(G.btile0[g.nlevels], ctx->orb_last_batch), dim3(256), 0, 0, G, ctx->pyr, ctx->blur,
+                       g.total_px);
+    FVO_LAUNCH_CHECK(ctx);
+  }
+  FVO_HIP(ctx, hipDeviceSynchronize());
   return 0;
 }
 

@@ -91,17 +91,46 @@ __global__ void k_backproject(const int16_t* __restrict__ disp, const float* __r
 }
 
 // ------------------------------------------------------------------ small fp64 linear algebra
+// Stable insertion sort of w descending (ord[] as dsvd's loop builds it) with every index
+// static: position j holds (sw[j], so[j]); the while loop becomes a predicated shift.
+template <int N>
+__device__ __forceinline__ void sort_desc(const double* w, double* sw, int* so) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) { sw[j] = w[j]; so[j] = j; }
+#pragma unroll
+  for (int i = 1; i < N; ++i) {
+    const double wk = sw[i];
+    const int k = so[i];
+    bool mv = true;
+#pragma unroll
+    for (int j = i; j > 0; --j) {
+      const bool sh = mv && sw[j - 1] < wk;
+      const double nw = sh ? sw[j - 1] : (mv ? wk : sw[j]);
+      const int no = sh ? so[j - 1] : (mv ? k : so[j]);
+      sw[j] = nw;
+      so[j] = no;
+      mv = sh;
+    }
+    if (mv) { sw[0] = wk; so[0] = k; }
+  }
+}
+
 // A (m x n row-major, m >= n) = U diag(W) V^T, W descending (one-sided Jacobi).
 template <int M, int N>
 __device__ void dsvd(const double* A, double* W, double* U, double* V) {
   double u[M * N], v[N * N], w[N];
+  #pragma unroll
   for (int i = 0; i < M * N; ++i) u[i] = A[i];
+  #pragma unroll
   for (int i = 0; i < N * N; ++i) v[i] = (i % (N + 1) == 0) ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 60; ++sweep) {
     double off = 0.0;
+    #pragma unroll
     for (int p = 0; p < N - 1; ++p)
+      #pragma unroll
       for (int q = p + 1; q < N; ++q) {
         double a = 0, bb = 0, g = 0;
+        #pragma unroll
         for (int i = 0; i < M; ++i) {
           double up = u[i * N + p], uq = u[i * N + q];
           a += up * up;
@@ -115,11 +144,13 @@ __device__ void dsvd(const double* A, double* W, double* U, double* V) {
         double zeta = (bb - a) / (2.0 * g);
         double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
         double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+        #pragma unroll
         for (int i = 0; i < M; ++i) {
           double up = u[i * N + p], uq = u[i * N + q];
           u[i * N + p] = c * up - s * uq;
           u[i * N + q] = s * up + c * uq;
         }
+        #pragma unroll
         for (int i = 0; i < N; ++i) {
           double vp = v[i * N + p], vq = v[i * N + q];
           v[i * N + p] = c * vp - s * vq;
@@ -128,24 +159,38 @@ __device__ void dsvd(const double* A, double* W, double* U, double* V) {
       }
     if (off < 1e-15) break;
   }
-  int ord[N];
+#pragma unroll
   for (int j = 0; j < N; ++j) {
     double s = 0;
+#pragma unroll
     for (int i = 0; i < M; ++i) s += u[i * N + j] * u[i * N + j];
     w[j] = sqrt(s);
-    ord[j] = j;
   }
-  for (int i = 1; i < N; ++i) {  // stable insertion sort, descending
-    int k = ord[i], j = i;
-    while (j > 0 && w[ord[j - 1]] < w[k]) { ord[j] = ord[j - 1]; --j; }
-    ord[j] = k;
-  }
+  double sw[N];
+  int ord[N];
+  sort_desc<N>(w, sw, ord);
+  // column ord[jj] picked by compile-time selects (a runtime column index would put u and v
+  // in scratch for the whole decomposition)
+#pragma unroll
   for (int jj = 0; jj < N; ++jj) {
-    int j = ord[jj];
-    W[jj] = w[j];
-    double inv = w[j] > 0 ? 1.0 / w[j] : 0.0;
-    for (int i = 0; i < M; ++i) U[i * N + jj] = u[i * N + j] * inv;
-    for (int i = 0; i < N; ++i) V[i * N + jj] = v[i * N + j];
+    const int j = ord[jj];
+    const double wj = sw[jj];
+    W[jj] = wj;
+    const double inv = wj > 0 ? 1.0 / wj : 0.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      double x = 0.0;
+#pragma unroll
+      for (int c = 0; c < N; ++c) x = (c == j) ? u[i * N + c] : x;
+      U[i * N + jj] = x * inv;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      double x = 0.0;
+#pragma unroll
+      for (int c = 0; c < N; ++c) x = (c == j) ? v[i * N + c] : x;
+      V[i * N + jj] = x;
+    }
   }
 }
 
@@ -276,10 +321,14 @@ __device__ void dlt12_null(const double* LLp, double* out) {
 // rank-deficient case.  On well-conditioned systems both give the same step to rounding.
 __device__ bool chol_solve6(const double* A, const double* b, double* x) {
   double L[6][6], y[6], dmax = 0.0;
+#pragma unroll
   for (int i = 0; i < 6; ++i) dmax = fmax(dmax, A[i * 6 + i]);
+#pragma unroll
   for (int i = 0; i < 6; ++i)
+#pragma unroll
     for (int j = 0; j <= i; ++j) {
       double s = A[i * 6 + j];
+#pragma unroll
       for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
       if (i == j) {
         if (!(s > 1e-12 * dmax)) return false;
@@ -288,13 +337,17 @@ __device__ bool chol_solve6(const double* A, const double* b, double* x) {
         L[i][j] = s / L[j][j];
       }
     }
+#pragma unroll
   for (int i = 0; i < 6; ++i) {
     double s = b[i];
+#pragma unroll
     for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
     y[i] = s / L[i][i];
   }
+#pragma unroll
   for (int i = 5; i >= 0; --i) {
     double s = y[i];
+#pragma unroll
     for (int k = i + 1; k < 6; ++k) s -= L[k][i] * x[k];
     x[i] = s / L[i][i];
   }
@@ -306,15 +359,19 @@ __device__ void dsolve(const double* A, const double* b, double* x) {
   double W[N], U[M * N], V[N * N], tmp[N];
   dsvd<M, N>(A, W, U, V);
   double thr = DBL_EPSILON * (M > N ? M : N) * W[0];
+#pragma unroll
   for (int j = 0; j < N; ++j) {
     tmp[j] = 0.0;
     if (W[j] <= thr) continue;
     double s = 0;
+#pragma unroll
     for (int i = 0; i < M; ++i) s += U[i * N + j] * b[i];
     tmp[j] = s / W[j];
   }
+#pragma unroll
   for (int i = 0; i < N; ++i) {
     double s = 0;
+#pragma unroll
     for (int j = 0; j < N; ++j) s += V[i * N + j] * tmp[j];
     x[i] = s;
   }
@@ -488,26 +545,20 @@ __device__ __forceinline__ void dsvd12_null4(double* __restrict__ u, double (*ou
     if (off < 1e-15) break;
   }
   double w[12];
-  int ord[12];
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
     double s = 0;
 #pragma unroll
     for (int i = 0; i < 12; ++i) s += u[(i * 12 + j) * S] * u[(i * 12 + j) * S];
     w[j] = sqrt(s);
-    ord[j] = j;
   }
-  for (int i = 1; i < 12; ++i) {  // stable insertion sort, descending (as dsvd)
-    int k = ord[i], j = i;
-    while (j > 0 && w[ord[j - 1]] < w[k]) { ord[j] = ord[j - 1]; --j; }
-    ord[j] = k;
-  }
+  double sw[12];
+  int ord[12];
+  sort_desc<12>(w, sw, ord);  // stable, descending (as dsvd)
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int j = ord[8 + r];
-    double wj = 0.0;
-#pragma unroll
-    for (int c = 0; c < 12; ++c) wj = (c == j) ? w[c] : wj;
+    const double wj = sw[8 + r];
     const double inv = wj > 0 ? 1.0 / wj : 0.0;
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
@@ -532,37 +583,53 @@ struct EPnPd {
   double cws[4][3], ccs[4][3];
 
   __device__ void choose_control_points() {
+    #pragma unroll
     for (int j = 0; j < 3; ++j) cws[0][j] = 0;
+    #pragma unroll
     for (int i = 0; i < NP; ++i)
+      #pragma unroll
       for (int j = 0; j < 3; ++j) cws[0][j] += pws[3 * i + j];
+    #pragma unroll
     for (int j = 0; j < 3; ++j) cws[0][j] /= NP;
     double A[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    #pragma unroll
     for (int i = 0; i < NP; ++i) {
       double d[3] = {pws[3 * i] - cws[0][0], pws[3 * i + 1] - cws[0][1], pws[3 * i + 2] - cws[0][2]};
+      #pragma unroll
       for (int a = 0; a < 3; ++a)
+        #pragma unroll
         for (int bb = 0; bb < 3; ++bb) A[a * 3 + bb] += d[a] * d[bb];
     }
     double W[3], U[9], V[9];
     dsvd<3, 3>(A, W, U, V);
+    #pragma unroll
     for (int i = 1; i < 4; ++i) {
       double k = sqrt(W[i - 1] / NP);
+      #pragma unroll
       for (int j = 0; j < 3; ++j) cws[i][j] = cws[0][j] + k * U[j * 3 + (i - 1)];
     }
   }
   __device__ void barycentric() {
     double cc[9], ci[9], W[3], U[9], V[9];
+    #pragma unroll
     for (int i = 0; i < 3; ++i)
+      #pragma unroll
       for (int j = 1; j < 4; ++j) cc[3 * i + j - 1] = cws[j][i] - cws[0][i];
     dsvd<3, 3>(cc, W, U, V);
+    #pragma unroll
     for (int i = 0; i < 3; ++i)
+      #pragma unroll
       for (int j = 0; j < 3; ++j) {
         double s = 0;
+        #pragma unroll
         for (int k = 0; k < 3; ++k) s += (W[k] > 0 ? V[i * 3 + k] / W[k] : 0.0) * U[j * 3 + k];
         ci[i * 3 + j] = s;
       }
+    #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const double* p = &pws[3 * i];
       double* a = &alphas[4 * i];
+      #pragma unroll
       for (int j = 0; j < 3; ++j)
         a[1 + j] = ci[3 * j] * (p[0] - cws[0][0]) + ci[3 * j + 1] * (p[1] - cws[0][1]) + ci[3 * j + 2] * (p[2] - cws[0][2]);
       a[0] = 1.0f - a[1] - a[2] - a[3];
@@ -570,16 +637,22 @@ struct EPnPd {
   }
   // nv[r] = ut row 8 + r (EPnP's v_{3-r}); rows 11..8 are the four null-space directions
   __device__ void compute_ccs(const double* betas, const double (*nv)[12]) {
+    #pragma unroll
     for (int i = 0; i < 4; ++i) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
+    #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const double* v = nv[3 - i];
+      #pragma unroll
       for (int j = 0; j < 4; ++j)
+        #pragma unroll
         for (int k = 0; k < 3; ++k) ccs[j][k] += betas[i] * v[3 * j + k];
     }
   }
   __device__ void compute_pcs() {
+    #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const double* a = &alphas[4 * i];
+      #pragma unroll
       for (int j = 0; j < 3; ++j) pcs[3 * i + j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
     }
   }
@@ -587,22 +660,30 @@ struct EPnPd {
     compute_ccs(betas, nv);
     compute_pcs();
     if (pcs[2] < 0.0) {
+      #pragma unroll
       for (int i = 0; i < 4; ++i)
+        #pragma unroll
         for (int j = 0; j < 3; ++j) ccs[i][j] = -ccs[i][j];
+      #pragma unroll
       for (int i = 0; i < 3 * NP; ++i) pcs[i] = -pcs[i];
     }
     double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+    #pragma unroll
     for (int i = 0; i < NP; ++i)
+      #pragma unroll
       for (int j = 0; j < 3; ++j) {
         pc0[j] += pcs[3 * i + j];
         pw0[j] += pws[3 * i + j];
       }
+    #pragma unroll
     for (int j = 0; j < 3; ++j) {
       pc0[j] /= NP;
       pw0[j] /= NP;
     }
     double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    #pragma unroll
     for (int i = 0; i < NP; ++i)
+      #pragma unroll
       for (int j = 0; j < 3; ++j) {
         double dc = pcs[3 * i + j] - pc0[j];
         abt[3 * j] += dc * (pws[3 * i] - pw0[0]);
@@ -611,7 +692,9 @@ struct EPnPd {
       }
     double W[3], U[9], V[9];
     dsvd<3, 3>(abt, W, U, V);
+    #pragma unroll
     for (int i = 0; i < 3; ++i)
+      #pragma unroll
       for (int j = 0; j < 3; ++j) R[i * 3 + j] = U[i * 3] * V[j * 3] + U[i * 3 + 1] * V[j * 3 + 1] + U[i * 3 + 2] * V[j * 3 + 2];
     double det = R[0] * R[4] * R[8] + R[1] * R[5] * R[6] + R[2] * R[3] * R[7] - R[2] * R[4] * R[6] - R[1] * R[3] * R[8] -
                  R[0] * R[5] * R[7];
@@ -620,8 +703,10 @@ struct EPnPd {
       R[7] = -R[7];
       R[8] = -R[8];
     }
+    #pragma unroll
     for (int i = 0; i < 3; ++i) t[i] = pc0[i] - dot3(&R[3 * i], pw0);
     double sum2 = 0.0;
+    #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const double* pw = &pws[3 * i];
       double Xc = dot3(&R[0], pw) + t[0], Yc = dot3(&R[3], pw) + t[1];
@@ -635,11 +720,14 @@ struct EPnPd {
   __device__ static void qr_solve(double* A, double* b, double* X) {
     const int nr = 6, nc = 4;
     double A1[4], A2[4];
+    #pragma unroll
     for (int k = 0; k < nc; ++k) {
       double eta = fabs(A[k * nc + k]);
+      #pragma unroll
       for (int i = k + 1; i < nr; ++i) eta = fmax(eta, fabs(A[i * nc + k]));
       if (eta == 0) return;
       double sum2 = 0.0, inv = 1. / eta;
+      #pragma unroll
       for (int i = k; i < nr; ++i) {
         A[i * nc + k] *= inv;
         sum2 += A[i * nc + k] * A[i * nc + k];
@@ -649,29 +737,39 @@ struct EPnPd {
       A[k * nc + k] += sigma;
       A1[k] = sigma * A[k * nc + k];
       A2[k] = -eta * sigma;
+      #pragma unroll
       for (int j = k + 1; j < nc; ++j) {
         double sum = 0;
+        #pragma unroll
         for (int i = k; i < nr; ++i) sum += A[i * nc + k] * A[i * nc + j];
         double tau = sum / A1[k];
+        #pragma unroll
         for (int i = k; i < nr; ++i) A[i * nc + j] -= tau * A[i * nc + k];
       }
     }
+    #pragma unroll
     for (int j = 0; j < nc; ++j) {
       double tau = 0;
+      #pragma unroll
       for (int i = j; i < nr; ++i) tau += A[i * nc + j] * b[i];
       tau /= A1[j];
+      #pragma unroll
       for (int i = j; i < nr; ++i) b[i] -= tau * A[i * nc + j];
     }
     X[nc - 1] = b[nc - 1] / A2[nc - 1];
+    #pragma unroll
     for (int i = nc - 2; i >= 0; --i) {
       double sum = 0;
+      #pragma unroll
       for (int j = i + 1; j < nc; ++j) sum += A[i * nc + j] * X[j];
       X[i] = (b[i] - sum) / A2[i];
     }
   }
   __device__ static void gauss_newton(const double* L, const double* rho, double* betas) {
+#pragma nounroll
     for (int it = 0; it < 5; ++it) {
       double A[24], b[6], x[4] = {0, 0, 0, 0};
+      #pragma unroll
       for (int i = 0; i < 6; ++i) {
         const double* r = L + 10 * i;
         A[i * 4 + 0] = 2 * r[0] * betas[0] + r[1] * betas[1] + r[3] * betas[2] + r[6] * betas[3];
@@ -684,30 +782,43 @@ struct EPnPd {
                          r[9] * betas[3] * betas[3]);
       }
       qr_solve(A, b, x);
+      #pragma unroll
       for (int i = 0; i < 4; ++i) betas[i] += x[i];
     }
   }
-  // MtM: this lane's slice of an LDS [144][64] array (element k at MtM[k * 64]).
-  __device__ void compute_pose(double* R, double* t, double* __restrict__ MtM) {
+  // First half of compute_pose: control points, barycentric coordinates, M^T M and its four
+  // null-space directions nv.  MtM: this lane's slice of an LDS [144][64] array (element k at
+  // MtM[k * 64]).
+  __device__ void null_space(double* __restrict__ MtM, double (*nv)[12]) {
     choose_control_points();
     barycentric();
+    #pragma unroll
     for (int i = 0; i < 144; ++i) MtM[i * 64] = 0.0;
+    #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const double* as = &alphas[4 * i];
       double u = us[2 * i], v = us[2 * i + 1];
       double M1[12], M2[12];
+      #pragma unroll
       for (int j = 0; j < 4; ++j) {
         M1[3 * j] = as[j] * fu; M1[3 * j + 1] = 0.0; M1[3 * j + 2] = as[j] * (uc - u);
         M2[3 * j] = 0.0; M2[3 * j + 1] = as[j] * fv; M2[3 * j + 2] = as[j] * (vc - v);
       }
       // rows of M in order (M1 then M2), each accumulated on its own: the oracle's summation order
+      #pragma unroll
       for (int a = 0; a < 12; ++a)
+        #pragma unroll
         for (int bb = 0; bb < 12; ++bb) MtM[(a * 12 + bb) * 64] += M1[a] * M1[bb];
+      #pragma unroll
       for (int a = 0; a < 12; ++a)
+        #pragma unroll
         for (int bb = 0; bb < 12; ++bb) MtM[(a * 12 + bb) * 64] += M2[a] * M2[bb];
     }
-    double nv[4][12];  // U^T rows 8..11 (singular vectors of the 4 smallest singular values)
-    dsvd12_null4<64>(MtM, nv);
+    dsvd12_null4<64>(MtM, nv);  // U^T rows 8..11 (singular vectors of the 4 smallest singular values)
+  }
+  // Second half: the three beta approximations + Gauss-Newton, the best (R, t).  Needs pws,
+  // us, alphas and cws from null_space().
+  __device__ void pose_from_null(const double (*nv)[12], double* R, double* t) {
     double L[60], rho[6];
     {
       const double* vv[4] = {nv[3], nv[2], nv[1], nv[0]};
@@ -736,6 +847,7 @@ struct EPnPd {
       rho[3] = dist2(cws[1], cws[2]); rho[4] = dist2(cws[1], cws[3]); rho[5] = dist2(cws[2], cws[3]);
     }
     double best_err = 0, Rb[9], tb[3];
+#pragma nounroll
     for (int N = 1; N <= 3; ++N) {
       double betas[4];
       if (N == 1) {
@@ -822,6 +934,7 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
   // ---- init (cvFindExtrinsicCameraParams2, useExtrinsicGuess = false)
   const int lane = wave_lane();
   double acc[28];
+#pragma unroll
   for (int k = 0; k < 28; ++k) acc[k] = 0;
   for (int i = lane; i < n; i += 64) {
     int j = inl[i];
@@ -830,15 +943,19 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
     acc[1] += (double)P3[3 * j + 1];
     acc[2] += (double)P3[3 * j + 2];
   }
+#pragma unroll
   for (int k = 0; k < 3; ++k) acc[k] = wsum_d(acc[k]);
   double Mc[3] = {acc[0] / n, acc[1] / n, acc[2] / n};
   double MM[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int i = lane; i < n; i += 64) {
     int j = inl[i];
     double d[3] = {(double)P3[3 * j] - Mc[0], (double)P3[3 * j + 1] - Mc[1], (double)P3[3 * j + 2] - Mc[2]};
+#pragma unroll
     for (int a = 0; a < 3; ++a)
+#pragma unroll
       for (int b = 0; b < 3; ++b) MM[a * 3 + b] += d[a] * d[b];
   }
+#pragma unroll
   for (int k = 0; k < 9; ++k) MM[k] = wsum_d(MM[k]);
   double W3[3], U3[9], V3[9];
   dsvd<3, 3>(MM, W3, U3, V3);
@@ -849,6 +966,7 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
     return;
   }
   double LLp[78];
+#pragma unroll
   for (int k = 0; k < 78; ++k) LLp[k] = 0;
   double Rt[9], T[3];
   if (!planar) {
@@ -859,16 +977,23 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
       double r0[12] = {P[0], P[1], P[2], 1., 0, 0, 0, 0, x * P[0], x * P[1], x * P[2], x};
       double r1[12] = {0, 0, 0, 0, P[0], P[1], P[2], 1., y * P[0], y * P[1], y * P[2], y};
       int k = 0;
+#pragma unroll
       for (int a = 0; a < 12; ++a)
+#pragma unroll
         for (int b = a; b < 12; ++b) LLp[k++] += r0[a] * r0[b] + r1[a] * r1[b];
     }
   } else {
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
       for (int j = 0; j < 3; ++j) Rt[i * 3 + j] = V3[j * 3 + i];
     if (Rt[2] * Rt[2] + Rt[5] * Rt[5] < 1e-10)
+#pragma unroll
       for (int i = 0; i < 9; ++i) Rt[i] = (i % 4 == 0);
     if (ddet3(Rt) < 0)
+#pragma unroll
       for (int i = 0; i < 9; ++i) Rt[i] = -Rt[i];
+#pragma unroll
     for (int i = 0; i < 3; ++i) T[i] = -(Rt[i * 3] * Mc[0] + Rt[i * 3 + 1] * Mc[1] + Rt[i * 3 + 2] * Mc[2]);
     // homography DLT (A^T A, 9x9 upper triangle = 45 entries)
     for (int i = lane; i < n; i += 64) {
@@ -880,10 +1005,13 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
       double r0[9] = {X, Y, 1, 0, 0, 0, -u * X, -u * Y, -u};
       double r1[9] = {0, 0, 0, X, Y, 1, -v * X, -v * Y, -v};
       int k = 0;
+#pragma unroll
       for (int a = 0; a < 9; ++a)
+#pragma unroll
         for (int b = a; b < 9; ++b) LLp[k++] += r0[a] * r0[b] + r1[a] * r1[b];
     }
   }
+#pragma unroll
   for (int k = 0; k < 78; ++k) LLp[k] = wsum_d(LLp[k]);
   double param[6] = {0, 0, 0, 0, 0, 0};
   double RRt[12];
@@ -894,19 +1022,26 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
       double RR[9] = {RRt[0], RRt[1], RRt[2], RRt[4], RRt[5], RRt[6], RRt[8], RRt[9], RRt[10]};
       double tt[3] = {RRt[3], RRt[7], RRt[11]};
       if (ddet3(RR) < 0) {
+#pragma unroll
         for (int i = 0; i < 9; ++i) RR[i] = -RR[i];
+#pragma unroll
         for (int i = 0; i < 3; ++i) tt[i] = -tt[i];
       }
       double sc = 0;
+#pragma unroll
       for (int i = 0; i < 9; ++i) sc += RR[i] * RR[i];
       sc = sqrt(sc);
       double Wr[3], Ur[9], Vr[9];
       dsvd<3, 3>(RR, Wr, Ur, Vr);
+#pragma unroll
       for (int i = 0; i < 3; ++i)
+#pragma unroll
         for (int j = 0; j < 3; ++j) R[i * 3 + j] = Ur[i * 3] * Vr[j * 3] + Ur[i * 3 + 1] * Vr[j * 3 + 1] + Ur[i * 3 + 2] * Vr[j * 3 + 2];
       double nR = 0;
+#pragma unroll
       for (int i = 0; i < 9; ++i) nR += R[i] * R[i];
       nR = sqrt(nR);
+#pragma unroll
       for (int i = 0; i < 3; ++i) param[3 + i] = tt[i] * nR / sc;
       rod_R2r(R, param);
     } else {
@@ -915,14 +1050,19 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
       double* V9 = sh.dlt[4];
       double W9[9], H[9], t[3];
       int k = 0;
+#pragma unroll
       for (int a = 0; a < 9; ++a)
+#pragma unroll
         for (int b = a; b < 9; ++b) { AtA[a * 9 + b] = LLp[k]; AtA[b * 9 + a] = LLp[k]; ++k; }
       dsvd_ws<9, 9>(AtA, W9, U9, V9, sh.dlt[1], sh.dlt[2]);
+#pragma unroll
       for (int i = 0; i < 9; ++i) H[i] = V9[i * 9 + 8];
       if (fabs(H[8]) >= 1e-300) {
+#pragma unroll
         for (int i = 0; i < 9; ++i) H[i] /= H[8];
         double h1 = sqrt(H[0] * H[0] + H[3] * H[3] + H[6] * H[6]);
         double h2 = sqrt(H[1] * H[1] + H[4] * H[4] + H[7] * H[7]);
+#pragma unroll
         for (int i = 0; i < 3; ++i) {
           H[i * 3] /= fmax(h1, DBL_EPSILON);
           H[i * 3 + 1] /= fmax(h2, DBL_EPSILON);
@@ -934,25 +1074,32 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
         double r[3];
         rod_R2r(H, r);
         rod_r2R(r, H, nullptr);
+#pragma unroll
         for (int i = 0; i < 3; ++i) t[i] += H[i * 3] * T[0] + H[i * 3 + 1] * T[1] + H[i * 3 + 2] * T[2];
+#pragma unroll
         for (int i = 0; i < 3; ++i)
+#pragma unroll
           for (int j = 0; j < 3; ++j) R[i * 3 + j] = H[i * 3] * Rt[j] + H[i * 3 + 1] * Rt[3 + j] + H[i * 3 + 2] * Rt[6 + j];
         param[3] = t[0]; param[4] = t[1]; param[5] = t[2];
       } else {
+#pragma unroll
         for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0);
       }
       rod_R2r(R, param);
     }
+#pragma unroll
     for (int i = 0; i < 6; ++i) sh.param[i] = param[i];
   }
   __syncthreads();
   // ---- Levenberg-Marquardt (CvLevMarq semantics)
   auto eval = [&](bool withJ, double* JtJ, double* JtErr) -> double {
     double p[6];
+#pragma unroll
     for (int i = 0; i < 6; ++i) p[i] = sh.param[i];
     double R[9], dR[27];
     rod_r2R(p, R, dR);
     double a[28];
+#pragma unroll
     for (int k = 0; k < 28; ++k) a[k] = 0;
     for (int i = lane; i < n; i += 64) {
       int j = inl[i];
@@ -962,16 +1109,23 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
       a[27] += e0 * e0 + e1 * e1;
       if (withJ) {
         int k = 0;
+#pragma unroll
         for (int r = 0; r < 6; ++r)
+#pragma unroll
           for (int c = r; c < 6; ++c) a[k++] += J[r] * J[c] + J[6 + r] * J[6 + c];
+#pragma unroll
         for (int r = 0; r < 6; ++r) a[21 + r] += J[r] * e0 + J[6 + r] * e1;
       }
     }
+#pragma unroll
     for (int k = withJ ? 0 : 27; k < 28; ++k) a[k] = wsum_d(a[k]);
     if (withJ) {
       int k = 0;
+#pragma unroll
       for (int r = 0; r < 6; ++r)
+#pragma unroll
         for (int c = r; c < 6; ++c) { JtJ[r * 6 + c] = a[k]; JtJ[c * 6 + r] = a[k]; ++k; }
+#pragma unroll
       for (int r = 0; r < 6; ++r) JtErr[r] = a[21 + r];
     }
     return sqrt(a[27]);
@@ -982,21 +1136,27 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
     if (lane == 0) {
       double lambda = exp(lambdaLg10 * log(10.));
       double A[36], x[6];
+#pragma unroll
       for (int i = 0; i < 36; ++i) A[i] = JtJ[i];
+#pragma unroll
       for (int i = 0; i < 6; ++i) A[i * 6 + i] *= 1. + lambda;
       if (!chol_solve6(A, JtErr, x)) dsolve<6, 6>(A, JtErr, x);
+#pragma unroll
       for (int i = 0; i < 6; ++i) sh.param[i] = prev[i] - x[i];
     }
     __syncthreads();
   };
   int iters = 0;
+#pragma unroll
   for (;;) {
     double e0 = eval(true, JtJ, JtErr);
+#pragma unroll
     for (int i = 0; i < 6; ++i) prev[i] = sh.param[i];
     __syncthreads();
     step();
     if (iters == 0) prevErrNorm = e0;
     double errNorm;
+#pragma unroll
     for (;;) {
       errNorm = eval(false, nullptr, nullptr);
       if (errNorm > prevErrNorm && ++lambdaLg10 <= 16) {
@@ -1007,6 +1167,7 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
     }
     lambdaLg10 = fmax(lambdaLg10 - 1, -16.0);
     double dn = 0, pn = 0;
+#pragma unroll
     for (int i = 0; i < 6; ++i) {
       dn += (sh.param[i] - prev[i]) * (sh.param[i] - prev[i]);
       pn += prev[i] * prev[i];
@@ -1048,32 +1209,37 @@ __global__ void k_pnp_subsets(const int32_t* __restrict__ npts, int batch, int c
   state[b] = st;
 }
 
-// One lane per RANSAC iteration: EPnP on its subset (undistorted, float32-rounded
-// normalised points, as solvePnP(SOLVEPNP_EPNP) sees them) and the inlier count of the
-// hypothesis over all points (projectPoints in fp64, error in float32).  Blocks whose
-// first iteration is past the frame's current iteration bound exit immediately.
-__global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ P3all, const float* __restrict__ p2all,
-                                                int cap, Cam K, float thr2, int maxIters, int it_lo,
-                                                const int16_t* __restrict__ table, int table_iters,
-                                                const PnpState* __restrict__ state,
-                                                double* __restrict__ model, int32_t* __restrict__ good) {
+// One lane per RANSAC iteration, EPnP in two launches (one kernel held the whole EPnP state
+// plus the scoring loop at 256 VGPRs with 1.6 KB of scratch per lane):
+//   k_pnp_hyp_a  the subset's points (undistorted, float32-rounded normalised image points, as
+//                solvePnP(SOLVEPNP_EPNP) sees them), control points, barycentric coordinates,
+//                M^T M in LDS and its null space -> workspace;
+//   k_pnp_hyp_b  the beta approximations + Gauss-Newton + (R, t), the model, and its inlier
+//                count over all points (projectPoints in fp64, error in float32).
+// Blocks whose first iteration is past the frame's current iteration bound exit immediately.
+constexpr int PNP_WS = 112;  // doubles per subset: nv 48 | cws 12 | alphas 20 | pws 15 | us 10
+constexpr int PW_NV = 0, PW_CWS = 48, PW_AL = 60, PW_PWS = 80, PW_US = 95;
+
+__global__ __launch_bounds__(64) void k_pnp_hyp_a(const float* __restrict__ P3all, const float* __restrict__ p2all,
+                                                  int cap, Cam K, int maxIters, int it_lo,
+                                                  const int16_t* __restrict__ table, int table_iters,
+                                                  const PnpState* __restrict__ state, double* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) double smem[];  // [144][64] EPnP MtM (one column per lane)
-  double* su = smem;
   const int b = blockIdx.y;
   const int it = it_lo + blockIdx.x * 64 + threadIdx.x;
   const PnpState st = state[b];
   const int n = st.n;
   if (n < 6 || it_lo + (int)blockIdx.x * 64 >= min(st.niters, maxIters)) return;
   if (it >= maxIters) return;
-  // points are read from global memory: the scoring loop's addresses are wave-uniform
-  // (scalar loads), so they take no LDS and leave room for two waves per CU
   const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
   const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
   const int16_t* sb = table + ((int64_t)n * table_iters + it) * 5;
   EPnPd<5> e;
   e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
+#pragma unroll
   for (int i = 0; i < 5; ++i) {
     int j = sb[i];
+#pragma unroll
     for (int c = 0; c < 3; ++c) e.pws[3 * i + c] = (double)P3[j * 3 + c];
     double xy[2];
     dundistort(K, (double)p2[j * 2], (double)p2[j * 2 + 1], xy);
@@ -1081,8 +1247,59 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ P3all,
     e.us[2 * i] = fx * K.fx + K.cx;
     e.us[2 * i + 1] = fy * K.fy + K.cy;
   }
+  double nv[4][12];
+  e.null_space(smem + threadIdx.x, nv);
+  double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int k = 0; k < 12; ++k) w[PW_NV + r * 12 + k] = nv[r][k];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) w[PW_CWS + r * 3 + k] = e.cws[r][k];
+#pragma unroll
+  for (int k = 0; k < 20; ++k) w[PW_AL + k] = e.alphas[k];
+#pragma unroll
+  for (int k = 0; k < 15; ++k) w[PW_PWS + k] = e.pws[k];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) w[PW_US + k] = e.us[k];
+}
+
+__global__ __launch_bounds__(64) void k_pnp_hyp_b(const float* __restrict__ P3all, const float* __restrict__ p2all,
+                                                  int cap, Cam K, float thr2, int maxIters, int it_lo,
+                                                  const PnpState* __restrict__ state, const double* __restrict__ ws,
+                                                  double* __restrict__ model, int32_t* __restrict__ good) {
+  const int b = blockIdx.y;
+  const int it = it_lo + blockIdx.x * 64 + threadIdx.x;
+  const PnpState st = state[b];
+  const int n = st.n;
+  if (n < 6 || it_lo + (int)blockIdx.x * 64 >= min(st.niters, maxIters)) return;
+  if (it >= maxIters) return;
+  // points are read from global memory: the scoring loop's addresses are wave-uniform
+  // (scalar loads)
+  const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
+  const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
+  const double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
+  EPnPd<5> e;
+  e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
+  double nv[4][12];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int k = 0; k < 12; ++k) nv[r][k] = w[PW_NV + r * 12 + k];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) e.cws[r][k] = w[PW_CWS + r * 3 + k];
+#pragma unroll
+  for (int k = 0; k < 20; ++k) e.alphas[k] = w[PW_AL + k];
+#pragma unroll
+  for (int k = 0; k < 15; ++k) e.pws[k] = w[PW_PWS + k];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) e.us[k] = w[PW_US + k];
   double R[9], t[3], r[3], dR[27];
-  e.compute_pose(R, t, su + threadIdx.x);
+  e.pose_from_null(nv, R, t);
   rod_R2r(R, r);
   double* mo = model + ((int64_t)b * maxIters + it) * 6;
   for (int i = 0; i < 3; ++i) { mo[i] = r[i]; mo[3 + i] = t[i]; }
@@ -1100,21 +1317,27 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ P3all,
 // RANSACPointSetRegistrator::run's acceptance loop replayed in iteration order over
 // [it_lo, it_hi): accept iff goodCount > max(maxGoodCount, 4); niters is updated with
 // RANSACUpdateNumIters(confidence, (n - good)/n, 5, niters) and bounds the loop.
-__global__ void k_pnp_replay(int batch, int maxIters, int it_lo, int it_hi, double conf,
-                             const int32_t* __restrict__ good, PnpState* __restrict__ state) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= batch) return;
+// One wave per frame: 64 iterations' counts loaded at once, then walked in order with
+// wave-uniform reads (a lane per frame walking global memory was 73 us per launch).
+__global__ __launch_bounds__(64) void k_pnp_replay(int maxIters, int it_lo, int it_hi, double conf,
+                                                   const int32_t* __restrict__ good, PnpState* __restrict__ state) {
+  const int b = blockIdx.x, lane = threadIdx.x;
   PnpState st = state[b];
   if (st.n < 6) return;
-  for (int it = it_lo; it < it_hi && it < st.niters; ++it) {
-    int g = good[(int64_t)b * maxIters + it];
-    if (g > max(st.maxGood, 4)) {
-      st.best_it = it;
-      st.maxGood = g;
-      st.niters = update_num_iters(conf, (double)(st.n - g) / st.n, 5, st.niters);
+  for (int base = it_lo; base < it_hi && base < st.niters; base += 64) {
+    const int it = base + lane;
+    const int g = (it < it_hi && it < st.niters) ? good[(int64_t)b * maxIters + it] : 0;
+    for (int j = 0; j < 64; ++j) {
+      if (base + j >= it_hi || base + j >= st.niters) break;
+      const int gj = __builtin_amdgcn_readlane(g, j);
+      if (gj > max(st.maxGood, 4)) {
+        st.best_it = base + j;
+        st.maxGood = gj;
+        st.niters = update_num_iters(conf, (double)(st.n - gj) / st.n, 5, st.niters);
+      }
     }
   }
-  state[b] = st;
+  if (lane == 0) state[b] = st;
 }
 
 __global__ __launch_bounds__(64) void k_pnp_refine(const float* __restrict__ P3all, const float* __restrict__ p2all,
@@ -1194,6 +1417,7 @@ int pose_init(fvo_ctx* ctx) {
   int rc;
   if ((rc = fvo_alloc(ctx, &ctx->pnp_sub, n)) || (rc = fvo_alloc(ctx, &ctx->pnp_hyp, 2 * n)) ||
       (rc = ransac_table_init(ctx)) || (rc = fvo_alloc(ctx, &ctx->pnp_models, it * 6)) ||
+      (rc = fvo_alloc(ctx, &ctx->pnp_ws, it * PNP_WS)) ||
       (rc = fvo_alloc(ctx, &ctx->pnp_good, it)) || (rc = fvo_alloc(ctx, (PnpState**)&ctx->pnp_state, B)))
     return rc;
   return 0;
@@ -1234,21 +1458,20 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
   PnpState* st = (PnpState*)ctx->pnp_state;
   const size_t shm = 144 * 64 * sizeof(double);
   if (shm > 64 * 1024)
-    FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_pnp_hyp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_pnp_hyp_a, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   const int first = std::min(maxIters, 128);
+  auto hyp = [&](int lo, int hi) {
+    const dim3 grid((hi - lo + 63) / 64, batch);
+    hipLaunchKernelGGL(k_pnp_hyp_a, grid, dim3(64), shm, s, P3, p2, cap, c, maxIters, lo, ctx->rs_table,
+                       ctx->rs_table_iters, st, ctx->pnp_ws);
+    hipLaunchKernelGGL(k_pnp_hyp_b, grid, dim3(64), 0, s, P3, p2, cap, c, thr2, maxIters, lo, st, ctx->pnp_ws,
+                       ctx->pnp_models, ctx->pnp_good);
+    hipLaunchKernelGGL(k_pnp_replay, dim3(batch), dim3(64), 0, s, maxIters, lo, hi, conf, ctx->pnp_good, st);
+  };
   FVO_TIMED(ctx, KN_PNP, s, {
     hipLaunchKernelGGL(k_pnp_subsets, dim3((batch + 63) / 64), dim3(64), 0, s, npts, batch, cap, maxIters, st);
-    hipLaunchKernelGGL(k_pnp_hyp, dim3((first + 63) / 64, batch), dim3(64), shm, s, P3, p2, cap, c, thr2, maxIters, 0,
-                       ctx->rs_table, ctx->rs_table_iters, st, ctx->pnp_models, ctx->pnp_good);
-    hipLaunchKernelGGL(k_pnp_replay, dim3((batch + 63) / 64), dim3(64), 0, s, batch, maxIters, 0, first, conf,
-                       ctx->pnp_good, st);
-    if (maxIters > first) {
-      hipLaunchKernelGGL(k_pnp_hyp, dim3((maxIters - first + 63) / 64, batch), dim3(64), shm, s, P3, p2, cap, c, thr2,
-                         maxIters, first, ctx->rs_table, ctx->rs_table_iters, st, ctx->pnp_models,
-                         ctx->pnp_good);
-      hipLaunchKernelGGL(k_pnp_replay, dim3((batch + 63) / 64), dim3(64), 0, s, batch, maxIters, first, maxIters, conf,
-                         ctx->pnp_good, st);
-    }
+    hyp(0, first);
+    if (maxIters > first) hyp(first, maxIters);
     hipLaunchKernelGGL(k_pnp_refine, dim3(batch), dim3(64), 0, s, P3, p2, cap, c, thr2, maxIters, st,
                        ctx->pnp_models, rvec, tvec, T, status, inliers, ctx->pnp_sub, ctx->pnp_hyp);
   });
