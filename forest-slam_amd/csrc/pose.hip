@@ -508,65 +508,74 @@ __device__ void dundistort(const Cam& K, double u, double v, double* xy) {
 }
 
 // dsvd<12,12> specialised for EPnP: only U is consumed (the rows ut[8..11] of U^T, i.e. the
-// singular vectors of the four smallest singular values), so V is not accumulated; u lives
-// in LDS (one column of a [144][64] array per lane: conflict-free, and no scratch).  The
+// singular vectors of the four smallest singular values), so V is not accumulated; the
 // operations on u, the norms, the stable descending order and the scaling are exactly those
-// of dsvd (and of the oracle's svd()).
-template <int S>  // u[k] lives at u[k * S] (S = 64: a lane's column of an LDS array [144][64])
-__device__ __forceinline__ void dsvd12_null4(double* __restrict__ u, double (*out)[12]) {
+// of dsvd (and of the oracle's svd()).  Run by an 8-lane group, u[144] (row-major) in LDS
+// shared by the group.  The
+// cyclic pair order (0,1), (0,2), ..., (10,11) is replaced by its anti-diagonals p + q = 2..21:
+// a pair's columns are touched, before and after it, by exactly the same pairs in the same
+// order in both orders (pair (p,q) follows (p,q-1) and (p-1,q) and nothing else on p or q
+// sits between), and the pairs of one anti-diagonal share no column, so the group rotates
+// them at once -- bit-identical to the serial sweep, with 21 dependent steps instead of 66.
+// The column norms, the sort and the output (out[r * 12 + i], r = 0..3) are lane 0's.
+__device__ __forceinline__ void jacobi12_null4_group(double* __restrict__ u, int l, double* __restrict__ out) {
   for (int sweep = 0; sweep < 60; ++sweep) {
     double off = 0.0;
-    for (int p = 0; p < 11; ++p)
-      for (int q = p + 1; q < 12; ++q) {
+#pragma nounroll
+    for (int d = 1; d <= 21; ++d) {
+      const int p0 = d > 11 ? d - 11 : 0;
+      const int cnt = (d - 1) / 2 - p0 + 1;
+      if (l < cnt) {
+        const int p = p0 + l, q = d - p;
         double a = 0, bb = 0, g = 0;
 #pragma unroll
         for (int i = 0; i < 12; ++i) {
-          double up = u[(i * 12 + p) * S], uq = u[(i * 12 + q) * S];
+          const double up = u[i * 12 + p], uq = u[i * 12 + q];
           a += up * up;
           bb += uq * uq;
           g += up * uq;
         }
         if (!(g == 0.0 || fabs(g) <= 1e-300)) {
-          double rel = fabs(g) / sqrt(a * bb);
+          const double rel = fabs(g) / sqrt(a * bb);
           off = fmax(off, rel);
           if (!(rel < 1e-15)) {
-            double zeta = (bb - a) / (2.0 * g);
-            double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-            double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
+            const double zeta = (bb - a) / (2.0 * g);
+            const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+            const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
 #pragma unroll
             for (int i = 0; i < 12; ++i) {
-              double up = u[(i * 12 + p) * S], uq = u[(i * 12 + q) * S];
-              u[(i * 12 + p) * S] = c * up - sn * uq;
-              u[(i * 12 + q) * S] = sn * up + c * uq;
+              const double up = u[i * 12 + p], uq = u[i * 12 + q];
+              u[i * 12 + p] = c * up - sn * uq;
+              u[i * 12 + q] = sn * up + c * uq;
             }
           }
         }
       }
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) off = fmax(off, __shfl_xor(off, o, 8));
     if (off < 1e-15) break;
   }
+  if (l != 0) return;
   double w[12];
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
     double s = 0;
 #pragma unroll
-    for (int i = 0; i < 12; ++i) s += u[(i * 12 + j) * S] * u[(i * 12 + j) * S];
+    for (int i = 0; i < 12; ++i) s += u[i * 12 + j] * u[i * 12 + j];
     w[j] = sqrt(s);
   }
   double sw[12];
   int ord[12];
-  sort_desc<12>(w, sw, ord);  // stable, descending (as dsvd)
+  sort_desc<12>(w, sw, ord);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int j = ord[8 + r];
     const double wj = sw[8 + r];
     const double inv = wj > 0 ? 1.0 / wj : 0.0;
 #pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      double v = 0.0;
-#pragma unroll
-      for (int c = 0; c < 12; ++c) v = (c == j) ? u[(i * 12 + c) * S] : v;
-      out[r][i] = v * inv;
-    }
+    for (int i = 0; i < 12; ++i) out[r * 12 + i] = u[i * 12 + j] * inv;  // u is in LDS: index it directly
   }
 }
 
@@ -786,38 +795,37 @@ struct EPnPd {
       for (int i = 0; i < 4; ++i) betas[i] += x[i];
     }
   }
-  // First half of compute_pose: control points, barycentric coordinates, M^T M and its four
-  // null-space directions nv.  MtM: this lane's slice of an LDS [144][64] array (element k at
-  // MtM[k * 64]).
-  __device__ void null_space(double* __restrict__ MtM, double (*nv)[12]) {
+  // First half of compute_pose: control points, barycentric coordinates and M^T M (element k
+  // at MtM[k * S]); its four null-space directions come from jacobi12_null4.
+  template <int S>
+  __device__ void build_mtm(double* __restrict__ MtM) {
     choose_control_points();
     barycentric();
-    #pragma unroll
-    for (int i = 0; i < 144; ++i) MtM[i * 64] = 0.0;
-    #pragma unroll
+#pragma unroll
+    for (int i = 0; i < 144; ++i) MtM[i * S] = 0.0;
+#pragma unroll
     for (int i = 0; i < NP; ++i) {
       const double* as = &alphas[4 * i];
       double u = us[2 * i], v = us[2 * i + 1];
       double M1[12], M2[12];
-      #pragma unroll
+#pragma unroll
       for (int j = 0; j < 4; ++j) {
         M1[3 * j] = as[j] * fu; M1[3 * j + 1] = 0.0; M1[3 * j + 2] = as[j] * (uc - u);
         M2[3 * j] = 0.0; M2[3 * j + 1] = as[j] * fv; M2[3 * j + 2] = as[j] * (vc - v);
       }
       // rows of M in order (M1 then M2), each accumulated on its own: the oracle's summation order
-      #pragma unroll
+#pragma unroll
       for (int a = 0; a < 12; ++a)
-        #pragma unroll
-        for (int bb = 0; bb < 12; ++bb) MtM[(a * 12 + bb) * 64] += M1[a] * M1[bb];
-      #pragma unroll
+#pragma unroll
+        for (int bb = 0; bb < 12; ++bb) MtM[(a * 12 + bb) * S] += M1[a] * M1[bb];
+#pragma unroll
       for (int a = 0; a < 12; ++a)
-        #pragma unroll
-        for (int bb = 0; bb < 12; ++bb) MtM[(a * 12 + bb) * 64] += M2[a] * M2[bb];
+#pragma unroll
+        for (int bb = 0; bb < 12; ++bb) MtM[(a * 12 + bb) * S] += M2[a] * M2[bb];
     }
-    dsvd12_null4<64>(MtM, nv);  // U^T rows 8..11 (singular vectors of the 4 smallest singular values)
   }
   // Second half: the three beta approximations + Gauss-Newton, the best (R, t).  Needs pws,
-  // us, alphas and cws from null_space().
+  // us, alphas and cws from build_mtm().
   __device__ void pose_from_null(const double (*nv)[12], double* R, double* t) {
     double L[60], rho[6];
     {
@@ -1224,46 +1232,46 @@ __global__ __launch_bounds__(64) void k_pnp_hyp_a(const float* __restrict__ P3al
                                                   int cap, Cam K, int maxIters, int it_lo,
                                                   const int16_t* __restrict__ table, int table_iters,
                                                   const PnpState* __restrict__ state, double* __restrict__ ws) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];  // [144][64] EPnP MtM (one column per lane)
-  const int b = blockIdx.y;
-  const int it = it_lo + blockIdx.x * 64 + threadIdx.x;
+  __shared__ double su[8][144];  // M^T M of the block's 8 subsets (one 8-lane group each)
+  const int b = blockIdx.y, g = threadIdx.x >> 3, l = threadIdx.x & 7;
+  const int it = it_lo + blockIdx.x * 8 + g;
   const PnpState st = state[b];
   const int n = st.n;
-  if (n < 6 || it_lo + (int)blockIdx.x * 64 >= min(st.niters, maxIters)) return;
-  if (it >= maxIters) return;
-  const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
-  const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
-  const int16_t* sb = table + ((int64_t)n * table_iters + it) * 5;
-  EPnPd<5> e;
-  e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    int j = sb[i];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) e.pws[3 * i + c] = (double)P3[j * 3 + c];
-    double xy[2];
-    dundistort(K, (double)p2[j * 2], (double)p2[j * 2 + 1], xy);
-    float fx = (float)xy[0], fy = (float)xy[1];
-    e.us[2 * i] = fx * K.fx + K.cx;
-    e.us[2 * i + 1] = fy * K.fy + K.cy;
-  }
-  double nv[4][12];
-  e.null_space(smem + threadIdx.x, nv);
+  if (n < 6 || it_lo + (int)blockIdx.x * 8 >= min(st.niters, maxIters)) return;
+  if (it >= maxIters) return;  // the whole group
+  double* u = su[g];
   double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
+  if (l == 0) {
+    const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
+    const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
+    const int16_t* sb = table + ((int64_t)n * table_iters + it) * 5;
+    EPnPd<5> e;
+    e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+    for (int i = 0; i < 5; ++i) {
+      int j = sb[i];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) w[PW_NV + r * 12 + k] = nv[r][k];
+      for (int c = 0; c < 3; ++c) e.pws[3 * i + c] = (double)P3[j * 3 + c];
+      double xy[2];
+      dundistort(K, (double)p2[j * 2], (double)p2[j * 2 + 1], xy);
+      float fx = (float)xy[0], fy = (float)xy[1];
+      e.us[2 * i] = fx * K.fx + K.cx;
+      e.us[2 * i + 1] = fy * K.fy + K.cy;
+    }
+    e.build_mtm<1>(u);
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) w[PW_CWS + r * 3 + k] = e.cws[r][k];
+      for (int k = 0; k < 3; ++k) w[PW_CWS + r * 3 + k] = e.cws[r][k];
 #pragma unroll
-  for (int k = 0; k < 20; ++k) w[PW_AL + k] = e.alphas[k];
+    for (int k = 0; k < 20; ++k) w[PW_AL + k] = e.alphas[k];
 #pragma unroll
-  for (int k = 0; k < 15; ++k) w[PW_PWS + k] = e.pws[k];
+    for (int k = 0; k < 15; ++k) w[PW_PWS + k] = e.pws[k];
 #pragma unroll
-  for (int k = 0; k < 10; ++k) w[PW_US + k] = e.us[k];
+    for (int k = 0; k < 10; ++k) w[PW_US + k] = e.us[k];
+  }
+  __builtin_amdgcn_wave_barrier();
+  jacobi12_null4_group(u, l, w + PW_NV);
 }
 
 __global__ __launch_bounds__(64) void k_pnp_hyp_b(const float* __restrict__ P3all, const float* __restrict__ p2all,
@@ -1456,14 +1464,11 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
   const float thr2 = (float)((double)reproj * reproj);
   const int maxIters = iters;
   PnpState* st = (PnpState*)ctx->pnp_state;
-  const size_t shm = 144 * 64 * sizeof(double);
-  if (shm > 64 * 1024)
-    FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_pnp_hyp_a, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   const int first = std::min(maxIters, 128);
   auto hyp = [&](int lo, int hi) {
     const dim3 grid((hi - lo + 63) / 64, batch);
-    hipLaunchKernelGGL(k_pnp_hyp_a, grid, dim3(64), shm, s, P3, p2, cap, c, maxIters, lo, ctx->rs_table,
-                       ctx->rs_table_iters, st, ctx->pnp_ws);
+    hipLaunchKernelGGL(k_pnp_hyp_a, dim3((hi - lo + 7) / 8, batch), dim3(64), 0, s, P3, p2, cap, c, maxIters, lo,
+                       ctx->rs_table, ctx->rs_table_iters, st, ctx->pnp_ws);
     hipLaunchKernelGGL(k_pnp_hyp_b, grid, dim3(64), 0, s, P3, p2, cap, c, thr2, maxIters, lo, st, ctx->pnp_ws,
                        ctx->pnp_models, ctx->pnp_good);
     hipLaunchKernelGGL(k_pnp_replay, dim3(batch), dim3(64), 0, s, maxIters, lo, hi, conf, ctx->pnp_good, st);
