@@ -824,93 +824,89 @@ struct EPnPd {
         for (int bb = 0; bb < 12; ++bb) MtM[(a * 12 + bb) * S] += M2[a] * M2[bb];
     }
   }
-  // Second half: the three beta approximations + Gauss-Newton, the best (R, t).  Needs pws,
-  // us, alphas and cws from build_mtm().
-  __device__ void pose_from_null(const double (*nv)[12], double* R, double* t) {
-    double L[60], rho[6];
-    {
-      const double* vv[4] = {nv[3], nv[2], nv[1], nv[0]};
-      double dv[4][6][3];
-      for (int i = 0; i < 4; ++i) {
-        int a = 0, bb = 1;
-        for (int j = 0; j < 6; ++j) {
-          for (int k = 0; k < 3; ++k) dv[i][j][k] = vv[i][3 * a + k] - vv[i][3 * bb + k];
-          if (++bb > 3) { ++a; bb = a + 1; }
-        }
-      }
-      for (int i = 0; i < 6; ++i) {
-        double* r = L + 10 * i;
-        r[0] = dot3(dv[0][i], dv[0][i]);
-        r[1] = 2.0f * dot3(dv[0][i], dv[1][i]);
-        r[2] = dot3(dv[1][i], dv[1][i]);
-        r[3] = 2.0f * dot3(dv[0][i], dv[2][i]);
-        r[4] = 2.0f * dot3(dv[1][i], dv[2][i]);
-        r[5] = dot3(dv[2][i], dv[2][i]);
-        r[6] = 2.0f * dot3(dv[0][i], dv[3][i]);
-        r[7] = 2.0f * dot3(dv[1][i], dv[3][i]);
-        r[8] = 2.0f * dot3(dv[2][i], dv[3][i]);
-        r[9] = dot3(dv[3][i], dv[3][i]);
-      }
-      rho[0] = dist2(cws[0], cws[1]); rho[1] = dist2(cws[0], cws[2]); rho[2] = dist2(cws[0], cws[3]);
-      rho[3] = dist2(cws[1], cws[2]); rho[4] = dist2(cws[1], cws[3]); rho[5] = dist2(cws[2], cws[3]);
+  // Second half: L (6x10) and rho from the null space and the control points ...
+  __device__ void prep(const double (*nv)[12], double* L, double* rho) const {
+    const double* vv[4] = {nv[3], nv[2], nv[1], nv[0]};
+    double dv[4][6][3];
+    constexpr int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dv[i][j][k] = vv[i][3 * pa[j] + k] - vv[i][3 * pb[j] + k];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      double* r = L + 10 * i;
+      r[0] = dot3(dv[0][i], dv[0][i]);
+      r[1] = 2.0f * dot3(dv[0][i], dv[1][i]);
+      r[2] = dot3(dv[1][i], dv[1][i]);
+      r[3] = 2.0f * dot3(dv[0][i], dv[2][i]);
+      r[4] = 2.0f * dot3(dv[1][i], dv[2][i]);
+      r[5] = dot3(dv[2][i], dv[2][i]);
+      r[6] = 2.0f * dot3(dv[0][i], dv[3][i]);
+      r[7] = 2.0f * dot3(dv[1][i], dv[3][i]);
+      r[8] = 2.0f * dot3(dv[2][i], dv[3][i]);
+      r[9] = dot3(dv[3][i], dv[3][i]);
     }
-    double best_err = 0, Rb[9], tb[3];
-#pragma nounroll
-    for (int N = 1; N <= 3; ++N) {
-      double betas[4];
-      if (N == 1) {
-        double A[24], b4[4];
-        const int c[4] = {0, 1, 3, 6};
-        for (int i = 0; i < 6; ++i)
-          for (int j = 0; j < 4; ++j) A[i * 4 + j] = L[i * 10 + c[j]];
-        dsolve<6, 4>(A, rho, b4);
-        double s = b4[0] < 0 ? -1.0 : 1.0;
-        betas[0] = sqrt(s * b4[0]);
-        betas[1] = s * b4[1] / betas[0];
-        betas[2] = s * b4[2] / betas[0];
-        betas[3] = s * b4[3] / betas[0];
-      } else if (N == 2) {
-        double A[18], b3[3];
-        for (int i = 0; i < 6; ++i)
-          for (int j = 0; j < 3; ++j) A[i * 3 + j] = L[i * 10 + j];
-        dsolve<6, 3>(A, rho, b3);
-        if (b3[0] < 0) {
-          betas[0] = sqrt(-b3[0]);
-          betas[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
-        } else {
-          betas[0] = sqrt(b3[0]);
-          betas[1] = (b3[2] > 0) ? sqrt(b3[2]) : 0.0;
-        }
-        if (b3[1] < 0) betas[0] = -betas[0];
-        betas[2] = 0.0;
-        betas[3] = 0.0;
+    rho[0] = dist2(cws[0], cws[1]); rho[1] = dist2(cws[0], cws[2]); rho[2] = dist2(cws[0], cws[3]);
+    rho[3] = dist2(cws[1], cws[2]); rho[4] = dist2(cws[1], cws[3]); rho[5] = dist2(cws[2], cws[3]);
+  }
+  // ... and beta approximation N (1..3) + Gauss-Newton -> (R, t) and its reprojection error.
+  // compute_pose keeps approximation 1 and replaces it by a later one with a strictly smaller
+  // error (the caller does that selection).
+  __device__ double approx(int N, const double* L, const double* rho, const double (*nv)[12], double* R, double* t) {
+    double betas[4];
+    if (N == 1) {
+      double A[24], b4[4];
+      constexpr int c[4] = {0, 1, 3, 6};
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) A[i * 4 + j] = L[i * 10 + c[j]];
+      dsolve<6, 4>(A, rho, b4);
+      double s = b4[0] < 0 ? -1.0 : 1.0;
+      betas[0] = sqrt(s * b4[0]);
+      betas[1] = s * b4[1] / betas[0];
+      betas[2] = s * b4[2] / betas[0];
+      betas[3] = s * b4[3] / betas[0];
+    } else if (N == 2) {
+      double A[18], b3[3];
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) A[i * 3 + j] = L[i * 10 + j];
+      dsolve<6, 3>(A, rho, b3);
+      if (b3[0] < 0) {
+        betas[0] = sqrt(-b3[0]);
+        betas[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
       } else {
-        double A[30], b5[5];
-        for (int i = 0; i < 6; ++i)
-          for (int j = 0; j < 5; ++j) A[i * 5 + j] = L[i * 10 + j];
-        dsolve<6, 5>(A, rho, b5);
-        if (b5[0] < 0) {
-          betas[0] = sqrt(-b5[0]);
-          betas[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
-        } else {
-          betas[0] = sqrt(b5[0]);
-          betas[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0;
-        }
-        if (b5[1] < 0) betas[0] = -betas[0];
-        betas[2] = b5[3] / betas[0];
-        betas[3] = 0.0;
+        betas[0] = sqrt(b3[0]);
+        betas[1] = (b3[2] > 0) ? sqrt(b3[2]) : 0.0;
       }
-      gauss_newton(L, rho, betas);
-      double Rn[9], tn[3];
-      double e = compute_R_and_t(nv, betas, Rn, tn);
-      if (N == 1 || e < best_err) {
-        best_err = e;
-        for (int i = 0; i < 9; ++i) Rb[i] = Rn[i];
-        for (int i = 0; i < 3; ++i) tb[i] = tn[i];
+      if (b3[1] < 0) betas[0] = -betas[0];
+      betas[2] = 0.0;
+      betas[3] = 0.0;
+    } else {
+      double A[30], b5[5];
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) A[i * 5 + j] = L[i * 10 + j];
+      dsolve<6, 5>(A, rho, b5);
+      if (b5[0] < 0) {
+        betas[0] = sqrt(-b5[0]);
+        betas[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
+      } else {
+        betas[0] = sqrt(b5[0]);
+        betas[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0;
       }
+      if (b5[1] < 0) betas[0] = -betas[0];
+      betas[2] = b5[3] / betas[0];
+      betas[3] = 0.0;
     }
-    for (int i = 0; i < 9; ++i) R[i] = Rb[i];
-    for (int i = 0; i < 3; ++i) t[i] = tb[i];
+    gauss_newton(L, rho, betas);
+    return compute_R_and_t(nv, betas, R, t);
   }
 };
 
@@ -1278,14 +1274,16 @@ __global__ __launch_bounds__(64) void k_pnp_hyp_b(const float* __restrict__ P3al
                                                   int cap, Cam K, float thr2, int maxIters, int it_lo,
                                                   const PnpState* __restrict__ state, const double* __restrict__ ws,
                                                   double* __restrict__ model, int32_t* __restrict__ good) {
-  const int b = blockIdx.y;
-  const int it = it_lo + blockIdx.x * 64 + threadIdx.x;
+  // a 4-lane group per subset: lanes 0..2 run the three beta approximations side by side (the
+  // serial loop's selection -- approximation 1, replaced by a later one only on a strictly
+  // smaller error -- is applied to their results in order), then all four lanes score the
+  // model over a quarter of the points each
+  const int b = blockIdx.y, g = threadIdx.x >> 2, l = threadIdx.x & 3;
+  const int it = it_lo + blockIdx.x * 16 + g;
   const PnpState st = state[b];
   const int n = st.n;
-  if (n < 6 || it_lo + (int)blockIdx.x * 64 >= min(st.niters, maxIters)) return;
-  if (it >= maxIters) return;
-  // points are read from global memory: the scoring loop's addresses are wave-uniform
-  // (scalar loads)
+  if (n < 6 || it_lo + (int)blockIdx.x * 16 >= min(st.niters, maxIters)) return;
+  if (it >= maxIters) return;  // the whole group
   const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
   const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
   const double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
@@ -1306,25 +1304,41 @@ __global__ __launch_bounds__(64) void k_pnp_hyp_b(const float* __restrict__ P3al
   for (int k = 0; k < 15; ++k) e.pws[k] = w[PW_PWS + k];
 #pragma unroll
   for (int k = 0; k < 10; ++k) e.us[k] = w[PW_US + k];
-  double R[9], t[3], r[3], dR[27];
-  e.pose_from_null(nv, R, t);
+  double R[9], t[3], err = 0.0;
+  {
+    double L[60], rho[6];
+    e.prep(nv, L, rho);
+    err = e.approx(l < 3 ? l + 1 : 3, L, rho, nv, R, t);
+  }
+  const int base = threadIdx.x & ~3;
+  const double e1 = __shfl(err, base + 1, 64), e2 = __shfl(err, base + 2, 64);
+  int sel = 0;
+  double best = __shfl(err, base, 64);
+  if (e1 < best) { best = e1; sel = 1; }
+  if (e2 < best) sel = 2;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) R[k] = __shfl(R[k], base + sel, 64);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) t[k] = __shfl(t[k], base + sel, 64);
+  double r[3], dR[27];
   rod_R2r(R, r);
-  double* mo = model + ((int64_t)b * maxIters + it) * 6;
-  for (int i = 0; i < 3; ++i) { mo[i] = r[i]; mo[3 + i] = t[i]; }
+  if (l == 0) {
+    double* mo = model + ((int64_t)b * maxIters + it) * 6;
+    for (int i = 0; i < 3; ++i) { mo[i] = r[i]; mo[3 + i] = t[i]; }
+  }
   rod_r2R(r, R, dR);
-  int g = 0;
-  for (int i = 0; i < n; ++i) {
+  int gcount = 0;
+  for (int i = l; i < n; i += 4) {
     double M[3] = {(double)P3[3 * i], (double)P3[3 * i + 1], (double)P3[3 * i + 2]}, uv[2];
     dproject(K, R, dR, t, M, uv, nullptr);
     float du = p2[2 * i] - (float)uv[0], dv = p2[2 * i + 1] - (float)uv[1];
-    g += (du * du + dv * dv) <= thr2;
+    gcount += (du * du + dv * dv) <= thr2;
   }
-  good[(int64_t)b * maxIters + it] = g;
+  gcount += __shfl_xor(gcount, 1, 4);
+  gcount += __shfl_xor(gcount, 2, 4);
+  if (l == 0) good[(int64_t)b * maxIters + it] = gcount;
 }
 
-// RANSACPointSetRegistrator::run's acceptance loop replayed in iteration order over
-// [it_lo, it_hi): accept iff goodCount > max(maxGoodCount, 4); niters is updated with
-// RANSACUpdateNumIters(confidence, (n - good)/n, 5, niters) and bounds the loop.
 // One wave per frame: 64 iterations' counts loaded at once, then walked in order with
 // wave-uniform reads (a lane per frame walking global memory was 73 us per launch).
 __global__ __launch_bounds__(64) void k_pnp_replay(int maxIters, int it_lo, int it_hi, double conf,
@@ -1466,11 +1480,10 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
   PnpState* st = (PnpState*)ctx->pnp_state;
   const int first = std::min(maxIters, 128);
   auto hyp = [&](int lo, int hi) {
-    const dim3 grid((hi - lo + 63) / 64, batch);
     hipLaunchKernelGGL(k_pnp_hyp_a, dim3((hi - lo + 7) / 8, batch), dim3(64), 0, s, P3, p2, cap, c, maxIters, lo,
                        ctx->rs_table, ctx->rs_table_iters, st, ctx->pnp_ws);
-    hipLaunchKernelGGL(k_pnp_hyp_b, grid, dim3(64), 0, s, P3, p2, cap, c, thr2, maxIters, lo, st, ctx->pnp_ws,
-                       ctx->pnp_models, ctx->pnp_good);
+    hipLaunchKernelGGL(k_pnp_hyp_b, dim3((hi - lo + 15) / 16, batch), dim3(64), 0, s, P3, p2, cap, c, thr2, maxIters,
+                       lo, st, ctx->pnp_ws, ctx->pnp_models, ctx->pnp_good);
     hipLaunchKernelGGL(k_pnp_replay, dim3(batch), dim3(64), 0, s, maxIters, lo, hi, conf, ctx->pnp_good, st);
   };
   FVO_TIMED(ctx, KN_PNP, s, {
