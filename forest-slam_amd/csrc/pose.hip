@@ -253,68 +253,6 @@ __device__ void dsvd_ws(const double* A, double* W, double* U, double* V, double
   }
 }
 
-// Right singular vector of the smallest singular value of the symmetric 12x12 DLT matrix
-// (packed upper triangle LLp, identical on every lane) -- column 11 of dsvd_ws<12,12>'s V --
-// by the same cyclic one-sided Jacobi, parallel over rows: lane i < 12 holds row i of the
-// working matrix and of V, the three column dot products of a rotation are 16-lane sums.
-// Only the summation order of those dot products differs from the serial dsvd_ws.
-// Returns the vector on every lane.
-__device__ void dlt12_null(const double* LLp, double* out) {
-  const int lane = threadIdx.x & 63, i = lane & 15;
-  const bool act = i < 12;
-  double u[12], v[12];
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    u[j] = 0.0;
-    v[j] = (act && j == i) ? 1.0 : 0.0;
-  }
-  // row i of the symmetric matrix from the packed upper triangle (compile-time indices only)
-#pragma unroll
-  for (int a = 0, k = 0; a < 12; ++a)
-#pragma unroll
-    for (int b = a; b < 12; ++b, ++k) {
-      if (i == a) u[b] = LLp[k];
-      if (i == b) u[a] = LLp[k];
-    }
-  auto red = [](double x) {
-#pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) x += __shfl_xor(x, o, 16);
-    return x;
-  };
-  for (int sweep = 0; sweep < 60; ++sweep) {
-    double off = 0.0;
-#pragma unroll
-    for (int p = 0; p < 11; ++p)
-#pragma unroll
-      for (int q = p + 1; q < 12; ++q) {
-        const double a = red(u[p] * u[p]), bb = red(u[q] * u[q]), g = red(u[p] * u[q]);
-        if (g == 0.0 || fabs(g) <= 1e-300) continue;
-        const double rel = fabs(g) / sqrt(a * bb);
-        off = fmax(off, rel);
-        if (rel < 1e-15) continue;
-        const double zeta = (bb - a) / (2.0 * g);
-        const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-        const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
-        const double up = u[p], uq = u[q], vp = v[p], vq = v[q];
-        u[p] = c * up - sn * uq;
-        u[q] = sn * up + c * uq;
-        v[p] = c * vp - sn * vq;
-        v[q] = sn * vp + c * vq;
-      }
-    if (off < 1e-15) break;
-  }
-  // the smallest column norm, the last one in dsvd_ws's stable descending order
-  double wmin = 0.0, vm = 0.0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    const double w = sqrt(red(u[j] * u[j]));
-    if (j == 0 || w <= wmin) { wmin = w; vm = v[j]; }
-  }
-  const int base = lane & ~15;
-#pragma unroll
-  for (int k = 0; k < 12; ++k) out[k] = __shfl(vm, base + k, 64);
-}
-
 // SPD 6x6 solve by Cholesky for the LM step (JtJ with the (1 + lambda) diagonal).  Returns
 // false when a pivot is not clearly positive (pivot^2 below 1e-12 of the largest diagonal
 // entry): the caller then takes OpenCV's DECOMP_SVD path (dsolve), which also handles the
@@ -518,7 +456,10 @@ __device__ void dundistort(const Cam& K, double u, double v, double* xy) {
 // sits between), and the pairs of one anti-diagonal share no column, so the group rotates
 // them at once -- bit-identical to the serial sweep, with 21 dependent steps instead of 66.
 // The column norms, the sort and the output (out[r * 12 + i], r = 0..3) are lane 0's.
-__device__ __forceinline__ void jacobi12_null4_group(double* __restrict__ u, int l, double* __restrict__ out) {
+// The sweeps of dsvd<12,12> (cyclic one-sided Jacobi on u, and on v when V is wanted) by an
+// 8-lane group on row-major [144] arrays in LDS.
+template <bool WITH_V>
+__device__ __forceinline__ void jacobi12_sweeps_group(double* __restrict__ u, double* __restrict__ v, int l) {
   for (int sweep = 0; sweep < 60; ++sweep) {
     double off = 0.0;
 #pragma nounroll
@@ -548,6 +489,13 @@ __device__ __forceinline__ void jacobi12_null4_group(double* __restrict__ u, int
               u[i * 12 + p] = c * up - sn * uq;
               u[i * 12 + q] = sn * up + c * uq;
             }
+            if (WITH_V)
+#pragma unroll
+              for (int i = 0; i < 12; ++i) {
+                const double vp = v[i * 12 + p], vq = v[i * 12 + q];
+                v[i * 12 + p] = c * vp - sn * vq;
+                v[i * 12 + q] = sn * vp + c * vq;
+              }
           }
         }
       }
@@ -557,6 +505,10 @@ __device__ __forceinline__ void jacobi12_null4_group(double* __restrict__ u, int
     for (int o = 1; o < 8; o <<= 1) off = fmax(off, __shfl_xor(off, o, 8));
     if (off < 1e-15) break;
   }
+}
+
+__device__ __forceinline__ void jacobi12_null4_group(double* __restrict__ u, int l, double* __restrict__ out) {
+  jacobi12_sweeps_group<false>(u, nullptr, l);
   if (l != 0) return;
   double w[12];
 #pragma unroll
@@ -577,6 +529,43 @@ __device__ __forceinline__ void jacobi12_null4_group(double* __restrict__ u, int
 #pragma unroll
     for (int i = 0; i < 12; ++i) out[r * 12 + i] = u[i * 12 + j] * inv;  // u is in LDS: index it directly
   }
+}
+
+// Right singular vector of the smallest singular value of the symmetric 12x12 DLT matrix
+// (packed upper triangle LLp, identical on every lane) -- column 11 of dsvd_ws<12,12>'s V,
+// with dsvd_ws's exact arithmetic -- by lanes 0..7 of the wave on LDS work arrays u, v [144].
+// Returns the vector on every lane.
+__device__ void dlt12_null(const double* LLp, double* __restrict__ u, double* __restrict__ v, double* out) {
+  const int lane = threadIdx.x & 63;
+  for (int k = lane; k < 144; k += 64) v[k] = (k % 13 == 0) ? 1.0 : 0.0;
+  if (lane < 12) {
+#pragma unroll
+    for (int a = 0, k = 0; a < 12; ++a)
+#pragma unroll
+      for (int b = a; b < 12; ++b, ++k) {
+        if (lane == a) u[a * 12 + b] = LLp[k];
+        if (lane == b) u[b * 12 + a] = LLp[k];  // each lane writes its row of the symmetric matrix
+      }
+  }
+  __syncthreads();
+  if (lane < 8) jacobi12_sweeps_group<true>(u, v, lane);
+  __syncthreads();
+  // the smallest column norm, the last one in dsvd_ws's stable descending order
+  double w[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) s += u[i * 12 + j] * u[i * 12 + j];
+    w[j] = sqrt(s);
+  }
+  double sw[12];
+  int ord[12];
+  sort_desc<12>(w, sw, ord);
+  const int j = ord[11];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) out[i] = v[i * 12 + j];
+  __syncthreads();
 }
 
 // ------------------------------------------------------------------ EPnP (5 points)
@@ -1019,7 +1008,7 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
   for (int k = 0; k < 78; ++k) LLp[k] = wsum_d(LLp[k]);
   double param[6] = {0, 0, 0, 0, 0, 0};
   double RRt[12];
-  if (!planar) dlt12_null(LLp, RRt);  // the whole wave
+  if (!planar) dlt12_null(LLp, sh.dlt[1], sh.dlt[2], RRt);  // the whole wave
   if (lane == 0) {
     double R[9];
     if (!planar) {
