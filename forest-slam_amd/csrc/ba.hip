@@ -687,21 +687,35 @@ __global__ __launch_bounds__(kBlock) void k_ba_solve(void* ws, BaDims dm) {
   }
   for (int i = tid; i < np; i += kBlock) sS[i * np + i] = sdiag[i];
   __syncthreads();
-  if (wid == 0) {  // L y = rhs, L^T x = y (wave 0)
-    for (int i = 0; i < np; ++i) {
-      double p = 0;
-      for (int j = lane; j < i; j += 64) p += sS[i * np + j] * rhs[j];
-      p = wave_sum(p);
-      if (lane == 0) rhs[i] = (rhs[i] - p) / sS[i * np + i];
-      __builtin_amdgcn_wave_barrier();
+  if (wid == 0) {
+    // L y = rhs, then L^T x = y, column-oriented on wave 0: lane owns rows lane and lane + 64
+    // (np <= 120); each step divides the finished row's value by its pivot (every lane, same
+    // arithmetic), broadcasts it with a wave-uniform read, and every remaining row subtracts
+    // its term -- one dependent step per row instead of a wave reduction per row.
+    auto bcast = [](double v, int src) {
+      const long long b = __double_as_longlong(v);
+      const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), src);
+      const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+      return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+    };
+    const int r0 = lane, r1 = lane + 64;
+    double x0 = r0 < np ? rhs[r0] : 0.0, x1 = r1 < np ? rhs[r1] : 0.0;
+    for (int j = 0; j < np; ++j) {
+      const double yj = bcast(j < 64 ? x0 : x1, j & 63) / sS[j * np + j];
+      if (r0 == j) x0 = yj;
+      if (r1 == j) x1 = yj;
+      if (r0 > j && r0 < np) x0 -= sS[r0 * np + j] * yj;
+      if (r1 > j && r1 < np) x1 -= sS[r1 * np + j] * yj;
     }
-    for (int i = np - 1; i >= 0; --i) {
-      double p = 0;
-      for (int j = i + 1 + lane; j < np; j += 64) p += sS[j * np + i] * rhs[j];
-      p = wave_sum(p);
-      if (lane == 0) rhs[i] = (rhs[i] - p) / sS[i * np + i];
-      __builtin_amdgcn_wave_barrier();
+    for (int j = np - 1; j >= 0; --j) {
+      const double xj = bcast(j < 64 ? x0 : x1, j & 63) / sS[j * np + j];
+      if (r0 == j) x0 = xj;
+      if (r1 == j) x1 = xj;
+      if (r0 < j) x0 -= sS[j * np + r0] * xj;
+      if (r1 < j) x1 -= sS[j * np + r1] * xj;
     }
+    if (r0 < np) rhs[r0] = x0;
+    if (r1 < np) rhs[r1] = x1;
   }
   __syncthreads();
   for (int a = tid; a < 6 * n; a += kBlock) S->dp[a] = a < 6 ? 0.0 : rhs[a - 6];
