@@ -362,6 +362,12 @@ __device__ __forceinline__ uint32_t rdpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
 }
 
+// Ring sizes of the row pass's LDS windows (powers of two): keys cover x2 over 2D + 4 SEG
+// columns, raw disparities wait D + 2 SEG columns for their check.
+__host__ __device__ constexpr int sg_pow2(int n) { return n <= 1 ? 1 : 2 * sg_pow2((n + 1) / 2); }
+__host__ __device__ constexpr int sg_ring_keys(int D) { return sg_pow2(2 * D + 32); }
+__host__ __device__ constexpr int sg_ring_raw(int D) { return sg_pow2(D + 16); }
+
 // One path step of a 16-lane row (PQ packed words per lane); returns the row minimum.
 template <int PQ>
 __device__ __forceinline__ uint32_t step16(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
@@ -407,19 +413,42 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
   constexpr int DQ = D / 16, PQ = DQ / 2, SEG = 8, PF = 16;
   constexpr int CKW = PQ + 1 <= 4 ? 4 : 8;
   constexpr int XS = 2 * D;  // u32 words per column of a 4-row group
-  extern __shared__ uint32_t smem[];
+  constexpr int RK = sg_ring_keys(D), RS = sg_ring_raw(D);
+  __shared__ uint32_t s_key[4][RK];  // right-view keys of the live x2 window (ring, by x2)
+  __shared__ int16_t s_raw[4][RS];   // raw disparities awaiting their check (ring, by x1)
   const int lane = threadIdx.x, q = lane & 15, r = lane >> 4;
   const int y = blockIdx.x * 4 + r, b = blockIdx.y;
   const int H = p.H, W = p.W, W1 = p.width1;
   const bool rowok = y < H;
   const int yy = min(y, H - 1);  // rows past H walk the last row's volumes (never output)
-  uint32_t* key = smem + r * W;
-  int16_t* sraw = reinterpret_cast<int16_t*>(smem + 4 * W) + r * W;
+  uint32_t* key = s_key[r];
+  int16_t* sraw = s_raw[r];
   const int INVALID = (p.minD - 1) * 16;
-  for (int x = q; x < W; x += 16) {
-    key[x] = 0xFFFFFFFFu;
-    sraw[x] = (int16_t)INVALID;
-  }
+  for (int k = q; k < RK; k += 16) key[k] = 0xFFFFFFFFu;
+  int16_t* out = raw + ((int64_t)b * H + yy) * W;
+  if (rowok)  // columns left of the first x1 (and right of the last) never get a disparity
+    for (int x = q; x < W; x += 16)
+      if (x < p.minX1 || x >= p.minX1 + W1) out[x] = (int16_t)INVALID;
+  // pseudo left-right check of pixel x1 (its right-view keys are final once the sweep has
+  // passed x1 - D: every x2 it reads lies within D of x1 + minX1 - minD)
+  auto disp2 = [&](int x2) -> int {
+    const uint32_t kv = key[x2 & (RK - 1)];
+    return kv == 0xFFFFFFFFu ? INVALID : (int)(0xFFFFu - (kv & 0xFFFFu)) + p.minX1 - x2;
+  };
+  auto check = [&](int x1) {
+    const int x = x1 + p.minX1;
+    int d1 = sraw[x1 & (RS - 1)];
+    if (d1 != INVALID) {
+      const int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
+      const int _x = x - _d, x_ = x - d_;
+      if (0 <= x_ && x_ < W && 0 <= _x && _x < W) {
+        const int a = disp2(x_), cc = disp2(_x);
+        if (a >= p.minD && abs(a - d_) > p.disp12 && cc >= p.minD && abs(cc - _d) > p.disp12) d1 = INVALID;
+      }
+    }
+    if (rowok) out[x] = (int16_t)d1;
+  };
+  int next_chk = W1 - 1;  // highest pixel not yet checked
   const int64_t rowofs = (((int64_t)b * p.HG4 + (yy >> 2)) * W1 * (4 * D) + (yy & 3) * D + q * DQ) / 2;
   const uint32_t* Cr = reinterpret_cast<const uint32_t*>(Cvol) + rowofs;
   const uint32_t* Vr = reinterpret_cast<const uint32_t*>(Vvol) + rowofs;
@@ -556,9 +585,12 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
         nb |= rdpp<kRMirror>(nb);
         if (q == 0) {
           const int sm1 = (int)(nb >> 16), sp1 = (int)(nb & 0xFFFFu);
+          // the lowest x2 this column can reach enters the key window: reset its ring slot
+          // (it last held x2 + RK, whose readers were all checked RK - 2D columns ago)
+          key[(x1 + p.minX1 - p.minD - (D - 1)) & (RK - 1)] = 0xFFFFFFFFu;
           const int x2 = x1 + p.minX1 - d - p.minD;
           if (x2 >= 0 && x2 < W && best < 0x7FFF)  // disp2cost starts at SHRT_MAX
-            atomicMin(&key[x2], ((uint32_t)best << 16) | (uint32_t)(0xFFFF - x1));
+            atomicMin(&key[x2 & (RK - 1)], ((uint32_t)best << 16) | (uint32_t)(0xFFFF - x1));
           int dd;
           if (0 < d && d < D - 1) {
             const int denom2 = max(sm1 + sp1 - 2 * best, 1);
@@ -566,31 +598,19 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
           } else {
             dd = d * 16;
           }
-          sraw[x1 + p.minX1] = (int16_t)(dd + p.minD * 16);
+          sraw[x1 & (RS - 1)] = (int16_t)(dd + p.minD * 16);
         }
       }
-    }
-  }
-  __syncthreads();  // one wave: orders the LDS atomics / raw stores before the check below
-  if (!rowok) return;
-  // ---- pseudo left-right consistency check on the LDS row, then the row-major raw row
-  auto disp2 = [&](int x2) -> int {
-    const uint32_t kv = key[x2];
-    return kv == 0xFFFFFFFFu ? INVALID : (int)(0xFFFFu - (kv & 0xFFFFu)) + p.minX1 - x2;
-  };
-  int16_t* out = raw + ((int64_t)b * H + y) * W;
-  for (int x = q; x < W; x += 16) {
-    int d1 = sraw[x];
-    if (d1 != INVALID && x >= p.minX1 && x < p.minX1 + W1) {
-      const int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
-      const int _x = x - _d, x_ = x - d_;
-      if (0 <= x_ && x_ < W && 0 <= _x && _x < W) {
-        const int a = disp2(x_), cc = disp2(_x);
-        if (a >= p.minD && abs(a - d_) > p.disp12 && cc >= p.minD && abs(cc - _d) > p.disp12) d1 = INVALID;
+      // pixels whose keys became final with this segment (at most SEG): one lane each
+      const int x1_lo = W1 - 1 - (SEG * sg + ihi);
+      if (ihi >= 0) {
+        const int cnt = min(next_chk - (x1_lo + D) + 1, SEG);
+        if (q < cnt) check(next_chk - q);
+        if (cnt > 0) next_chk -= cnt;
       }
     }
-    out[x] = (int16_t)d1;
   }
+  for (int x1 = next_chk - q; x1 >= 0; x1 -= 16) check(x1);  // the last D (+ < SEG) pixels
 }
 
 // ------------------------------------------------------------------ median 3x3
@@ -663,8 +683,7 @@ void launch_chunk(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8
     else if (cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 4>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, C, V);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 64, 4>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, C, V);
   });
-  const size_t lds = (size_t)4 * p.W * (sizeof(uint32_t) + sizeof(int16_t));
-  FVO_TIMED(ctx, KN_SG_ROWS, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_rows<D>), dim3(sg_nblk(p), nb), dim3(64), lds, s,
+  FVO_TIMED(ctx, KN_SG_ROWS, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_rows<D>), dim3(sg_nblk(p), nb), dim3(64), 0, s,
                                                    C, V, p, ck, sg_nck(p), raw));
   FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.W + 255) / 256, p.H, nb), dim3(256), 0, s,
                                                      raw, disp, p.W, p.H));
@@ -716,7 +735,6 @@ int sgbm_init(fvo_ctx* ctx) {
   if ((rc = fvo_alloc(ctx, &ctx->sg_C, B * vol)) || (rc = fvo_alloc(ctx, &ctx->sg_V, B * vol)) ||
       (rc = fvo_alloc(ctx, &ctx->sg_ckpt, B * ckp)) || (rc = fvo_alloc(ctx, &ctx->sg_raw, B * p.H * p.W)))
     return rc;
-  if ((size_t)4 * p.W * 6 > 160 * 1024) return fvo_fail(ctx, "SGBM: image too wide for the row kernel's LDS rows");
   FVO_HIP(ctx, hipStreamCreateWithFlags(&ctx->sg_s2, hipStreamNonBlocking));
   FVO_HIP(ctx, hipEventCreateWithFlags(&ctx->sg_fork, hipEventDisableTiming));
   FVO_HIP(ctx, hipEventCreateWithFlags(&ctx->sg_join, hipEventDisableTiming));
