@@ -507,21 +507,20 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
   uint32_t minR = 0;
 #pragma unroll
   for (int k = 0; k < PQ; ++k) Rst[k] = 0;
-  uint32_t Cs[2][SEG][PQ], Vs[2][SEG][PQ];
-  auto ldseg = [&](int sg, uint32_t (*cs)[PQ], uint32_t (*vs)[PQ]) {
+  // C double-buffered one segment ahead (the L recompute needs it first); V loaded at the
+  // segment start, used only after the L recompute (fewer VGPRs: more waves per SIMD)
+  uint32_t Cs[2][SEG][PQ], Vs[SEG][PQ];
+  auto ldseg = [&](const uint32_t* base, int sg, uint32_t (*cs)[PQ]) {
 #pragma unroll
-    for (int i = 0; i < SEG; ++i) {
-      const int x1 = max(W1 - 1 - (SEG * sg + i), 0);
-      ld(Cr, x1, cs[i]);
-      ld(Vr, x1, vs[i]);
-    }
+    for (int i = 0; i < SEG; ++i) ld(base, max(W1 - 1 - (SEG * sg + i), 0), cs[i]);
   };
-  ldseg(0, Cs[0], Vs[0]);
+  ldseg(Cr, 0, Cs[0]);
   for (int s0 = 0; s0 < nseg; s0 += 2) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int sg = s0 + h;  // may be nseg (an empty segment: every step below is skipped)
-      ldseg(sg + 1, Cs[h ^ 1], Vs[h ^ 1]);
+      ldseg(Vr, sg, Vs);
+      ldseg(Cr, sg + 1, Cs[h ^ 1]);
       const int ihi = min(SEG - 1, W1 - 1 - SEG * sg);  // valid i: x' < W1
       // L over the segment (i descending = real x ascending) from the checkpoint at the real
       // column left of it, x' = SEG*(sg+1); zero state when the segment starts at x = 0
@@ -556,7 +555,7 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
         uint32_t kmin = 0xFFFFFFFFu;
 #pragma unroll
         for (int kk = 0; kk < PQ; ++kk) {
-          Sw[kk] = as_u(as_v(Ls[i][kk]) + as_v(Rst[kk]) + as_v(Vs[h][i][kk]));
+          Sw[kk] = as_u(as_v(Ls[i][kk]) + as_v(Rst[kk]) + as_v(Vs[i][kk]));
           const uint32_t d0 = (uint32_t)(q * DQ + 2 * kk);
           kmin = min(kmin, ((Sw[kk] & 0xFFFFu) << 7) | d0);
           kmin = min(kmin, ((Sw[kk] >> 16) << 7) | (d0 + 1));
