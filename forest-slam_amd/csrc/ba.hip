@@ -600,7 +600,6 @@ __global__ __launch_bounds__(kBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm,
 // reduced camera system, Cholesky, pose step and tentative poses
 __global__ __launch_bounds__(kBlock) void k_ba_solve(void* ws, BaDims dm) {
   extern __shared__ double sS[];  // [np*np] + rhs[np]
-  __shared__ int s_fail;
   const BaWin v = view(ws, dm, blockIdx.x);
   BaState* S = v.st;
   if (!S->active) return;
@@ -639,54 +638,80 @@ __global__ __launch_bounds__(kBlock) void k_ba_solve(void* ws, BaDims dm) {
     for (int c = 0; c < nch; ++c) gs += gp[(int64_t)c * NR * NR];
     rhs[a] = -S->Hpp[a / 6 + 1][21 + a % 6] + gs;
   }
-  double* sdiag = rhs + np;  // sqrt of the pivots
-  if (tid == 0) s_fail = 0;
   __syncthreads();
-  // Right-looking Cholesky, one barrier per column: phase k applies column k to the trailing
-  // matrix and finishes column k+1 at the same time -- every thread that owns an element
-  // (i, k+1) recomputes the updated pivot d = S[k+1][k+1] - S[k+1][k]^2 itself (identical
-  // arithmetic in every thread), so the pivot's square root and the column scaling need no
-  // extra barrier.  The pivot entries themselves stay untouched (sdiag holds the roots).
-  if (tid == 0) {
-    const double d = sS[0];
-    if (!(d > 0.0)) s_fail = 1;
-    sdiag[0] = sqrt(d);
-  }
-  __syncthreads();
-  if (s_fail) {
-    if (tid == 0) S->fail = 1;
-    return;
-  }
-  for (int i = 1 + tid; i < np; i += kBlock) sS[i * np] /= sdiag[0];
-  __syncthreads();
-  for (int k = 0; k + 1 < np; ++k) {
-    const int k1 = k + 1;
-    const double lk1 = sS[k1 * np + k];
-    const double dk1 = sS[k1 * np + k1] - lk1 * lk1;
-    const double rk1 = sqrt(dk1);
-    if (tid == 0) {
-      if (!(dk1 > 0.0)) s_fail = 1;
-      sdiag[k1] = rk1;
+  // Right-looking Cholesky by panels of kChol columns, two barriers per panel: (A) every
+  // thread factors the panel's diagonal block itself (identical arithmetic everywhere, so
+  // the pivots need no broadcast), (B) one thread per row below solves the row's panel
+  // entries, (C) the 16 x 16 thread grid applies the panel to the trailing matrix.  Every
+  // element sees exactly the column-by-column algorithm's operations in the same order
+  // (updates S -= L_ic L_jc for c ascending, then the division by the pivot), so the factor
+  // is bit-identical to it; only the barrier count drops (np -> 2 np / kChol).
+  constexpr int kChol = 4;
+  bool fail = false;
+  for (int k = 0; k < np; k += kChol) {
+    const int pw = min(kChol, np - k);
+    double Lb[kChol][kChol];
+#pragma unroll
+    for (int a2 = 0; a2 < kChol; ++a2) {
+      if (a2 < pw) {
+        double d = sS[(k + a2) * np + k + a2];
+#pragma unroll
+        for (int c = 0; c < kChol; ++c)
+          if (c < a2) d -= Lb[a2][c] * Lb[a2][c];
+        if (!(d > 0.0)) fail = true;
+        Lb[a2][a2] = sqrt(d);
+#pragma unroll
+        for (int b2 = 0; b2 < kChol; ++b2) {
+          if (b2 > a2 && b2 < pw) {
+            double v2 = sS[(k + b2) * np + k + a2];
+#pragma unroll
+            for (int c = 0; c < kChol; ++c)
+              if (c < a2) v2 -= Lb[b2][c] * Lb[a2][c];
+            Lb[b2][a2] = v2 / Lb[a2][a2];
+          }
+        }
+      }
     }
-    for (int i = k1 + ta; i < np; i += 16) {
-      const double lik = sS[i * np + k];
-      for (int j = k1 + tb; j <= i; j += 16) {
-        if (j == k1) {
-          if (i > k1) sS[i * np + k1] = (sS[i * np + k1] - lik * lk1) / rk1;
-        } else {
-          sS[i * np + j] -= lik * sS[j * np + k];
+    if (fail) break;  // uniform: every thread computed the same pivots
+    for (int i = k + pw + tid; i < np; i += kBlock) {
+      double x[kChol];
+#pragma unroll
+      for (int a2 = 0; a2 < kChol; ++a2) {
+        if (a2 < pw) {
+          double v2 = sS[i * np + k + a2];
+#pragma unroll
+          for (int c = 0; c < kChol; ++c)
+            if (c < a2) v2 -= x[c] * Lb[a2][c];
+          x[a2] = v2 / Lb[a2][a2];
+          sS[i * np + k + a2] = x[a2];
         }
       }
     }
     __syncthreads();
-    if (s_fail) break;
+    for (int i = k + pw + ta; i < np; i += 16) {
+      double li[kChol];
+#pragma unroll
+      for (int a2 = 0; a2 < kChol; ++a2) li[a2] = a2 < pw ? sS[i * np + k + a2] : 0.0;
+      for (int j = k + pw + tb; j <= i; j += 16) {
+        double v2 = sS[i * np + j];
+#pragma unroll
+        for (int a2 = 0; a2 < kChol; ++a2)
+          if (a2 < pw) v2 -= li[a2] * sS[j * np + k + a2];
+        sS[i * np + j] = v2;
+      }
+    }
+    if (tid == 0)  // the diagonal block's factor (no thread reads these rows in this phase)
+#pragma unroll
+      for (int a2 = 0; a2 < kChol; ++a2)
+#pragma unroll
+        for (int b2 = 0; b2 < kChol; ++b2)
+          if (a2 < pw && b2 >= a2 && b2 < pw) sS[(k + b2) * np + k + a2] = Lb[b2][a2];
+    __syncthreads();
   }
-  if (s_fail) {
+  if (fail) {
     if (tid == 0) S->fail = 1;
     return;
   }
-  for (int i = tid; i < np; i += kBlock) sS[i * np + i] = sdiag[i];
-  __syncthreads();
   if (wid == 0) {
     // L y = rhs, then L^T x = y, column-oriented on wave 0: lane owns rows lane and lane + 64
     // (np <= 120); each step divides the finished row's value by its pivot (every lane, same
