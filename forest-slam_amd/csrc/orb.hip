@@ -64,13 +64,28 @@ __global__ void k_copy_level0(const uint8_t* __restrict__ img, int64_t stride, i
   pyr[b * total + (int64_t)y * W + x] = img[b * stride + (int64_t)y * pitch + x];
 }
 
+// 16 pixels per thread when rows, strides and both bases are 16-byte aligned (the usual
+// contiguous [B][H][W] batch with W % 16 == 0; the pyramid's per-image size is padded to 256)
+__global__ void k_copy_level0_v(const uint4* __restrict__ img, int64_t stride16, int pitch16,
+                                uint4* __restrict__ pyr, int64_t total16, int W16, int H, int batch) {
+  const int64_t n = (int64_t)batch * H * W16;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / W16;
+    const int x = (int)(i - row * W16);
+    const int b = (int)(row / H), y = (int)(row - (int64_t)b * H);
+    pyr[b * total16 + (int64_t)y * W16 + x] = img[b * stride16 + (int64_t)y * pitch16 + x];
+  }
+}
+
+// INTER_LINEAR_EXACT level l from level l-1; a block covers 256 columns x 4 rows (the column
+// tables are read once per thread)
+constexpr int kResRows = 4;
 __global__ void k_resize(const OrbDev G, uint8_t* __restrict__ pyr, int64_t total, int l, const int32_t* __restrict__ xofs,
                          const int32_t* __restrict__ xc1, const int32_t* __restrict__ yofs,
                          const int32_t* __restrict__ yc1) {
   int x = blockIdx.x * blockDim.x + threadIdx.x;
-  int y = blockIdx.y;
   int b = blockIdx.z;
-  int w = G.w[l];
+  int w = G.w[l], h = G.h[l];
   if (x >= w) return;
   int sw = G.w[l - 1], sh = G.h[l - 1];
   const uint8_t* src = pyr + b * total + G.off[l - 1];
@@ -82,15 +97,20 @@ __global__ void k_resize(const OrbDev G, uint8_t* __restrict__ pyr, int64_t tota
     if (ox == -2) return (uint32_t)s[sw - 1] << 8;
     return (uint32_t)cx0 * s[ox] + (uint32_t)cx1 * s[ox + 1];
   };
-  int oy = yofs[y];
-  uint32_t v;
-  if (oy < 0) {
-    v = (hrow(oy == -1 ? 0 : sh - 1) + 128u) >> 8;
-  } else {
-    int cy1 = yc1[y], cy0 = 256 - cy1;
-    v = (hrow(oy) * (uint32_t)cy0 + hrow(oy + 1) * (uint32_t)cy1 + 32768u) >> 16;
+#pragma unroll
+  for (int k = 0; k < kResRows; ++k) {
+    const int y = blockIdx.y * kResRows + k;
+    if (y >= h) break;
+    int oy = yofs[y];
+    uint32_t v;
+    if (oy < 0) {
+      v = (hrow(oy == -1 ? 0 : sh - 1) + 128u) >> 8;
+    } else {
+      int cy1 = yc1[y], cy0 = 256 - cy1;
+      v = (hrow(oy) * (uint32_t)cy0 + hrow(oy + 1) * (uint32_t)cy1 + 32768u) >> 16;
+    }
+    dst[(int64_t)y * w + x] = (uint8_t)(v > 255u ? 255u : v);
   }
-  dst[(int64_t)y * w + x] = (uint8_t)(v > 255u ? 255u : v);
 }
 
 // ------------------------------------------------------------------ FAST
@@ -829,7 +849,7 @@ int orb_init(fvo_ctx* ctx) {
   g.off[c.nlevels] = off;
   g.row0[c.nlevels] = row;
   g.cand_off[c.nlevels] = coff;
-  g.total_px = off;
+  g.total_px = (off + 255) / 256 * 256;  // per-image stride: 256-byte aligned images
   g.total_rows = row;
   g.cand_total = coff;
   {
@@ -957,10 +977,21 @@ int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride
   const int thr = std::min(std::max(c.fast_threshold, 0), 255);
   const OrbDev G = make_dev(g);
   const int ntiles = G.tile0[L];
-  FVO_TIMED(ctx, KN_ORB_COPY, s, hipLaunchKernelGGL(k_copy_level0, dim3((W + 255) / 256, H, batch), dim3(256), 0, s, images, image_stride, pitch,
-                     ctx->pyr, total, W, H));
+  const bool vec = ((uintptr_t)images & 15) == 0 && (image_stride & 15) == 0 && (pitch & 15) == 0 && (W & 15) == 0 &&
+                   (total & 15) == 0;
+  if (vec) {
+    const int64_t n16 = (int64_t)batch * H * (W / 16);
+    const int nblk = (int)std::min<int64_t>((n16 + 255) / 256, 4096);
+    FVO_TIMED(ctx, KN_ORB_COPY, s, hipLaunchKernelGGL(k_copy_level0_v, dim3(nblk), dim3(256), 0, s,
+                                                      reinterpret_cast<const uint4*>(images), image_stride / 16,
+                                                      pitch / 16, reinterpret_cast<uint4*>(ctx->pyr), total / 16, W / 16,
+                                                      H, batch));
+  } else {
+    FVO_TIMED(ctx, KN_ORB_COPY, s, hipLaunchKernelGGL(k_copy_level0, dim3((W + 255) / 256, H, batch), dim3(256), 0, s,
+                                                      images, image_stride, pitch, ctx->pyr, total, W, H));
+  }
   for (int l = 1; l < L; ++l)
-    FVO_TIMED(ctx, KN_ORB_RESIZE, s, hipLaunchKernelGGL(k_resize, dim3((g.w[l] + 255) / 256, g.h[l], batch), dim3(256), 0, s, G, ctx->pyr, total, l,
+    FVO_TIMED(ctx, KN_ORB_RESIZE, s, hipLaunchKernelGGL(k_resize, dim3((g.w[l] + 255) / 256, (g.h[l] + kResRows - 1) / kResRows, batch), dim3(256), 0, s, G, ctx->pyr, total, l,
                        ctx->rt.xofs + ctx->rt.xoff[l], ctx->rt.xc1 + ctx->rt.xoff[l], ctx->rt.yofs + ctx->rt.yoff[l],
                        ctx->rt.yc1 + ctx->rt.yoff[l]));
   FVO_HIP(ctx, hipMemsetAsync(ctx->rowcnt, 0, sizeof(int32_t) * (size_t)batch * g.total_rows, s));
