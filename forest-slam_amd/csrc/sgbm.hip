@@ -410,7 +410,7 @@ template <int D>
 __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvol, const uint16_t* __restrict__ Vvol,
                                                 SgParams p, uint32_t* __restrict__ ckpt, int nck,
                                                 int16_t* __restrict__ raw) {
-  constexpr int DQ = D / 16, PQ = DQ / 2, SEG = 8, PF = 16;
+  constexpr int DQ = D / 16, PQ = DQ / 2, SEG = 8, PF = 8;
   constexpr int CKW = PQ + 1 <= 4 ? 4 : 8;
   constexpr int XS = 2 * D;  // u32 words per column of a 4-row group
   constexpr int RK = sg_ring_keys(D), RS = sg_ring_raw(D);
@@ -507,20 +507,20 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
   uint32_t minR = 0;
 #pragma unroll
   for (int k = 0; k < PQ; ++k) Rst[k] = 0;
-  // C double-buffered one segment ahead (the L recompute needs it first); V loaded at the
-  // segment start, used only after the L recompute (fewer VGPRs: more waves per SIMD)
+  // C and V of a segment loaded at its start (C double-buffered one segment ahead measured the
+  // same at 3 waves/SIMD; single buffers and an 8-column prefetch in sweep 1 give 106 VGPRs,
+  // 4 waves/SIMD, which leaves room for the main stream's kernels on the same CUs)
   uint32_t Cs[2][SEG][PQ], Vs[SEG][PQ];
   auto ldseg = [&](const uint32_t* base, int sg, uint32_t (*cs)[PQ]) {
 #pragma unroll
     for (int i = 0; i < SEG; ++i) ld(base, max(W1 - 1 - (SEG * sg + i), 0), cs[i]);
   };
-  ldseg(Cr, 0, Cs[0]);
   for (int s0 = 0; s0 < nseg; s0 += 2) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int sg = s0 + h;  // may be nseg (an empty segment: every step below is skipped)
+      ldseg(Cr, sg, Cs[h]);
       ldseg(Vr, sg, Vs);
-      ldseg(Cr, sg + 1, Cs[h ^ 1]);
       const int ihi = min(SEG - 1, W1 - 1 - SEG * sg);  // valid i: x' < W1
       // L over the segment (i descending = real x ascending) from the checkpoint at the real
       // column left of it, x' = SEG*(sg+1); zero state when the segment starts at x = 0
