@@ -56,19 +56,22 @@ class StereoFrontEnd:
         self.W, self.H = width, height
         B, cap, dev = batch, self.cap, self.dev
         e = lambda shape, dt: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
-        # persistent device buffers (no allocation inside step)
-        self.kp = e((2 * B, cap, _lib.KP_STRIDE), torch.float32)
-        self.desc = e((2 * B, cap, _lib.DESC_BYTES), torch.uint8)
-        self.cnt = e((2 * B,), torch.int32)
+        # persistent device buffers (no allocation inside step).  The per-step front-stage
+        # outputs (images, ORB, BF, SGBM) have two slots: with overlap_sgbm the front stage of
+        # step k+1 fills one slot while the back stage of step k reads the other.
+        two = lambda shape, dt: [e(shape, dt), e(shape, dt)]  # noqa: E731
+        self.kp_buf = two((2 * B, cap, _lib.KP_STRIDE), torch.float32)
+        self.desc_buf = two((2 * B, cap, _lib.DESC_BYTES), torch.uint8)
+        self.cnt_buf = two((2 * B,), torch.int32)
         self.q_desc = e((2 * B, cap, _lib.DESC_BYTES), torch.uint8)
-        self.q_cnt = e((2 * B,), torch.int32)
-        self.q_kp = e((B, cap, _lib.KP_STRIDE), torch.float32)
-        self.matches = e((2 * B, cap, 3), torch.int32)
-        self.nmatch = e((2 * B,), torch.int32)
+        self.q_cnt_buf = two((2 * B,), torch.int32)
+        self.q_kp_buf = two((B, cap, _lib.KP_STRIDE), torch.float32)
+        self.matches_buf = two((2 * B, cap, 3), torch.int32)
+        self.nmatch_buf = two((2 * B,), torch.int32)
         self.prevL = e((B, height, width), torch.uint8)
         self.prevR = e((B, height, width), torch.uint8)
-        self.disp_buf = [e((B, height, width), torch.int16), e((B, height, width), torch.int16)]
-        self.disp = self.disp_buf[0]
+        self.disp_buf = two((B, height, width), torch.int16)
+        self._select(0)
         self.P3 = e((B, cap, 3), torch.float32)
         self.p2 = e((B, cap, 2), torch.float32)
         self.npts = e((B,), torch.int32)
@@ -93,14 +96,14 @@ class StereoFrontEnd:
             self.T_ba = e((B, 4, 4), torch.float64)
             self.ba_stats = e((B, 6), torch.float64)
             self.valid_from = Kw - 2
-        # overlap_sgbm: SGBM (HBM-bound) runs on its own stream with double-buffered
-        # disparities, so the SGBM of step k+1 overlaps the PnP / BA of step k; the caller's
-        # stream joins it before back-projection.  The step inputs must then be complete
-        # when step() is called (resident in HBM, or pass inputs_ready).  Default: SGBM runs
-        # in order on the caller's stream.
+        # overlap_sgbm: the front stage (SGBM of the previous pairs, ORB + BF of the new frames
+        # -- throughput-bound) runs on its own stream into double-buffered outputs, so the front
+        # stage of step k+1 overlaps the back stage (back-projection, PnP, local BA -- latency-
+        # bound) of step k, which runs on the caller's stream and joins the front stage first.
+        # The step inputs must then be complete when step() is called (resident in HBM, or
+        # pass inputs_ready).  Default: everything in order on the caller's stream.
         self.overlap_sgbm = bool(overlap_sgbm)
-        # sgbm_cus: the compute units the overlapped SGBM stream may use (None = all); the
-        # others stay free for the latency-bound pose / BA kernels of the caller's stream
+        # sgbm_cus: the compute units the front stream may use (None = all)
         if self.overlap_sgbm and sgbm_cus is not None:
             self.s_sgbm = _lib.cu_masked_stream(sgbm_cus, dev)
         else:
@@ -140,22 +143,23 @@ class StereoFrontEnd:
         ctx = self.ctx
         main = torch.cuda.current_stream(self.dev)
         slot = self.k % 2
-        self.disp = self.disp_buf[slot]
-        sg = self.s_sgbm if self.overlap_sgbm else main
+        self._select(slot)
+        fs = self.s_sgbm if self.overlap_sgbm else main
         capturing = torch.cuda.is_current_stream_capturing()
         if self.overlap_sgbm:
             if capturing:
-                # inside a HIP graph the SGBM branch forks from the step's own start (graph
-                # replays are stream-ordered, so no earlier step still reads its buffer)
-                sg.wait_stream(main)
+                # inside a HIP graph the front stage forks from the step's own start (graph
+                # replays are stream-ordered, so no earlier step still reads its slot)
+                fs.wait_stream(main)
             else:
                 if inputs_ready is not None:
-                    sg.wait_event(inputs_ready)
-                if self.main_done[slot] is not None:  # main's reads of this disparity buffer (step k-2)
-                    sg.wait_event(self.main_done[slot])
-                L.record_stream(sg)
-                R.record_stream(sg)
-        with torch.cuda.stream(sg):  # previous stereo pairs -> SGBM (needs only images)
+                    fs.wait_event(inputs_ready)
+                if self.main_done[slot] is not None:  # the back stage of step k-2 read this slot
+                    fs.wait_event(self.main_done[slot])
+                L.record_stream(fs)
+                R.record_stream(fs)
+        with torch.cuda.stream(fs):
+            # ---- front stage: SGBM of the previous pairs (needs only images), ORB + BF
             self.prevL[0].copy_(self.sg_lastL)
             self.prevR[0].copy_(self.sg_lastR)
             if n > 1:
@@ -164,29 +168,35 @@ class StereoFrontEnd:
             self.sg_lastL.copy_(L[n - 1])
             self.sg_lastR.copy_(R[n - 1])
             disp = ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n])
-        self.imgs[:n].copy_(L)
-        self.imgs[n:2 * n].copy_(R)
-        kp, desc, cnt = ctx.orb(self.imgs[:2 * n], out=(self.kp[:2 * n], self.desc[:2 * n], self.cnt[:2 * n]))
-        # query (previous) descriptor sets: left frames then right frames
-        self.q_desc[0].copy_(self.last_desc[0])
-        self.q_cnt[0:1].copy_(self.last_cnt[0:1])
-        if n > 1:
-            self.q_desc[1:n].copy_(desc[:n - 1])
-            self.q_cnt[1:n].copy_(cnt[:n - 1])
-        self.q_desc[n].copy_(self.last_desc[1])
-        self.q_cnt[n:n + 1].copy_(self.last_cnt[1:2])
-        if n > 1:
-            self.q_desc[n + 1:2 * n].copy_(desc[n:2 * n - 1])
-            self.q_cnt[n + 1:2 * n].copy_(cnt[n:2 * n - 1])
-        nb = 2 * n if self.match_right else n
-        m, nm = ctx.bf_match(self.q_desc[:nb], self.q_cnt[:nb], desc[:nb], cnt[:nb],
-                             out=(self.matches[:nb], self.nmatch[:nb]))
-        # previous-left keypoints for back-projection
-        self.q_kp[0].copy_(self.last_kp)
-        if n > 1:
-            self.q_kp[1:n].copy_(kp[:n - 1])
+            self.imgs[:n].copy_(L)
+            self.imgs[n:2 * n].copy_(R)
+            kp, desc, cnt = ctx.orb(self.imgs[:2 * n], out=(self.kp[:2 * n], self.desc[:2 * n], self.cnt[:2 * n]))
+            # query (previous) descriptor sets: left frames then right frames
+            self.q_desc[0].copy_(self.last_desc[0])
+            self.q_cnt[0:1].copy_(self.last_cnt[0:1])
+            if n > 1:
+                self.q_desc[1:n].copy_(desc[:n - 1])
+                self.q_cnt[1:n].copy_(cnt[:n - 1])
+            self.q_desc[n].copy_(self.last_desc[1])
+            self.q_cnt[n:n + 1].copy_(self.last_cnt[1:2])
+            if n > 1:
+                self.q_desc[n + 1:2 * n].copy_(desc[n:2 * n - 1])
+                self.q_cnt[n + 1:2 * n].copy_(cnt[n:2 * n - 1])
+            nb = 2 * n if self.match_right else n
+            m, nm = ctx.bf_match(self.q_desc[:nb], self.q_cnt[:nb], desc[:nb], cnt[:nb],
+                                 out=(self.matches[:nb], self.nmatch[:nb]))
+            # previous-left keypoints for back-projection
+            self.q_kp[0].copy_(self.last_kp)
+            if n > 1:
+                self.q_kp[1:n].copy_(kp[:n - 1])
+            self.last_kp.copy_(kp[n - 1])
+            self.last_desc[0].copy_(desc[n - 1])
+            self.last_desc[1].copy_(desc[2 * n - 1])
+            self.last_cnt[0:1].copy_(cnt[n - 1:n])
+            self.last_cnt[1:2].copy_(cnt[2 * n - 1:2 * n])
         if self.overlap_sgbm:
-            main.wait_stream(self.s_sgbm)
+            main.wait_stream(fs)
+        # ---- back stage: back-projection, PnP, local BA
         P3, p2, npts = ctx.backproject(disp, self.q_kp[:n], kp[:n], m[:n], nm[:n], self.K, self.baseline,
                                        out=(self.P3[:n], self.p2[:n], self.npts[:n]))
         rv, tv, T, st, _ = ctx.pnp_ransac(P3, p2, npts, self.K, self.dist,
@@ -199,15 +209,17 @@ class StereoFrontEnd:
         out = T
         if self.ba_window:
             out = self._local_ba(n, kp, cnt, m, nm, disp, T)
-        self.last_kp.copy_(kp[n - 1])
-        self.last_desc[0].copy_(desc[n - 1])
-        self.last_desc[1].copy_(desc[2 * n - 1])
-        self.last_cnt[0:1].copy_(cnt[n - 1:n])
-        self.last_cnt[1:2].copy_(cnt[2 * n - 1:2 * n])
         if self.overlap_sgbm and not capturing:
             self.main_done[slot] = main.record_event()
         self.k += 1
         return out, st
+
+    def _select(self, slot: int):
+        """Point the per-step buffer names at one of the two slots."""
+        self.kp, self.desc, self.cnt = self.kp_buf[slot], self.desc_buf[slot], self.cnt_buf[slot]
+        self.q_cnt, self.q_kp = self.q_cnt_buf[slot], self.q_kp_buf[slot]
+        self.matches, self.nmatch = self.matches_buf[slot], self.nmatch_buf[slot]
+        self.disp = self.disp_buf[slot]
 
     def _local_ba(self, n, kp, cnt, m, nm, disp, T):
         Kw, ctx = self.ba_window, self.ctx
