@@ -19,10 +19,13 @@ run() {  # run <name> <rocprof args...>
     > "$OUT/$n.out" 2> "$OUT/$n.err" || { echo "pass $n failed"; tail -3 "$OUT/$n.err"; exit 1; }
 }
 run trace --kernel-trace --stats
-run fetch --pmc FETCH_SIZE --kernel-trace
-run write --pmc WRITE_SIZE --kernel-trace
-run valu --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-trace
-run mfma --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_VALU_MFMA_F64 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE --kernel-trace
+# counters on libfvo's kernels only (all in anonymous namespaces): instrumenting the synthetic
+# renderer's torch kernels crashed rocprofv3's PMC passes at 1080p
+KF=(--kernel-include-regex 'anonymous namespace\)::k_')
+run fetch --pmc FETCH_SIZE --kernel-trace "${KF[@]}"
+run write --pmc WRITE_SIZE --kernel-trace "${KF[@]}"
+run valu --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS GRBM_GUI_ACTIVE --kernel-trace "${KF[@]}"
+run mfma --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_VALU_MFMA_F64 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE --kernel-trace "${KF[@]}"
 python3 "$R/profiles/summarize.py" /tmp/p_trace /tmp/p_fetch /tmp/p_write "$OUT" "$SHAPE" &&
 python3 "$R/profiles/summarize_pmc.py" /tmp/p_valu "$OUT/valu_per_kernel.csv" "$SHAPE" k_ > /dev/null &&
 python3 "$R/profiles/summarize_mfma.py" /tmp/p_mfma "$OUT" "$SHAPE" > /dev/null &&
