@@ -1210,51 +1210,68 @@ __global__ void k_pnp_subsets(const int32_t* __restrict__ npts, int batch, int c
 //   k_pnp_hyp_b  the beta approximations + Gauss-Newton + (R, t), the model, and its inlier
 //                count over all points (projectPoints in fp64, error in float32).
 // Blocks whose first iteration is past the frame's current iteration bound exit immediately.
-constexpr int PNP_WS = 112;  // doubles per subset: nv 48 | cws 12 | alphas 20 | pws 15 | us 10
-constexpr int PW_NV = 0, PW_CWS = 48, PW_AL = 60, PW_PWS = 80, PW_US = 95;
+constexpr int PNP_WS = 256;  // doubles per subset: nv 48 | cws 12 | alphas 20 | pws 15 | us 10 | pad | MtM 144
+constexpr int PW_NV = 0, PW_CWS = 48, PW_AL = 60, PW_PWS = 80, PW_US = 95, PW_MTM = 112;
 
-__global__ __launch_bounds__(64) void k_pnp_hyp_a(const float* __restrict__ P3all, const float* __restrict__ p2all,
+// lane per subset: points, control points, barycentric coordinates, M^T M -> workspace (the
+// register-heavy part, kept out of the long Jacobi kernel so that one stays small)
+__global__ __launch_bounds__(64) void k_pnp_setup(const float* __restrict__ P3all, const float* __restrict__ p2all,
                                                   int cap, Cam K, int maxIters, int it_lo,
                                                   const int16_t* __restrict__ table, int table_iters,
                                                   const PnpState* __restrict__ state, double* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) double smt[];  // [144][64]: one M^T M column per lane
+  const int b = blockIdx.y;
+  const int it = it_lo + blockIdx.x * 64 + threadIdx.x;
+  const PnpState st = state[b];
+  const int n = st.n;
+  if (n < 6 || it_lo + (int)blockIdx.x * 64 >= min(st.niters, maxIters)) return;
+  if (it >= maxIters) return;
+  double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
+  const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
+  const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
+  const int16_t* sb = table + ((int64_t)n * table_iters + it) * 5;
+  EPnPd<5> e;
+  e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    int j = sb[i];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) e.pws[3 * i + c] = (double)P3[j * 3 + c];
+    double xy[2];
+    dundistort(K, (double)p2[j * 2], (double)p2[j * 2 + 1], xy);
+    float fx = (float)xy[0], fy = (float)xy[1];
+    e.us[2 * i] = fx * K.fx + K.cx;
+    e.us[2 * i + 1] = fy * K.fy + K.cy;
+  }
+  double* mt = smt + threadIdx.x;
+  e.build_mtm<64>(mt);
+#pragma unroll 8
+  for (int k = 0; k < 144; ++k) w[PW_MTM + k] = mt[k * 64];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) w[PW_CWS + r * 3 + k] = e.cws[r][k];
+#pragma unroll
+  for (int k = 0; k < 20; ++k) w[PW_AL + k] = e.alphas[k];
+#pragma unroll
+  for (int k = 0; k < 15; ++k) w[PW_PWS + k] = e.pws[k];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) w[PW_US + k] = e.us[k];
+}
+
+// 8-lane group per subset: the null space of its M^T M (staged in LDS)
+__global__ __launch_bounds__(64) void k_pnp_hyp_a(int maxIters, int it_lo, const PnpState* __restrict__ state,
+                                                  double* __restrict__ ws) {
   __shared__ double su[8][144];  // M^T M of the block's 8 subsets (one 8-lane group each)
   const int b = blockIdx.y, g = threadIdx.x >> 3, l = threadIdx.x & 7;
   const int it = it_lo + blockIdx.x * 8 + g;
   const PnpState st = state[b];
-  const int n = st.n;
-  if (n < 6 || it_lo + (int)blockIdx.x * 8 >= min(st.niters, maxIters)) return;
+  if (st.n < 6 || it_lo + (int)blockIdx.x * 8 >= min(st.niters, maxIters)) return;
   if (it >= maxIters) return;  // the whole group
   double* u = su[g];
   double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
-  if (l == 0) {
-    const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
-    const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
-    const int16_t* sb = table + ((int64_t)n * table_iters + it) * 5;
-    EPnPd<5> e;
-    e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      int j = sb[i];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) e.pws[3 * i + c] = (double)P3[j * 3 + c];
-      double xy[2];
-      dundistort(K, (double)p2[j * 2], (double)p2[j * 2 + 1], xy);
-      float fx = (float)xy[0], fy = (float)xy[1];
-      e.us[2 * i] = fx * K.fx + K.cx;
-      e.us[2 * i + 1] = fy * K.fy + K.cy;
-    }
-    e.build_mtm<1>(u);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) w[PW_CWS + r * 3 + k] = e.cws[r][k];
-#pragma unroll
-    for (int k = 0; k < 20; ++k) w[PW_AL + k] = e.alphas[k];
-#pragma unroll
-    for (int k = 0; k < 15; ++k) w[PW_PWS + k] = e.pws[k];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) w[PW_US + k] = e.us[k];
-  }
+  for (int k = l; k < 144; k += 8) u[k] = w[PW_MTM + k];
+  __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
   jacobi12_null4_group(u, l, w + PW_NV);
 }
@@ -1429,6 +1446,8 @@ int pose_init(fvo_ctx* ctx) {
   if ((rc = fvo_alloc(ctx, &ctx->pnp_sub, n)) || (rc = fvo_alloc(ctx, &ctx->pnp_hyp, 2 * n)) ||
       (rc = ransac_table_init(ctx)) || (rc = fvo_alloc(ctx, &ctx->pnp_models, it * 6)) ||
       (rc = fvo_alloc(ctx, &ctx->pnp_ws, it * PNP_WS)) ||
+      (rc = hipFuncSetAttribute((const void*)k_pnp_setup, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                144 * 64 * (int)sizeof(double)) == hipSuccess ? 0 : fvo_fail(ctx, "pnp: LDS attribute")) ||
       (rc = fvo_alloc(ctx, &ctx->pnp_good, it)) || (rc = fvo_alloc(ctx, (PnpState**)&ctx->pnp_state, B)))
     return rc;
   return 0;
@@ -1469,8 +1488,10 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
   PnpState* st = (PnpState*)ctx->pnp_state;
   const int first = std::min(maxIters, 128);
   auto hyp = [&](int lo, int hi) {
-    hipLaunchKernelGGL(k_pnp_hyp_a, dim3((hi - lo + 7) / 8, batch), dim3(64), 0, s, P3, p2, cap, c, maxIters, lo,
+    hipLaunchKernelGGL(k_pnp_setup, dim3((hi - lo + 63) / 64, batch), dim3(64), 144 * 64 * sizeof(double), s, P3, p2,
+                       cap, c, maxIters, lo,
                        ctx->rs_table, ctx->rs_table_iters, st, ctx->pnp_ws);
+    hipLaunchKernelGGL(k_pnp_hyp_a, dim3((hi - lo + 7) / 8, batch), dim3(64), 0, s, maxIters, lo, st, ctx->pnp_ws);
     hipLaunchKernelGGL(k_pnp_hyp_b, dim3((hi - lo + 15) / 16, batch), dim3(64), 0, s, P3, p2, cap, c, thr2, maxIters,
                        lo, st, ctx->pnp_ws, ctx->pnp_models, ctx->pnp_good);
     hipLaunchKernelGGL(k_pnp_replay, dim3(batch), dim3(64), 0, s, maxIters, lo, hi, conf, ctx->pnp_good, st);
