@@ -1215,7 +1215,7 @@ constexpr int PW_NV = 0, PW_CWS = 48, PW_AL = 60, PW_PWS = 80, PW_US = 95, PW_MT
 
 // lane per subset: points, control points, barycentric coordinates, M^T M -> workspace (the
 // register-heavy part, kept out of the long Jacobi kernel so that one stays small)
-__global__ __launch_bounds__(64) void k_pnp_setup(const float* __restrict__ P3all, const float* __restrict__ p2all,
+__global__ __launch_bounds__(64, 4) void k_pnp_setup(const float* __restrict__ P3all, const float* __restrict__ p2all,
                                                   int cap, Cam K, int maxIters, int it_lo,
                                                   const int16_t* __restrict__ table, int table_iters,
                                                   const PnpState* __restrict__ state, double* __restrict__ ws) {
