@@ -359,21 +359,51 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
   }
   __syncthreads();
   const int L = s_L, O = s_O;
-  // per-frame observation lists (stable, landmark-major order inside a frame)
-  int fbase = 0;
-  for (int f = 0; f < n; ++f) {
-    if (tid == 0) v.hdr[8 + f] = fbase;
-    for (int base = 0; base < O; base += kBlock) {
-      const int i = base + tid;
-      const bool hit = i < O && v.obs[i].frame == f;
-      int tot;
-      const int pos = block_scan(hit ? 1 : 0, s_tmp, &tot);
-      if (hit) v.flist[fbase + pos] = i;
-      fbase += tot;
+  // per-frame observation lists (stable, landmark-major order inside a frame): a counting
+  // sort -- frame sizes by LDS atomics, then per 256-observation chunk every wave ranks its
+  // lanes within each frame by ballots, the waves' counts give the chunk's offsets (three
+  // barriers per chunk instead of two per frame per chunk)
+  __shared__ int s_fcnt[kKMax], s_foff[kKMax], s_wcnt[kBlock / 64][kKMax];
+  if (tid < kKMax) s_fcnt[tid] = 0;
+  __syncthreads();
+  for (int i = tid; i < O; i += kBlock) atomicAdd(&s_fcnt[v.obs[i].frame], 1);
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int f = 0; f < n; ++f) {
+      v.hdr[8 + f] = acc;
+      s_foff[f] = acc;
+      acc += s_fcnt[f];
     }
+    v.hdr[8 + n] = acc;
+  }
+  __syncthreads();
+  const int lane = tid & 63, wid = tid >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int base = 0; base < O; base += kBlock) {
+    const int i = base + tid;
+    const int f = i < O ? (int)v.obs[i].frame : -1;
+    int rank = 0;
+    for (int ff = 0; ff < n; ++ff) {
+      const unsigned long long mk = __ballot(f == ff);
+      if (f == ff) rank = __popcll(mk & lt);
+      if (lane == 0) s_wcnt[wid][ff] = __popcll(mk);
+    }
+    __syncthreads();
+    if (f >= 0) {
+      int pos = s_foff[f] + rank;
+      for (int w2 = 0; w2 < wid; ++w2) pos += s_wcnt[w2][f];
+      v.flist[pos] = i;
+    }
+    __syncthreads();
+    if (tid < n) {
+      int c = 0;
+      for (int w2 = 0; w2 < kBlock / 64; ++w2) c += s_wcnt[w2][tid];
+      s_foff[tid] += c;
+    }
+    __syncthreads();
   }
   if (tid == 0) {
-    v.hdr[8 + n] = fbase;
     v.lstart[L] = O;
     S->L = L;
     S->O = O;
