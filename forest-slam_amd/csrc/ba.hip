@@ -315,15 +315,18 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
           ++len;
         }
       }
-      int tl, to;
-      const int lid = block_scan(cand ? 1 : 0, s_tmp, &tl);
-      const int oof = block_scan(len, s_tmp, &to);
+      // one scan of (observations << 10 | candidate): len <= 21, so both sums fit
+      int tp;
+      const int packed = block_scan((len << 10) | (cand ? 1 : 0), s_tmp, &tp);
+      const int lid = packed & 1023, oof = packed >> 10, tl = tp & 1023, to = tp >> 10;
       const int L0 = s_L, O0 = s_O;
       // creation stops at the first landmark that does not fit (the failing rows are a
-      // suffix of this chunk's candidates: both prefix sums are monotone)
-      const bool ok = cand && (L0 + lid < dm.Lmax) && (O0 + oof + len <= dm.Omax);
-      const int nok = __syncthreads_count(ok);
-      const int nfail = __syncthreads_count(cand && !ok);
+      // suffix of this chunk's candidates: both prefix sums are monotone); when the whole
+      // chunk fits (the block totals say so, uniformly) no per-thread test is needed
+      const bool allfit = L0 + tl <= dm.Lmax && O0 + to <= dm.Omax;
+      const bool ok = cand && (allfit || ((L0 + lid < dm.Lmax) && (O0 + oof + len <= dm.Omax)));
+      const int nok = allfit ? tl : __syncthreads_count(ok);
+      const int nfail = allfit ? 0 : __syncthreads_count(cand && !ok);
       if (ok) {
         const int id = L0 + lid;
         int o = O0 + oof;
@@ -345,8 +348,8 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
           b = nb;
         }
       }
-      int tot_ok;
-      (void)block_scan(ok ? len : 0, s_tmp, &tot_ok);
+      int tot_ok = to;
+      if (!allfit) (void)block_scan(ok ? len : 0, s_tmp, &tot_ok);
       if (tid == 0) {
         s_L = L0 + nok;
         s_O = O0 + tot_ok;
