@@ -17,6 +17,7 @@
 //                per-point Jacobian rows accumulated across lanes.
 // All pose math is fp64 (as in OpenCV); compiled with -ffp-contract=off.
 #include <cfloat>
+#include <type_traits>
 
 #include "fvo_internal.h"
 #include "ransac.h"
@@ -574,11 +575,19 @@ __device__ __forceinline__ double dist2(const double* a, const double* b) {
   return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
 }
 
-template <int NP>
+// VIEW: the subset's points, barycentric coordinates and control points are read in place
+// (workspace pointers) instead of held in registers -- the β stage only reads them.
+template <int NP, bool VIEW = false>
 struct EPnPd {
+  template <int N>
+  using Arr = typename std::conditional<VIEW, const double*, double[N]>::type;
+  using Cws = typename std::conditional<VIEW, const double (*)[3], double[4][3]>::type;
   double fu, fv, uc, vc;
-  double pws[3 * NP], us[2 * NP], alphas[4 * NP], pcs[3 * NP];
-  double cws[4][3], ccs[4][3];
+  Arr<3 * NP> pws;
+  Arr<2 * NP> us;
+  Arr<4 * NP> alphas;
+  Cws cws;
+  double pcs[3 * NP], ccs[4][3];
 
   __device__ void choose_control_points() {
     #pragma unroll
@@ -1284,6 +1293,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp_b(const float* __restrict__ P3al
   // serial loop's selection -- approximation 1, replaced by a later one only on a strictly
   // smaller error -- is applied to their results in order), then all four lanes score the
   // model over a quarter of the points each
+  __shared__ double sL[16][66];  // per group: L (6x10) then rho (6)
   const int b = blockIdx.y, g = threadIdx.x >> 2, l = threadIdx.x & 3;
   const int it = it_lo + blockIdx.x * 16 + g;
   const PnpState st = state[b];
@@ -1293,29 +1303,20 @@ __global__ __launch_bounds__(64) void k_pnp_hyp_b(const float* __restrict__ P3al
   const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
   const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
   const double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
-  EPnPd<5> e;
+  EPnPd<5, true> e;
   e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
-  double nv[4][12];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int k = 0; k < 12; ++k) nv[r][k] = w[PW_NV + r * 12 + k];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) e.cws[r][k] = w[PW_CWS + r * 3 + k];
-#pragma unroll
-  for (int k = 0; k < 20; ++k) e.alphas[k] = w[PW_AL + k];
-#pragma unroll
-  for (int k = 0; k < 15; ++k) e.pws[k] = w[PW_PWS + k];
-#pragma unroll
-  for (int k = 0; k < 10; ++k) e.us[k] = w[PW_US + k];
-  double R[9], t[3], err = 0.0;
-  {
-    double L[60], rho[6];
-    e.prep(nv, L, rho);
-    err = e.approx(l < 3 ? l + 1 : 3, L, rho, nv, R, t);
-  }
+  e.pws = w + PW_PWS;
+  e.us = w + PW_US;
+  e.alphas = w + PW_AL;
+  e.cws = reinterpret_cast<const double (*)[3]>(w + PW_CWS);
+  const double (*nv)[12] = reinterpret_cast<const double (*)[12]>(w + PW_NV);
+  // L (6x10) and rho are the same for the group's three approximations: lane 0 forms them
+  double* L = sL[g];
+  if (l == 0) e.prep(nv, L, L + 60);
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  double R[9], t[3];
+  const double err = e.approx(l < 3 ? l + 1 : 3, L, L + 60, nv, R, t);
   const int base = threadIdx.x & ~3;
   const double e1 = __shfl(err, base + 1, 64), e2 = __shfl(err, base + 2, 64);
   int sel = 0;
