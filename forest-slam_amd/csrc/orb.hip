@@ -144,7 +144,8 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   __shared__ uint8_t s_img[kIH][kIW];
   __shared__ uint8_t s_sc[kFH][kFW];
   __shared__ uint16_t s_list[kFH * kFW];
-  __shared__ int s_n;
+  __shared__ uint16_t s_pre[kFH * kFW];
+  __shared__ int s_n, s_npre;
   const int b = blockIdx.y, t = blockIdx.x;
   const int l = tile_level(G, t);
   const int lt = t - G.tile0[l];
@@ -158,15 +159,40 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
     s_img[r][c] = im[(int64_t)y * w + x];
   }
   for (int i = threadIdx.x; i < kFH * kFW; i += 256) (&s_sc[0][0])[i] = 0;
-  if (threadIdx.x == 0) s_n = 0;
+  if (threadIdx.x == 0) { s_n = 0; s_npre = 0; }
   __syncthreads();
-  // FAST-9 test on the tile + halo; positions that pass go to the list
+  // FAST-9 on the tile + halo in two compacted stages.  (1) A 9-arc of the 16-circle always
+  // holds at least two of the four cardinal pixels (0, 4, 8, 12), so a position with fewer
+  // than two cardinals brighter than v+t and fewer than two darker than v-t cannot be a
+  // corner; the rest go to a pre-list.  (2) The full 16-pixel test on the pre-list; corners
+  // go to the list.  Same corners as testing every position.
   for (int i0 = 0; i0 < kFH * kFW; i0 += 256) {  // uniform trip count: ballots see whole waves
     const int i = i0 + threadIdx.x;
     const int r = i / kFW, c = i % kFW;
     const int y = y0 - 1 + r, x = x0 - 1 + c;
-    bool corner = false;
+    bool maybe = false;
     if (i < kFH * kFW && x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
+      const int v = s_img[r + 3][c + 3];
+      const int p0 = s_img[r][c + 3], p4 = s_img[r + 3][c + 6], p8 = s_img[r + 6][c + 3], p12 = s_img[r + 3][c];
+      const int nb = (p0 > v + thr) + (p4 > v + thr) + (p8 > v + thr) + (p12 > v + thr);
+      const int nd = (p0 < v - thr) + (p4 < v - thr) + (p8 < v - thr) + (p12 < v - thr);
+      maybe = nb >= 2 || nd >= 2;
+    }
+    const unsigned long long m = __ballot(maybe);
+    int base = 0;
+    if ((threadIdx.x & 63) == 0 && m) base = atomicAdd(&s_npre, __popcll(m));
+    base = __shfl(base, 0, 64);
+    if (maybe) s_pre[base + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1ull))] = (uint16_t)i;
+  }
+  __syncthreads();
+  const int npre = s_npre;
+  for (int j0 = 0; j0 < npre; j0 += 256) {  // uniform trip count
+    const int j = j0 + threadIdx.x;
+    bool corner = false;
+    int i = 0;
+    if (j < npre) {
+      i = s_pre[j];
+      const int r = i / kFW, c = i % kFW;
       const int v = s_img[r + 3][c + 3];
       unsigned bright = 0, dark = 0;
 #pragma unroll
@@ -175,11 +201,11 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
         bright |= (unsigned)(p > v + thr) << k;
         dark |= (unsigned)(p < v - thr) << k;
       }
-      auto has9 = [](unsigned m) {
-        unsigned mm = m | (m << 16);
+      auto has9 = [](unsigned mm0) {
+        unsigned mm = mm0 | (mm0 << 16);
         unsigned cc = mm;
 #pragma unroll
-        for (int j = 1; j <= 8; ++j) cc &= mm >> j;
+        for (int jj = 1; jj <= 8; ++jj) cc &= mm >> jj;
         return (cc & 0xFFFFu) != 0;
       };
       corner = has9(bright) || has9(dark);
