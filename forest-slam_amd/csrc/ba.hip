@@ -465,7 +465,6 @@ __global__ void k_ba_setcost(void* ws, BaDims dm, int first) {
 
 // pose blocks of one frame + W of its observations
 __global__ __launch_bounds__(kBlock) void k_ba_pp(BaIn in, void* ws, BaDims dm, BaCam cam) {
-  __shared__ double s_red[kBlock / 64];
   const BaWin v = view(ws, dm, blockIdx.x);
   BaState* S = v.st;
   const int f = blockIdx.y + 1;
@@ -490,9 +489,19 @@ __global__ __launch_bounds__(kBlock) void k_ba_pp(BaIn in, void* ws, BaDims dm, 
       for (int bb = 0; bb < 3; ++bb)
         Wo[3 * a + bb] = w * (Jp[0][a] * Jl[0][bb] + Jp[1][a] * Jl[1][bb] + Jp[2][a] * Jl[2][bb]);
   }
+  // the 27 block sums at once (same order as block_sum: wave sums, then the waves in order)
+  __shared__ double s_part[kBlock / 64][27];
+#pragma unroll
   for (int i = 0; i < 27; ++i) {
-    const double t = block_sum(h[i], s_red);
-    if (threadIdx.x == 0) S->Hpp[f][i] = t;
+    const double wv = wave_sum(h[i]);
+    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6][i] = wv;
+  }
+  __syncthreads();
+  if (threadIdx.x < 27) {
+    double t = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / 64; ++k) t += s_part[k][threadIdx.x];
+    S->Hpp[f][threadIdx.x] = t;
   }
 }
 
