@@ -17,6 +17,7 @@
 //                per-point Jacobian rows accumulated across lanes.
 // All pose math is fp64 (as in OpenCV); compiled with -ffp-contract=off.
 #include <cfloat>
+#include <cstdlib>
 #include <type_traits>
 
 #include "fvo_internal.h"

@@ -342,8 +342,9 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
       uint2* vp = reinterpret_cast<uint2*>(Vvol + colofs + yo);
 #pragma unroll
       for (int i = 0; i < NV2; ++i) {
-        cp[i] = make_uint2(crun[2 * i], crun[2 * i + 1]);
-        vp[i] = make_uint2(st[2 * i], st[2 * i + 1]);
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store(u32x2{crun[2 * i], crun[2 * i + 1]}, reinterpret_cast<u32x2*>(cp + i));
+        __builtin_nontemporal_store(u32x2{st[2 * i], st[2 * i + 1]}, reinterpret_cast<u32x2*>(vp + i));
       }
     }
   }
