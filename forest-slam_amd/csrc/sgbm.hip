@@ -457,7 +457,7 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
   const int64_t ckbase = ((int64_t)b * gridDim.x + blockIdx.x) * nck;
   auto ld = [&](const uint32_t* base, int x, uint32_t* out) {
 #pragma unroll
-    for (int k = 0; k < PQ; ++k) out[k] = base[(int64_t)x * XS + k];
+    for (int k = 0; k < PQ; ++k) out[k] = __builtin_nontemporal_load(base + (int64_t)x * XS + k);
   };
 
   // ---- sweep 1: left -> right, checkpoints.  Loads are unconditional (clamped columns) so
