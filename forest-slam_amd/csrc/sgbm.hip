@@ -148,14 +148,16 @@ __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q
 
 
 // ------------------------------------------------------------------ fused cost + vertical pass
-// One block (4 waves) per (64 columns, stripe, pair); quad of lanes per column as in
-// k_sg_vert.  Per new hsum row (the row entering the 7-row window) the block stages the 3
-// image rows of its column range in LDS (left: 70 px, right: 70 + D - 1 px, +2 apron),
-// derives the (x-Sobel, intensity) channel words and their BT min/max, evaluates the packed
-// BT pixel cost of its 70 x D cells into LDS and box-sums 7 columns per lane.  The window's
-// 8 hsum rows are a shift register in VGPRs, so the hsum volume never goes to HBM.  The next
-// row's image bytes are fetched before the current row is processed.  Same integer
-// arithmetic as k_sg_hsum + k_sg_vert (order-independent sums).
+// One block (G*CB threads) per (CB columns, stripe, pair), G lanes per column.  Per new hsum
+// row (the row entering the 7-row window) the block stages the 3 image rows of its column
+// range in LDS (left: CB+6 px, right: CB+6+D-1 px, +2 apron each side), derives the
+// (x-Sobel, intensity) channel words and their BT min/max, evaluates the packed BT pixel
+// cost of its (CB+6) x D cells into LDS (task slots laid out so neither the BT word reads nor
+// the cost stores conflict on LDS banks) and box-sums 7 columns per lane.  The window's 7
+// hsum rows are a shift register in VGPRs, so the hsum volume never goes to HBM.  The next
+// row's image bytes are loaded right after the current row is staged and taken before the
+// row's C / V stores (vmcnt retires in order: a wait for them behind the stores would also
+// wait for the stores).  Integer arithmetic as oracle/sgbm_ref.cpp (order-independent sums).
 template <int D, int CB, int G>
 __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
                                                     int64_t stride, int pitch, SgParams p, uint16_t* __restrict__ Cvol,
@@ -191,28 +193,25 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
   auto clip = [ft](int v) { return min(max(v, -ft), ft) + ft; };
 
   // image bytes of hsum row r (rows r-1, r, r+1, clamped): thread-private prefetch slots
-  uint8_t pre[PER];
+  uint32_t pre[PER];
   auto fetch = [&](int r) {
     const int rows[3] = {r > 0 ? r - 1 : r, r, r < H - 1 ? r + 1 : r};
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const int i = tid + NT * k;
-      uint8_t v = 0;
-      if (i < NIMG) {
-        const int rr = i / (NLI + NRI), j = i % (NLI + NRI);
-        if (j < NLI) v = Lb[(int64_t)rows[rr] * pitch + min(max(xl0 - 2 + j, 0), W - 1)];
-        else v = Rb[(int64_t)rows[rr] * pitch + min(max(xr0 - 2 + (j - NLI), 0), W - 1)];
-      }
-      pre[k] = v;
+      const int i = min(tid + NT * k, NIMG - 1);
+      const int rr = i / (NLI + NRI), j = i % (NLI + NRI);
+      const uint8_t* src = j < NLI ? Lb + min(max(xl0 - 2 + j, 0), W - 1) : Rb + min(max(xr0 - 2 + (j - NLI), 0), W - 1);
+      pre[k] = src[(int64_t)rows[rr] * pitch];
     }
   };
   // hsum row from the staged bytes -> acc (this lane's column and disparity run)
-  auto hs_row = [&](uint32_t* acc) {
+  auto hs_row = [&](uint32_t* acc, int next) {
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int i = tid + NT * k;
-      if (i < NIMG) (&sImg[0][0])[i] = pre[k];
+      if (i < NIMG) (&sImg[0][0])[i] = (uint8_t)pre[k];
     }
+    if (next >= 0) fetch(next);
     __syncthreads();
     // channel words at core-1 .. core+1 of both images; borders (x < 1, x >= W-1) read ftzero
     for (int j = tid; j < (nl + 2) + (nr + 2); j += NT) {
@@ -248,8 +247,12 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
     }
     __syncthreads();
     // pixel costs of the kCX (clamped) columns x D disparities, 8 disparities per task
-    for (int task = tid; task < kCX * (D / 8); task += NT) {
-      const int i = task / (D / 8), d0 = (task % (D / 8)) * 8;
+    constexpr int NDB = D / 32;
+    constexpr int NSLOT = ((kCX + 7) / 8) * NDB * 32;
+    for (int t = tid; t < NSLOT; t += NT) {
+      const int g = t >> 5, w = t & 31;
+      const int i = (g / NDB) * 8 + (w >> 2), d0 = ((g % NDB) * 4 + (w & 3)) * 8;
+      if (i >= kCX) continue;
       const int x1c = min(max(c0 - 3 + i, 0), p.width1 - 1);
       const int kl = x1c + p.minX1 - xl0;
       const u16x2 u = as_v(sW[0][kl]), u0 = as_v(sW[1][kl]), u1 = as_v(sW[2][kl]);
@@ -286,19 +289,15 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
   // window shift register: win[k] = hsum(clamp(y - 3 + k)), k = 0..6, for the output row y
   uint32_t win[7][PQ], crun[PQ], st[PQ];
   fetch(start);
-  hs_row(win[6]);
+  hs_row(win[6], start + 1 <= H - 1 ? start + 1 : -1);
   for (int r = start + 1; r <= start + 3; ++r) {
 #pragma unroll
     for (int k = 0; k < 6; ++k)
 #pragma unroll
       for (int j = 0; j < PQ; ++j) win[k][j] = win[k + 1][j];
-    if (r <= H - 1) {  // rows past H-1 clamp to H-1 (win[6] keeps it)
-      fetch(r);
-      hs_row(win[6]);
-    }
+    if (r <= H - 1) hs_row(win[6], r + 1 <= H - 1 ? r + 1 : -1);
   }
   // win[3..6] = hs(start..start+3 clamped); rows above start clamp to start
-  if (start + 4 <= H - 1) fetch(start + 4);
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
@@ -320,8 +319,7 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
     if (y > start) {  // window [y-3, y+3] clamped to [start, H-1]: out clamp(y-4), in clamp(y+3)
       uint32_t nw[PQ];
       if (y + 3 <= H - 1) {
-        hs_row(nw);
-        if (y + 4 <= H - 1) fetch(y + 4);
+        hs_row(nw, y + 4 <= H - 1 ? y + 4 : -1);
       } else {
 #pragma unroll
         for (int j = 0; j < PQ; ++j) nw[j] = win[6][j];
@@ -336,6 +334,8 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
       for (int j = 0; j < PQ; ++j) win[6][j] = nw[j];
     }
     minPrev = hstepG<PQ, G>(st, crun, q, P1, minPrev, p.P2);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) asm volatile("" : "+v"(pre[k]) :: "memory");
     if (y >= first_out && x1 < p.width1) {
       const int64_t yo = (int64_t)(y >> 2) * 4 * plane + (y & 3) * D;
       uint2* cp = reinterpret_cast<uint2*>(Cvol + colofs + yo);
@@ -436,7 +436,7 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
     const uint32_t kv = key[x2 & (RK - 1)];
     return kv == 0xFFFFFFFFu ? INVALID : (int)(0xFFFFu - (kv & 0xFFFFu)) + p.minX1 - x2;
   };
-  auto check = [&](int x1) {
+  auto checked = [&](int x1) -> int {
     const int x = x1 + p.minX1;
     int d1 = sraw[x1 & (RS - 1)];
     if (d1 != INVALID) {
@@ -447,8 +447,16 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
         if (a >= p.minD && abs(a - d_) > p.disp12 && cc >= p.minD && abs(cc - _d) > p.disp12) d1 = INVALID;
       }
     }
-    if (rowok) out[x] = (int16_t)d1;
+    return d1;
   };
+  auto check = [&](int x1) {
+    const int d1 = checked(x1);
+    if (rowok) out[x1 + p.minX1] = (int16_t)d1;
+  };
+  // lanes with no pixel to check store into this lane's words of the dummy checkpoint slot, so
+  // every segment issues the same global stores: with a conditional store the compiler's vmcnt
+  // bookkeeping falls back to draining every load in flight at the next segment
+  int16_t* const sink = reinterpret_cast<int16_t*>(ckpt + ((((int64_t)b * gridDim.x + blockIdx.x) * nck + nck - 1) * 64 + lane) * (PQ + 1 <= 4 ? 4 : 8));
   int next_chk = W1 - 1;  // highest pixel not yet checked
   const int64_t rowofs = (((int64_t)b * p.HG4 + (yy >> 2)) * W1 * (4 * D) + (yy & 3) * D + q * DQ) / 2;
   const uint32_t* Cr = reinterpret_cast<const uint32_t*>(Cvol) + rowofs;
@@ -520,25 +528,26 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int sg = s0 + h;  // may be nseg (an empty segment: every step below is skipped)
-      ldseg(Cr, sg, Cs[h]);
-      ldseg(Vr, sg, Vs);
-      const int ihi = min(SEG - 1, W1 - 1 - SEG * sg);  // valid i: x' < W1
-      // L over the segment (i descending = real x ascending) from the checkpoint at the real
-      // column left of it, x' = SEG*(sg+1); zero state when the segment starts at x = 0
+      // the checkpoint first, then C, then V: the L recompute needs the first two only
       uint32_t lst[PQ], Ls[SEG][PQ];
       const bool zero = SEG * (sg + 1) > W1 - 1;
+      uint32_t v[CKW];
       {
         const uint32_t* cp = ckpt + ((ckbase + (zero ? nck - 1 : sg)) * 64 + lane) * CKW;
-        uint32_t v[CKW];
 #pragma unroll
         for (int kk = 0; kk < CKW; kk += 4) {
           const uint4 w4 = *reinterpret_cast<const uint4*>(cp + kk);
           v[kk] = w4.x; v[kk + 1] = w4.y; v[kk + 2] = w4.z; v[kk + 3] = w4.w;
         }
-#pragma unroll
-        for (int kk = 0; kk < PQ; ++kk) lst[kk] = zero ? 0u : v[kk];
-        minPrev = zero ? 0u : v[PQ];
       }
+      ldseg(Cr, sg, Cs[h]);
+      ldseg(Vr, sg, Vs);
+      const int ihi = min(SEG - 1, W1 - 1 - SEG * sg);  // valid i: x' < W1
+      // L over the segment (i descending = real x ascending) from the checkpoint at the real
+      // column left of it, x' = SEG*(sg+1); zero state when the segment starts at x = 0
+#pragma unroll
+      for (int kk = 0; kk < PQ; ++kk) lst[kk] = zero ? 0u : v[kk];
+      minPrev = zero ? 0u : v[PQ];
       uint32_t lmin = minPrev;
 #pragma unroll
       for (int i = SEG - 1; i >= 0; --i) {
@@ -603,9 +612,11 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
       }
       // pixels whose keys became final with this segment (at most SEG): one lane each
       const int x1_lo = W1 - 1 - (SEG * sg + ihi);
-      if (ihi >= 0) {
-        const int cnt = min(next_chk - (x1_lo + D) + 1, SEG);
-        if (q < cnt) check(next_chk - q);
+      {
+        const int cnt = ihi >= 0 ? min(next_chk - (x1_lo + D) + 1, SEG) : 0;
+        const bool act = q < cnt && rowok;
+        const int d1 = checked(next_chk - q);
+        *(act ? out + (next_chk - q + p.minX1) : sink) = (int16_t)d1;
         if (cnt > 0) next_chk -= cnt;
       }
     }

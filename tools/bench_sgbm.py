@@ -35,7 +35,7 @@ def main():
     torch.cuda.synchronize()
     st = {k: round(v[0] / n, 4) for k, v in ctx.timing_read().items()}
     ctx.timing_enable([])
-    var = {k: os.environ.get(k, "") for k in ("FVO_SG_G", "FVO_SG_CB", "FVO_SG_HG", "FVO_SG_PF", "FVO_SG_CHUNKS")}
+    var = {k: os.environ.get(k, "") for k in ("FVO_SG_G", "FVO_SG_CB", "FVO_SG_PF", "FVO_SG_CHUNKS")}
     print(json.dumps({"variant": var, "call_ms": round(call_ms, 3), "kernels_ms": st}), flush=True)
 
 

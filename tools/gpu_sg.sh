@@ -1,0 +1,12 @@
+#!/bin/bash
+# SGBM iteration on the GPU box: parity tests of SGBM, then bench_sgbm variants.
+#   gpurun -- 'bash tools/gpu_sg.sh <tag> "<env assignments per variant>" ...'
+set -uo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1; shift
+mkdir -p "$R/gpurun_out"
+timeout -k 10 300 python -u -m pytest "$R/tests/test_gpu_parity.py" "$R/tests/test_natural.py" -k "sgbm" -x -q --timeout 200 --timeout-method thread > "$R/gpurun_out/sg_tests_$TAG.log" 2>&1 || { echo "sgbm tests failed"; tail -30 "$R/gpurun_out/sg_tests_$TAG.log"; exit 1; }
+tail -2 "$R/gpurun_out/sg_tests_$TAG.log"
+for v in "$@"; do
+  env $v timeout -k 10 120 python -u "$R/tools/bench_sgbm.py" || { echo "bench_sgbm failed: $v"; exit 1; }
+done
