@@ -49,7 +49,10 @@ constexpr int kBlock = 256;
 // one partial Schur product (MFMA accumulators kept across its chunks), so k_ba_solve sums
 // kLinParts partials instead of one per chunk.  Fixed chunk order: deterministic.
 constexpr int kLinParts = 16;
-constexpr int kLinMaxTiles = 9;  // 16x16 tiles per wave: 36 upper tiles at NR = 128 / 4 waves
+// k_ba_lin runs 16 waves per block: its LDS slice (up to 150 KB) allows one block per CU, so
+// the block's own waves are all the latency hiding the CU gets
+constexpr int kLinWaves = 16, kLinBlock = 64 * kLinWaves;
+constexpr int kLinMaxTiles = (36 + kLinWaves - 1) / kLinWaves;  // 16x16 tiles per wave: 36 upper tiles at NR = 128
 constexpr double kD2Mono = 5.991, kD2Stereo = 7.815, kMinZ = 0.01, kLam0 = 1e-3;
 
 struct BaState {
@@ -506,7 +509,7 @@ __global__ __launch_bounds__(kBlock) void k_ba_pp(BaIn in, void* ws, BaDims dm, 
 }
 
 // landmark blocks of a window's chunks + their share of the reduced camera system on MFMA
-// (tile k of the enumeration I <= J over the pose rows and the z column goes to wave k & 3)
+// (tile k of the enumeration I <= J over the pose rows and the z column goes to wave k mod kLinWaves)
 __device__ __forceinline__ void lin_tile(int k, int ntu, int NT, int& I, int& J) {
   int idx = 0;
   for (int i = 0; i < ntu; ++i)
@@ -517,7 +520,7 @@ __device__ __forceinline__ void lin_tile(int k, int ntu, int NT, int& I, int& J)
   I = J = -1;
 }
 
-__global__ __launch_bounds__(kBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm, BaCam cam) {
+__global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm, BaCam cam) {
   extern __shared__ double sY[];  // [3 LPC][NR + 2], then per-observation terms, then L factors
   const BaWin v = view(ws, dm, blockIdx.x);
   const BaState* S = v.st;
@@ -540,13 +543,13 @@ __global__ __launch_bounds__(kBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm,
 #pragma unroll
   for (int lt = 0; lt < kLinMaxTiles; ++lt) acc[lt][0] = acc[lt][1] = d4{0.0, 0.0, 0.0, 0.0};
   for (int c = part; c * LPC < L; c += dm.NPART) {
-    for (int i = threadIdx.x; i < rows * NRP; i += kBlock) sY[i] = 0.0;
+    for (int i = threadIdx.x; i < rows * NRP; i += kLinBlock) sY[i] = 0.0;
     __syncthreads();
     // the chunk's observations are contiguous (landmark-major): [ob0, ob1)
     const int lc0 = c * LPC, lc1 = min(L, lc0 + LPC);
     const int ob0 = v.lstart[lc0], nob = v.lstart[lc1] - ob0;
     // (a) per observation: its landmark-block terms w Jl^T Jl (upper 6) and w Jl^T r (3)
-    for (int i = threadIdx.x; i < nob; i += kBlock) {
+    for (int i = threadIdx.x; i < nob; i += kLinBlock) {
       const BaObs o = v.obs[ob0 + i];
       double r[3], w, rho, Jp[3][6], Jl[3][3];
       ba_eval<true>(S->T[o.frame], X + 3 * o.lm, o, cam, obs_is2(in, o), r, w, rho, Jp, Jl);
@@ -588,7 +591,7 @@ __global__ __launch_bounds__(kBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm,
     }
     __syncthreads();
     // (c) per observation: rows 6 (f-1) .. 6 (f-1) + 5 of W L^-T (solve L y = W_p)
-    for (int i = threadIdx.x; i < nob; i += kBlock) {
+    for (int i = threadIdx.x; i < nob; i += kLinBlock) {
       const BaObs o = v.obs[ob0 + i];
       const int f = o.frame;
       if (f == 0) continue;
@@ -611,7 +614,7 @@ __global__ __launch_bounds__(kBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm,
     // G += Yt^T Yt on MFMA: A[i][k] = Yt[k][16I + i], B[k][j] = Yt[k][16J + j], lane holds k = lane >> 4
 #pragma unroll
     for (int lt = 0; lt < kLinMaxTiles; ++lt) {
-      const int k = 4 * lt + wid;
+      const int k = kLinWaves * lt + wid;
       if (k < ntiles) {
         int I, J;
         lin_tile(k, ntu, NT, I, J);
@@ -629,7 +632,7 @@ __global__ __launch_bounds__(kBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm,
   double* Gc = v.Gp + (int64_t)part * NR * NR;
 #pragma unroll
   for (int lt = 0; lt < kLinMaxTiles; ++lt) {
-    const int k = 4 * lt + wid;
+    const int k = kLinWaves * lt + wid;
     if (k < ntiles) {
       int I, J;
       lin_tile(k, ntu, NT, I, J);
@@ -1027,7 +1030,7 @@ int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* mat
         hipLaunchKernelGGL(k_ba_setcost, dim3(nwin), dim3(64), 0, s, ws, d, 0);
       }
       hipLaunchKernelGGL(k_ba_pp, gfr, dim3(kBlock), 0, s, in, ws, d, cam);
-      hipLaunchKernelGGL(k_ba_lin, gch, dim3(kBlock), shl, s, in, ws, d, cam);
+      hipLaunchKernelGGL(k_ba_lin, gch, dim3(kLinBlock), shl, s, in, ws, d, cam);
       hipLaunchKernelGGL(k_ba_solve, dim3(nwin), dim3(kBlock), shs, s, ws, d);
       hipLaunchKernelGGL(k_ba_upd, gcu, dim3(kBlock), 0, s, in, ws, d, cam);
       hipLaunchKernelGGL(k_ba_accept, dim3(nwin), dim3(64), 0, s, ws, d);
