@@ -146,7 +146,17 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   __shared__ uint16_t s_list[kFH * kFW];
   __shared__ uint16_t s_pre[kFH * kFW];
   __shared__ int s_n, s_npre;
-  const int b = blockIdx.y, t = blockIdx.x;
+  // XCD-aware tile order: dispatch sends linear block L to XCD L mod 8, so logical tiles are
+  // handed out in 8 contiguous ranges, one per XCD -- the tiles whose staged rows share cache
+  // lines (their 4-px aprons) then meet in the same L2 instead of being fetched by two XCDs
+  int b, t;
+  {
+    const int nt = gridDim.x, N = nt * gridDim.y, L = blockIdx.y * nt + blockIdx.x;
+    const int per = N >> 3;
+    const int lg = L < (per << 3) ? (L & 7) * per + (L >> 3) : L;
+    b = lg / nt;
+    t = lg - b * nt;
+  }
   const int l = tile_level(G, t);
   const int lt = t - G.tile0[l];
   const int tx = lt % G.ntx[l], ty = lt / G.ntx[l];
