@@ -200,6 +200,22 @@ int fvo_alloc(fvo_ctx* ctx, T** p, size_t n) {
 // ---------------------------------------------------------------- device helpers
 __device__ __forceinline__ int wave_lane() { return (int)(threadIdx.x & 63); }
 
+// XCD-aware block order.  Dispatch sends linear block L to XCD L mod 8, so neighbouring
+// blocks (which read overlapping image rows / patches) would land in 8 different L2s; the
+// logical index returned here hands each XCD one contiguous eighth of the grid instead.
+struct XcdBlock {
+  int x, y, z;
+};
+__device__ __forceinline__ XcdBlock xcd_block() {
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int N = gx * gy * gridDim.z;
+  const int L = (blockIdx.z * gy + blockIdx.y) * gx + blockIdx.x;
+  const int per = N >> 3;
+  const int lg = L < (per << 3) ? (L & 7) * per + (L >> 3) : L;
+  const int t = lg / gx;
+  return XcdBlock{lg - t * gx, t % gy, t / gy};
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -83,8 +83,9 @@ constexpr int kResRows = 4;
 __global__ void k_resize(const OrbDev G, uint8_t* __restrict__ pyr, int64_t total, int l, const int32_t* __restrict__ xofs,
                          const int32_t* __restrict__ xc1, const int32_t* __restrict__ yofs,
                          const int32_t* __restrict__ yc1) {
-  int x = blockIdx.x * blockDim.x + threadIdx.x;
-  int b = blockIdx.z;
+  const XcdBlock xb = xcd_block();  // blocks sharing source rows on one XCD
+  int x = xb.x * blockDim.x + threadIdx.x;
+  int b = xb.z;
   int w = G.w[l], h = G.h[l];
   if (x >= w) return;
   int sw = G.w[l - 1], sh = G.h[l - 1];
@@ -99,7 +100,7 @@ __global__ void k_resize(const OrbDev G, uint8_t* __restrict__ pyr, int64_t tota
   };
 #pragma unroll
   for (int k = 0; k < kResRows; ++k) {
-    const int y = blockIdx.y * kResRows + k;
+    const int y = xb.y * kResRows + k;
     if (y >= h) break;
     int oy = yofs[y];
     uint32_t v;
@@ -146,17 +147,10 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   __shared__ uint16_t s_list[kFH * kFW];
   __shared__ uint16_t s_pre[kFH * kFW];
   __shared__ int s_n, s_npre;
-  // XCD-aware tile order: dispatch sends linear block L to XCD L mod 8, so logical tiles are
-  // handed out in 8 contiguous ranges, one per XCD -- the tiles whose staged rows share cache
-  // lines (their 4-px aprons) then meet in the same L2 instead of being fetched by two XCDs
-  int b, t;
-  {
-    const int nt = gridDim.x, N = nt * gridDim.y, L = blockIdx.y * nt + blockIdx.x;
-    const int per = N >> 3;
-    const int lg = L < (per << 3) ? (L & 7) * per + (L >> 3) : L;
-    b = lg / nt;
-    t = lg - b * nt;
-  }
+  // XCD-aware tile order (xcd_block): tiles whose staged aprons share cache lines meet in
+  // one L2 instead of being fetched by two XCDs
+  const XcdBlock xb = xcd_block();
+  const int b = xb.y, t = xb.x;
   const int l = tile_level(G, t);
   const int lt = t - G.tile0[l];
   const int tx = lt % G.ntx[l], ty = lt / G.ntx[l];
@@ -587,7 +581,8 @@ __global__ __launch_bounds__(kSelThreads) void k_select(const OrbDev G, typename
 __global__ void k_harris(const OrbDev G, const uint8_t* __restrict__ pyr, const uint32_t* __restrict__ cand,
                          const int32_t* __restrict__ nsel, uint64_t* __restrict__ hel, int64_t total,
                          int64_t cand_total, int nlevels) {
-  int l = blockIdx.y, b = blockIdx.z;
+  const XcdBlock xb = xcd_block();  // one (image, level)'s blocks on one XCD: shared patches in one L2
+  int l = xb.y, b = xb.z;
   int n = nsel[b * nlevels + l];
   int wpb = blockDim.x >> 6;
   int lane = wave_lane();
@@ -595,7 +590,7 @@ __global__ void k_harris(const OrbDev G, const uint8_t* __restrict__ pyr, const 
   int w = G.w[l];
   const uint32_t* cin = cand + b * cand_total + G.cand_off[l];
   uint64_t* hout = hel + b * cand_total + G.cand_off[l];
-  for (int i = blockIdx.x * wpb + (threadIdx.x >> 6); i < n; i += gridDim.x * wpb) {
+  for (int i = xb.x * wpb + (threadIdx.x >> 6); i < n; i += gridDim.x * wpb) {
     uint32_t e = cin[i];
     int x0 = e & 0xFFF, y0 = (e >> 12) & 0xFFF;
     int A = 0, B = 0, C = 0;
@@ -654,7 +649,8 @@ __device__ __forceinline__ float fast_atan2_deg(float y, float x) {
 __global__ void k_angle(const OrbDev G, const uint8_t* __restrict__ pyr, const uint64_t* __restrict__ hel,
                         const int32_t* __restrict__ nsel2, const int32_t* __restrict__ koff, float* __restrict__ kp,
                         int64_t total, int64_t cand_total, int nlevels, int cap, int patch) {
-  int l = blockIdx.y, b = blockIdx.z;
+  const XcdBlock xb = xcd_block();
+  int l = xb.y, b = xb.z;
   int n = nsel2[b * nlevels + l];
   int base = koff[b * (nlevels + 1) + l];
   int wpb = blockDim.x >> 6, lane = wave_lane();
@@ -662,7 +658,7 @@ __global__ void k_angle(const OrbDev G, const uint8_t* __restrict__ pyr, const u
   int w = G.w[l];
   const uint64_t* hin = hel + b * cand_total + G.cand_off[l];
   const int half = patch / 2;
-  for (int i = blockIdx.x * wpb + (threadIdx.x >> 6); i < n; i += gridDim.x * wpb) {
+  for (int i = xb.x * wpb + (threadIdx.x >> 6); i < n; i += gridDim.x * wpb) {
     if (base + i >= cap) break;
     uint64_t e = hin[i];
     int x0 = (int)(e & 0xFFF), y0 = (int)((e >> 12) & 0xFFF);
@@ -782,13 +778,14 @@ __global__ __launch_bounds__(256) void k_brief(const OrbDev G, const uint8_t* __
                                                uint8_t* __restrict__ desc, int64_t total, int cap) {
   __shared__ uint8_t s_src[4][kBrS][kBrSW];
   __shared__ uint8_t s_blr[4][kBrP][kBrPW];
-  const int b = blockIdx.y;
+  const XcdBlock xb = xcd_block();  // one image's blocks on one XCD: overlapping patches in one L2
+  const int b = xb.y;
   const int n = counts[b];
   if (n < 0) return;
   const int wpb = blockDim.x >> 6, lane = wave_lane(), wv = threadIdx.x >> 6;
   uint8_t(*src)[kBrSW] = s_src[wv];
   uint8_t(*blr)[kBrPW] = s_blr[wv];
-  for (int j = blockIdx.x * wpb + wv; j < n; j += gridDim.x * wpb) {
+  for (int j = xb.x * wpb + wv; j < n; j += gridDim.x * wpb) {
     const float* k = kp + ((int64_t)b * cap + j) * FVO_KP_STRIDE;
     const int l = (int)k[5];
     const float scale = 1.f / G.scale[l];

@@ -175,8 +175,9 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
   __shared__ __attribute__((aligned(16))) uint16_t sPC[kCX][D];    // pixel cost
   const int tid = threadIdx.x, lane = tid & 63, q = lane % G;
   const int col = (tid >> 6) * (64 / G) + lane / G;  // 0..CB-1
-  const int c0 = blockIdx.x * CB;
-  const int s = blockIdx.y, b = blockIdx.z;
+  const XcdBlock xb = xcd_block();  // neighbouring column blocks (shared image rows) on one XCD
+  const int c0 = xb.x * CB;
+  const int s = xb.y, b = xb.z;
   const int H = p.H, W = p.W;
   const int start = max(min(s * p.ss - p.ov, H), 0);
   const int end = min((s + 1) * p.ss, H);
