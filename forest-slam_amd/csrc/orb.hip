@@ -77,40 +77,42 @@ __global__ void k_copy_level0_v(const uint4* __restrict__ img, int64_t stride16,
   }
 }
 
-// INTER_LINEAR_EXACT level l from level l-1; a block covers 256 columns x 4 rows (the column
-// tables are read once per thread)
+// INTER_LINEAR_EXACT level l from level l-1; a block covers 256 columns x kResRows rows (the
+// column tables are read once per thread).  The border cases are folded into the weights
+// (a clamped source index with weights 256 / 0 gives exactly the border formulas: s << 8 for
+// a column, (h + 128) >> 8 = (256 h + 32768) >> 16 for a row), so every load is unconditional
+// and the kResRows rows' loads are all in flight at once.
 constexpr int kResRows = 4;
 __global__ void k_resize(const OrbDev G, uint8_t* __restrict__ pyr, int64_t total, int l, const int32_t* __restrict__ xofs,
                          const int32_t* __restrict__ xc1, const int32_t* __restrict__ yofs,
                          const int32_t* __restrict__ yc1) {
   const XcdBlock xb = xcd_block();  // blocks sharing source rows on one XCD
-  int x = xb.x * blockDim.x + threadIdx.x;
-  int b = xb.z;
-  int w = G.w[l], h = G.h[l];
+  const int x = xb.x * blockDim.x + threadIdx.x;
+  const int b = xb.z;
+  const int w = G.w[l], h = G.h[l];
   if (x >= w) return;
-  int sw = G.w[l - 1], sh = G.h[l - 1];
+  const int sw = G.w[l - 1], sh = G.h[l - 1];
   const uint8_t* src = pyr + b * total + G.off[l - 1];
   uint8_t* dst = pyr + b * total + G.off[l];
-  int ox = xofs[x], cx1 = xc1[x], cx0 = 256 - cx1;
-  auto hrow = [&](int r) -> uint32_t {
-    const uint8_t* s = src + (int64_t)r * sw;
-    if (ox == -1) return (uint32_t)s[0] << 8;
-    if (ox == -2) return (uint32_t)s[sw - 1] << 8;
-    return (uint32_t)cx0 * s[ox] + (uint32_t)cx1 * s[ox + 1];
-  };
+  const int ox = xofs[x];
+  const int oxa = ox >= 0 ? ox : (ox == -1 ? 0 : sw - 1), oxb = ox >= 0 ? ox + 1 : oxa;
+  const uint32_t cx1 = ox >= 0 ? (uint32_t)xc1[x] : 0u, cx0 = 256u - cx1;
+  uint32_t v[kResRows];
+#pragma unroll
+  for (int k = 0; k < kResRows; ++k) {
+    const int y = min(xb.y * kResRows + k, h - 1);
+    const int oy = yofs[y];
+    const int ra = oy >= 0 ? oy : (oy == -1 ? 0 : sh - 1), rb = oy >= 0 ? oy + 1 : ra;
+    const uint32_t cy1 = oy >= 0 ? (uint32_t)yc1[y] : 0u, cy0 = 256u - cy1;
+    const uint8_t* sa = src + (int64_t)ra * sw;
+    const uint8_t* sb = src + (int64_t)rb * sw;
+    const uint32_t ha = cx0 * sa[oxa] + cx1 * sa[oxb], hb = cx0 * sb[oxa] + cx1 * sb[oxb];
+    v[k] = (ha * cy0 + hb * cy1 + 32768u) >> 16;
+  }
 #pragma unroll
   for (int k = 0; k < kResRows; ++k) {
     const int y = xb.y * kResRows + k;
-    if (y >= h) break;
-    int oy = yofs[y];
-    uint32_t v;
-    if (oy < 0) {
-      v = (hrow(oy == -1 ? 0 : sh - 1) + 128u) >> 8;
-    } else {
-      int cy1 = yc1[y], cy0 = 256 - cy1;
-      v = (hrow(oy) * (uint32_t)cy0 + hrow(oy + 1) * (uint32_t)cy1 + 32768u) >> 16;
-    }
-    dst[(int64_t)y * w + x] = (uint8_t)(v > 255u ? 255u : v);
+    if (y < h) dst[(int64_t)y * w + x] = (uint8_t)(v[k] > 255u ? 255u : v[k]);
   }
 }
 
