@@ -670,12 +670,32 @@ __global__ void k_angle(const OrbDev G, const uint8_t* __restrict__ pyr, const u
     int u = lane - half;
     if (lane <= 2 * half) {
       m10 += u * c[u];
-      for (int v = 1; v <= half; ++v) {
-        int d = c_umax[v];
-        if (u >= -d && u <= d) {
-          int vp = c[u + v * w], vm = c[u - v * w];
-          m01 += v * (vp - vm);
-          m10 += u * (vp + vm);
+      if (half == 15) {
+        // the usual patch (31): every row's two bytes loaded unconditionally (keypoints lie at
+        // least edgeThreshold >= 15 px inside the level) and masked by the circle afterwards,
+        // so the 30 loads are in flight together instead of one round trip per row
+        int vp[15], vm[15];
+#pragma unroll
+        for (int v = 1; v <= 15; ++v) {
+          vp[v - 1] = c[u + v * w];
+          vm[v - 1] = c[u - v * w];
+        }
+#pragma unroll
+        for (int v = 1; v <= 15; ++v) {
+          const int d = c_umax[v];
+          if (u >= -d && u <= d) {
+            m01 += v * (vp[v - 1] - vm[v - 1]);
+            m10 += u * (vp[v - 1] + vm[v - 1]);
+          }
+        }
+      } else {
+        for (int v = 1; v <= half; ++v) {
+          int d = c_umax[v];
+          if (u >= -d && u <= d) {
+            int vp = c[u + v * w], vm = c[u - v * w];
+            m01 += v * (vp - vm);
+            m10 += u * (vp + vm);
+          }
         }
       }
     }
@@ -798,11 +818,25 @@ __global__ __launch_bounds__(256) void k_brief(const OrbDev G, const uint8_t* __
     const int w = G.w[l], h = G.h[l];
     const uint8_t* im = pyr + b * total + G.off[l];
     const int sx0 = cx - kBrR - 3, sy0 = cy - kBrR - 3;
-    for (int i = lane; i < kBrS * kBrS; i += 64) {
-      const int r = i / kBrS, c = i - r * kBrS;
-      const int y = reflect101(min(sy0 + r, 2 * (h - 1)), h);
-      const int x = reflect101(min(sx0 + c, 2 * (w - 1)), w);
-      src[r][c] = im[(int64_t)y * w + x];
+    // the 45 x 45 patch in two batches of 16 unconditional byte loads per lane (the tail
+    // slots re-read the last byte and are not stored), each batch in flight together
+    constexpr int kBrN = kBrS * kBrS, kBrIt = (kBrN + 63) / 64;
+#pragma unroll
+    for (int i0 = 0; i0 < kBrIt; i0 += 16) {
+      uint32_t pv[16];
+#pragma unroll
+      for (int k2 = 0; k2 < 16; ++k2) {
+        const int i = min(lane + 64 * (i0 + k2), kBrN - 1);
+        const int r = i / kBrS, c = i - r * kBrS;
+        const int y = reflect101(min(sy0 + r, 2 * (h - 1)), h);
+        const int x = reflect101(min(sx0 + c, 2 * (w - 1)), w);
+        pv[k2] = im[(int64_t)y * w + x];
+      }
+#pragma unroll
+      for (int k2 = 0; k2 < 16; ++k2) {
+        const int i = lane + 64 * (i0 + k2);
+        if (i0 + k2 < kBrIt && i < kBrN) (&src[0][0])[(i / kBrS) * kBrSW + i % kBrS] = (uint8_t)pv[k2];
+      }
     }
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
