@@ -212,6 +212,7 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=4, help="CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-ate", type=int, default=1, help="ATE of the CPU reference path on the ATE frames")
     ap.add_argument("--overlap-sgbm", type=int, default=1, help="SGBM of step k+1 on a side stream during step k")
+    ap.add_argument("--sgbm-last", type=int, default=0, help="front stage order: ORB + BF first, SGBM last (1)")
     ap.add_argument("--main-priority", type=int, default=0, help="HIP stream priority of the main path (-1 = high)")
     ap.add_argument("--sgbm-priority", type=int, default=0, help="HIP stream priority of the overlapped SGBM stream")
     ap.add_argument("--ba-max-landmarks", type=int, default=0, help="per-window landmark cap (0 = library default)")
@@ -256,7 +257,8 @@ def main():
         sgbm_cus = list(range(k)) if kind == "first" else [c for c in range(ncu) if c % k != k - 1]
     fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=B, nfeatures=args.nfeatures, device=dev,
                            ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm),
-                           sgbm_priority=args.sgbm_priority, sgbm_cus=sgbm_cus, **ba_caps)
+                           sgbm_priority=args.sgbm_priority, sgbm_cus=sgbm_cus, sgbm_last=bool(args.sgbm_last),
+                           **ba_caps)
     fe.prime(L_all[0], R_all[0])
     # Steps walk the rendered frames forward (1..B) then backward (B-1..0) and so on, so every
     # frame pair the front end sees -- including the carried pair across a step boundary -- is

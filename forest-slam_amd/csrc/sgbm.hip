@@ -553,8 +553,9 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
 #pragma unroll
       for (int i = SEG - 1; i >= 0; --i) {
         if (i <= ihi) lmin = step16<PQ>(lst, Cs[h][i], q, P1, lmin, p.P2);
+        // L + V at once (u16 sums, order-free): V's registers are free before the R path
 #pragma unroll
-        for (int kk = 0; kk < PQ; ++kk) Ls[i][kk] = lst[kk];
+        for (int kk = 0; kk < PQ; ++kk) Ls[i][kk] = as_u(as_v(lst[kk]) + as_v(Vs[i][kk]));
       }
 #pragma unroll
       for (int i = 0; i < SEG; ++i) {
@@ -566,7 +567,7 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
         uint32_t kmin = 0xFFFFFFFFu;
 #pragma unroll
         for (int kk = 0; kk < PQ; ++kk) {
-          Sw[kk] = as_u(as_v(Ls[i][kk]) + as_v(Rst[kk]) + as_v(Vs[i][kk]));
+          Sw[kk] = as_u(as_v(Ls[i][kk]) + as_v(Rst[kk]));
           const uint32_t d0 = (uint32_t)(q * DQ + 2 * kk);
           kmin = min(kmin, ((Sw[kk] & 0xFFFFu) << 7) | d0);
           kmin = min(kmin, ((Sw[kk] >> 16) << 7) | (d0 + 1));

@@ -36,7 +36,7 @@ class StereoFrontEnd:
     def __init__(self, width: int, height: int, K: np.ndarray, dist: np.ndarray, baseline: float, batch: int,
                  nfeatures: int = 500, match_right: bool = True, device=None, ba_window: int = 10,
                  ba_iters: int = 10, overlap_sgbm: bool = False, sgbm_priority: int = 0, sgbm_cus=None,
-                 **params):
+                 sgbm_last: bool = False, **params):
         self.B = batch
         self.K = np.asarray(K, np.float64)
         self.dist = np.resize(np.asarray(dist, np.float64), 5)
@@ -103,6 +103,9 @@ class StereoFrontEnd:
         # The step inputs must then be complete when step() is called (resident in HBM, or
         # pass inputs_ready).  Default: everything in order on the caller's stream.
         self.overlap_sgbm = bool(overlap_sgbm)
+        # sgbm_last: order of the front stage -- ORB + BF first, SGBM last (the stage whose waves
+        # hold the most VGPRs then starts after the back stage of the previous step has begun)
+        self.sgbm_last = bool(sgbm_last)
         # sgbm_cus: the compute units the front stream may use (None = all)
         if self.overlap_sgbm and sgbm_cus is not None:
             self.s_sgbm = _lib.cu_masked_stream(sgbm_cus, dev)
@@ -160,14 +163,8 @@ class StereoFrontEnd:
                 R.record_stream(fs)
         with torch.cuda.stream(fs):
             # ---- front stage: SGBM of the previous pairs (needs only images), ORB + BF
-            self.prevL[0].copy_(self.sg_lastL)
-            self.prevR[0].copy_(self.sg_lastR)
-            if n > 1:
-                self.prevL[1:n].copy_(L[:n - 1])
-                self.prevR[1:n].copy_(R[:n - 1])
-            self.sg_lastL.copy_(L[n - 1])
-            self.sg_lastR.copy_(R[n - 1])
-            disp = ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n])
+            if not self.sgbm_last:
+                disp = self._front_sgbm(L, R, n)
             self.imgs[:n].copy_(L)
             self.imgs[n:2 * n].copy_(R)
             kp, desc, cnt = ctx.orb(self.imgs[:2 * n], out=(self.kp[:2 * n], self.desc[:2 * n], self.cnt[:2 * n]))
@@ -194,6 +191,8 @@ class StereoFrontEnd:
             self.last_desc[1].copy_(desc[2 * n - 1])
             self.last_cnt[0:1].copy_(cnt[n - 1:n])
             self.last_cnt[1:2].copy_(cnt[2 * n - 1:2 * n])
+            if self.sgbm_last:
+                disp = self._front_sgbm(L, R, n)
         if self.overlap_sgbm:
             main.wait_stream(fs)
         # ---- back stage: back-projection, PnP, local BA
@@ -213,6 +212,17 @@ class StereoFrontEnd:
             self.main_done[slot] = main.record_event()
         self.k += 1
         return out, st
+
+    def _front_sgbm(self, L, R, n):
+        """SGBM of the step's previous pairs (the last pair of the previous step, then L/R[:n-1])."""
+        self.prevL[0].copy_(self.sg_lastL)
+        self.prevR[0].copy_(self.sg_lastR)
+        if n > 1:
+            self.prevL[1:n].copy_(L[:n - 1])
+            self.prevR[1:n].copy_(R[:n - 1])
+        self.sg_lastL.copy_(L[n - 1])
+        self.sg_lastR.copy_(R[n - 1])
+        return self.ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n])
 
     def _select(self, slot: int):
         """Point the per-step buffer names at one of the two slots."""
