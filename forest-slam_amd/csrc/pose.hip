@@ -509,6 +509,59 @@ __device__ __forceinline__ void jacobi12_sweeps_group(double* __restrict__ u, do
   }
 }
 
+// The same sweeps with V by a whole wave (the refinement's single DLT per frame, where the
+// 8-lane group's sweeps were the kernel's critical path: 60 sweeps x 21 dependent steps).
+// 8 lanes per pair of an anti-diagonal: the pair's 8 lanes form its three dot products
+// redundantly (the same sequential sums, hence the same rotation), then each rotates rows
+// sl and sl + 8 of u and v -- every element gets the group version's arithmetic.
+__device__ void jacobi12_sweeps_wave(double* __restrict__ u, double* __restrict__ v) {
+  const int lane = threadIdx.x & 63, pr = lane >> 3, sl = lane & 7;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0;
+#pragma nounroll
+    for (int d = 1; d <= 21; ++d) {
+      const int p0 = d > 11 ? d - 11 : 0;
+      const int cnt = (d - 1) / 2 - p0 + 1;
+      if (pr < cnt) {
+        const int p = p0 + pr, q = d - p;
+        double a = 0, bb = 0, g = 0;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          const double up = u[i * 12 + p], uq = u[i * 12 + q];
+          a += up * up;
+          bb += uq * uq;
+          g += up * uq;
+        }
+        if (!(g == 0.0 || fabs(g) <= 1e-300)) {
+          const double rel = fabs(g) / sqrt(a * bb);
+          off = fmax(off, rel);
+          if (!(rel < 1e-15)) {
+            const double zeta = (bb - a) / (2.0 * g);
+            const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+            const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              const int i = sl + 8 * k;
+              if (i < 12) {
+                const double up = u[i * 12 + p], uq = u[i * 12 + q];
+                u[i * 12 + p] = c * up - sn * uq;
+                u[i * 12 + q] = sn * up + c * uq;
+                const double vp = v[i * 12 + p], vq = v[i * 12 + q];
+                v[i * 12 + p] = c * vp - sn * vq;
+                v[i * 12 + q] = sn * vp + c * vq;
+              }
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) off = fmax(off, __shfl_xor(off, o, 64));
+    if (off < 1e-15) break;
+  }
+}
+
 __device__ __forceinline__ void jacobi12_null4_group(double* __restrict__ u, int l, double* __restrict__ out) {
   jacobi12_sweeps_group<false>(u, nullptr, l);
   if (l != 0) return;
@@ -535,7 +588,7 @@ __device__ __forceinline__ void jacobi12_null4_group(double* __restrict__ u, int
 
 // Right singular vector of the smallest singular value of the symmetric 12x12 DLT matrix
 // (packed upper triangle LLp, identical on every lane) -- column 11 of dsvd_ws<12,12>'s V,
-// with dsvd_ws's exact arithmetic -- by lanes 0..7 of the wave on LDS work arrays u, v [144].
+// with dsvd_ws's exact arithmetic -- by the whole wave on LDS work arrays u, v [144].
 // Returns the vector on every lane.
 __device__ void dlt12_null(const double* LLp, double* __restrict__ u, double* __restrict__ v, double* out) {
   const int lane = threadIdx.x & 63;
@@ -550,7 +603,7 @@ __device__ void dlt12_null(const double* LLp, double* __restrict__ u, double* __
       }
   }
   __syncthreads();
-  if (lane < 8) jacobi12_sweeps_group<true>(u, v, lane);
+  jacobi12_sweeps_wave(u, v);
   __syncthreads();
   // the smallest column norm, the last one in dsvd_ws's stable descending order
   double w[12];
