@@ -478,13 +478,15 @@ __device__ __forceinline__ void jacobi12_sweeps_group(double* __restrict__ u, do
           bb += uq * uq;
           g += up * uq;
         }
+        // the rotation is formed before the tests that gate it, so its sqrt / div chain
+        // overlaps the one of rel (same expressions: the values used are unchanged)
+        const double zeta = (bb - a) / (2.0 * g);
+        const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
         if (!(g == 0.0 || fabs(g) <= 1e-300)) {
           const double rel = fabs(g) / sqrt(a * bb);
           off = fmax(off, rel);
           if (!(rel < 1e-15)) {
-            const double zeta = (bb - a) / (2.0 * g);
-            const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-            const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
 #pragma unroll
             for (int i = 0; i < 12; ++i) {
               const double up = u[i * 12 + p], uq = u[i * 12 + q];
@@ -532,13 +534,15 @@ __device__ void jacobi12_sweeps_wave(double* __restrict__ u, double* __restrict_
           bb += uq * uq;
           g += up * uq;
         }
+        // the rotation is formed before the tests that gate it, so its sqrt / div chain
+        // overlaps the one of rel (same expressions: the values used are unchanged)
+        const double zeta = (bb - a) / (2.0 * g);
+        const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
         if (!(g == 0.0 || fabs(g) <= 1e-300)) {
           const double rel = fabs(g) / sqrt(a * bb);
           off = fmax(off, rel);
           if (!(rel < 1e-15)) {
-            const double zeta = (bb - a) / (2.0 * g);
-            const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-            const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
               const int i = sl + 8 * k;
