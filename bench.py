@@ -41,14 +41,41 @@ def algorithmic_bytes_per_frame(W: int, H: int, N: int) -> int:
     return 4 * W * H + 254 * N
 
 
-def cpu_threads() -> int:
-    """Threads the CPU legs use: the GPU box's CPU share is 16 (its os.cpu_count() reports the
-    whole machine), so at most 16; this container has 8."""
-    return max(1, min(16, os.cpu_count() or 1))
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup (v2 cpu.max "quota period", v1 cfs files), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_threads() -> tuple[int, str]:
+    """Threads the CPU legs use, and how that number was derived: the cgroup CPU quota when
+    one is set, else the affinity mask, capped by OMP_NUM_THREADS when the environment sets it
+    (the GPU box exports 16 = its CPU share while os.cpu_count() reports the whole machine)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = cgroup_cpu_quota()
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    n, why = aff, f"affinity mask ({aff} CPUs)"
+    if quota:
+        n, why = max(1, int(quota)), f"cgroup cpu quota {quota:g} CPUs (affinity {aff})"
+    if omp.isdigit() and 0 < int(omp) < n:
+        n, why = int(omp), why + f", capped by OMP_NUM_THREADS={omp}"
+    return n, why
 
 
 def host_cpus() -> dict:
-    """What the host reports (stated beside the thread count used, VERDICT r1)."""
+    """What the host reports (stated beside the thread count used, VERDICT r1/r2)."""
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -59,32 +86,36 @@ def host_cpus() -> dict:
     except OSError:
         pass
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
-    return {"os_cpu_count": os.cpu_count(), "affinity": aff, "model": model,
+    return {"os_cpu_count": os.cpu_count(), "affinity": aff, "cgroup_quota": cgroup_cpu_quota(), "model": model,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
-def cpu_baseline(n_frames: int, nfeatures: int, W: int, H: int) -> dict:
+def cpu_baseline(n_frames: int, nfeatures: int, W: int, H: int, ba_window: int) -> dict:
     """Scalar C++ restatement of the reference CPU path (oracle/) timed on a bounded sample:
-    per frame the reference's full per-iteration work — 4 ORB extractions (prev/cur x L/R),
-    2 BF cross-check matchings, SGBM-3way, back-projection, PnP.  Timed on 1 host thread
-    and with frames spread over `cores` threads (the C calls release the GIL), as
-    SURVEY.md §8(d) asks; `value` is the multi-core rate."""
+    per frame the reference's full per-iteration work -- 4 ORB extractions (prev/cur x L/R),
+    2 BF cross-check matchings, SGBM-3way, back-projection, PnP -- on 1 host thread and with
+    frames spread over `cores` threads (the C calls release the GIL), as SURVEY.md §8(d)
+    asks; `value` is the multi-core rate.  BASELINE.md §2's separate local-BA column: the
+    NumPy float64 BA specification (oracle/ba_ref.py) timed on K-frame windows of the same
+    frames (one window per frame, as the GPU path runs), 1 thread and over the pool."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test/baseline infrastructure only
+    import ba_ref
     from concurrent.futures import ThreadPoolExecutor
     from forest_slam_amd import synth
-    cores = cpu_threads()
-    n_mt = max(n_frames, cores * 2)
+    cores, why = cpu_threads()
+    n_mt = max(n_frames, cores * 2, ba_window + 4)
     rdev = "cuda" if torch.cuda.is_available() else "cpu"  # rendering only; the timed work is host C++
     seq = synth.StereoSequence(seed=0, n_frames=n_mt + 1, W=W, H=H, device=rdev)
     imgs = [tuple(x.cpu().numpy() for x in seq.frame(i)) for i in range(n_mt + 1)]
 
     def one(i):
         (pL, pR), (cL, cR) = imgs[i], imgs[i + 1]
-        oracle.frame_pose(pL, pR, cL, seq.K, synth.DIST_L, synth.BASELINE, nfeatures)
+        out = oracle.frame_pose(pL, pR, cL, seq.K, synth.DIST_L, synth.BASELINE, nfeatures)
         _, dR0 = oracle.orb_detect_compute(pR, nfeatures)
         _, dR1 = oracle.orb_detect_compute(cR, nfeatures)
         oracle.bf_match(dR0, dR1)
+        return out
 
     t0 = time.perf_counter()
     for i in range(n_frames):
@@ -92,13 +123,40 @@ def cpu_baseline(n_frames: int, nfeatures: int, W: int, H: int) -> dict:
     dt1 = time.perf_counter() - t0
     with ThreadPoolExecutor(max_workers=cores) as ex:
         t0 = time.perf_counter()
-        list(ex.map(one, range(n_mt)))
+        pairs = list(ex.map(one, range(n_mt)))
         dtm = time.perf_counter() - t0
-    return {"value": n_mt / dtm, "unit": "frames/s", "cores": cores, "kind": "port",
-            "value_1core": n_frames / dt1, "host_cpus": host_cpus(),
-            "sample": f"{W}x{H} synthetic stereo frames, nfeatures={nfeatures}: 4 ORB + 2 BF-xcheck + "
-                      f"SGBM-3way + back-projection + PnP-RANSAC per frame, oracle/ scalar C++; {n_mt} frames "
-                      f"over {cores} threads in {dtm:.1f} s; {n_frames} frames on 1 thread in {dt1:.1f} s"}
+    res = {"value": n_mt / dtm, "unit": "frames/s", "cores": cores, "cores_from": why, "kind": "port",
+           "value_1core": n_frames / dt1, "host_cpus": host_cpus(),
+           "sample": f"{W}x{H} synthetic stereo frames, nfeatures={nfeatures}: 4 ORB + 2 BF-xcheck + "
+                     f"SGBM-3way + back-projection + PnP-RANSAC per frame, oracle/ scalar C++; {n_mt} frames "
+                     f"over {cores} threads in {dtm:.1f} s; {n_frames} frames on 1 thread in {dt1:.1f} s"}
+    if ba_window:
+        kps = [p["kp0"] for p in pairs] + [pairs[-1]["kp1"]]
+        stereo = [ba_ref.stereo_points(kps[j], pairs[j]["disp16"], seq.K, synth.BASELINE) for j in range(n_mt)]
+        rel = [p["T"] if p["T"] is not None else np.eye(4) for p in pairs]
+        ends = list(range(ba_window - 1, n_mt))
+
+        def win(e):
+            s = e - ba_window + 1
+            return ba_ref.ba_window(kps[s:e + 1], [p["matches"] for p in pairs[s:e]], stereo[s:e], rel[s:e], seq.K,
+                                    synth.BASELINE, iters=10)
+
+        # ba_ref is NumPy on small arrays and holds the GIL, so threads do not scale it (measured:
+        # 8 threads slower than 1): timed on 1 thread; the per-core rate x cores is the bound a
+        # process-parallel CPU run could reach, and that optimistic figure is the one combined
+        n1 = min(2, len(ends))
+        t0 = time.perf_counter()
+        for e in ends[:n1]:
+            win(e)
+        b1 = time.perf_counter() - t0
+        ba_fps1 = n1 / b1
+        ba_fps = ba_fps1 * cores
+        res["local_ba"] = {"value": round(ba_fps, 3), "value_1core": round(ba_fps1, 4), "unit": "windows/s (= frames/s)",
+                           "window": ba_window, "what": "oracle/ba_ref.py (NumPy fp64 LM, 10 iterations) per window; "
+                                                       "value = 1-thread rate x cores (GIL-bound, not run threaded)",
+                           "sample": f"{n1} windows of {ba_window} frames on 1 thread in {b1:.1f} s"}
+        res["value_with_ba"] = round(1.0 / (1.0 / res["value"] + 1.0 / ba_fps), 3)
+    return res
 
 
 def cpu_reference_ate(L_all, R_all, K, stamps, gt, nfeatures: int) -> dict:
@@ -117,7 +175,7 @@ def cpu_reference_ate(L_all, R_all, K, stamps, gt, nfeatures: int) -> dict:
         return oracle.frame_pose(imgs[i - 1][0], imgs[i - 1][1], imgs[i][0], K, synth.DIST_L, synth.BASELINE,
                                  nfeatures)["T"]
 
-    cores = cpu_threads()
+    cores, _ = cpu_threads()
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=cores) as ex:
         Ts = list(ex.map(one, range(1, len(imgs))))
@@ -209,17 +267,11 @@ def main():
     ap.add_argument("--height", type=int, default=600)
     ap.add_argument("--ate-frames", type=int, default=200, help="frames of the ATE run (0 = skip)")
     ap.add_argument("--ba-window", type=int, default=10, help="local BA window K (0 = PnP only)")
-    ap.add_argument("--cpu-frames", type=int, default=4, help="CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-frames", type=int, default=2, help="CPU baseline 1-thread sample (0 = skip)")
     ap.add_argument("--cpu-ate", type=int, default=1, help="ATE of the CPU reference path on the ATE frames")
     ap.add_argument("--overlap-sgbm", type=int, default=1, help="SGBM of step k+1 on a side stream during step k")
-    ap.add_argument("--sgbm-last", type=int, default=0, help="front stage order: ORB + BF first, SGBM last (1)")
-    ap.add_argument("--main-priority", type=int, default=0, help="HIP stream priority of the main path (-1 = high)")
-    ap.add_argument("--sgbm-priority", type=int, default=0, help="HIP stream priority of the overlapped SGBM stream")
     ap.add_argument("--ba-max-landmarks", type=int, default=0, help="per-window landmark cap (0 = library default)")
     ap.add_argument("--ba-max-obs", type=int, default=0, help="per-window observation cap (0 = library default)")
-    ap.add_argument("--sgbm-cus", type=str, default="", help="CUs of the overlapped SGBM stream: 'first:N', "
-                    "'every:K' (all but every K-th CU) or '' (all)")
-    ap.add_argument("--graph", type=int, default=0, help="replay each step as a captured HIP graph (1) or launch eagerly (0)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -233,8 +285,6 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    if args.main_priority:
-        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=args.main_priority))
 
     import forest_slam_amd.build as fbuild
     from forest_slam_amd import eval as ev
@@ -248,17 +298,8 @@ def main():
     L_all, R_all = seq.frames(range(B + 1))
     torch.cuda.synchronize()
     ba_caps = {k: v for k, v in (("ba_max_landmarks", args.ba_max_landmarks), ("ba_max_obs", args.ba_max_obs)) if v}
-    sgbm_cus = None
-    if args.sgbm_cus:
-        from forest_slam_amd import _lib
-        ncu = _lib.load().fvo_device_cu_count()
-        kind, k = args.sgbm_cus.split(":")
-        k = int(k)
-        sgbm_cus = list(range(k)) if kind == "first" else [c for c in range(ncu) if c % k != k - 1]
     fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=B, nfeatures=args.nfeatures, device=dev,
-                           ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm),
-                           sgbm_priority=args.sgbm_priority, sgbm_cus=sgbm_cus, sgbm_last=bool(args.sgbm_last),
-                           **ba_caps)
+                           ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm), **ba_caps)
     fe.prime(L_all[0], R_all[0])
     # Steps walk the rendered frames forward (1..B) then backward (B-1..0) and so on, so every
     # frame pair the front end sees -- including the carried pair across a step boundary -- is
@@ -266,7 +307,10 @@ def main():
     fwd = (L_all[1:].contiguous(), R_all[1:].contiguous())
     bwd = (L_all[:B].flip(0).contiguous(), R_all[:B].flip(0).contiguous())
     from forest_slam_amd import dist as fdist
-    rank_step = fdist.SequenceRank(fe)  # front-end step + (world > 1, local BA) the RCCL map exchange
+    # front-end step + (world > 1, local BA) the RCCL map exchange and the multi-sequence map
+    # built from it (dist.GlobalMap: every rank's window landmarks in its sequence's frame)
+    lm_cap = int(fe.ctx.cfg.ba_max_landmarks)
+    rank_step = fdist.SequenceRank(fe, map_capacity=(args.warmup + args.steps + 4) * world * lm_cap)
     nstep = [0]
 
     def eager_step():
@@ -278,20 +322,6 @@ def main():
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
-    if args.graph and world == 1:
-        # one graph per direction (the inputs alternate between the two static buffers); the
-        # per-kernel breakdown below still launches eagerly (events cannot be recorded inside)
-        graphs = []
-        for d in range(2):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                eager_step()
-            graphs.append(g)
-        torch.cuda.synchronize()
-
-        def step():
-            graphs[nstep[0] % 2].replay()
-            nstep[0] += 1
 
     # per-kernel breakdown (separate pass, every launch bracketed by events).  SGBM runs in
     # order on the main stream here, so no kernel's time includes another stream's kernels
@@ -330,6 +360,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    global_map = None
+    if rank_step.gmap is not None:
+        gm = rank_step.gmap.flush()
+        global_map = {"points": len(gm), "sequences": world, "steps_placed": len(rank_step.gmap.counts),
+                      "what": "every rank's last-BA-window landmarks per step, all-gathered over RCCL and placed "
+                              "with each sequence's chained poses (dist.GlobalMap)"}
     frames = world * B * args.steps
     value = frames / elapsed
     dom_ms, dom_launches = dom_t.get(dom, (0.0, 0))
@@ -379,7 +415,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_frames > 0:
-        cpu = cpu_baseline(args.cpu_frames, args.nfeatures, W, H)
+        cpu = cpu_baseline(args.cpu_frames, args.nfeatures, W, H, args.ba_window)
 
     cfg_name = ("configs[1]" if (W, H, args.nfeatures) == (960, 600, 1000) else
                 "configs[4] (1080p, 2000 kp, BA window 20)" if (W, H) == (1920, 1080) else "custom")
@@ -423,6 +459,7 @@ def main():
             "valu": pmc_valu(shape),
             "pmc_shape": shape,
             "ate": ate,
+            "global_map": global_map,
             "stages_ms_per_step": stage_ms,
             "workspace_gb": round(fe.ctx.workspace_bytes / 1e9, 2),
         }

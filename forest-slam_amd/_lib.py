@@ -68,9 +68,6 @@ SIGNATURES = {
     "fvo_motion_blur": (ctypes.c_int, [_P, _P, _I, _L, _I, _I, ctypes.c_double, _P, _P, _I, _P, _P, _L, _I, _P]),
     "fvo_test_retain_best": (ctypes.c_int, [_P, _P, _I, _I, _P, _P, _P]),
     "fvo_debug_buffer": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
-    "fvo_stream_create_cu_mask": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), _I, ctypes.POINTER(_P)]),
-    "fvo_stream_destroy": (ctypes.c_int, [_P]),
-    "fvo_device_cu_count": (ctypes.c_int, []),
     "fvo_kernel_count": (ctypes.c_int, []),
     "fvo_kernel_name": (ctypes.c_char_p, [ctypes.c_int]),
     "fvo_timing_enable": (ctypes.c_int, [_P, ctypes.c_uint64]),
@@ -482,26 +479,3 @@ class Context:
                                                 _stream(self.device)))
         k = int(nout.item())
         return idx[:k].clone()
-
-
-def cu_masked_stream(cus, device=None) -> "torch.cuda.ExternalStream":
-    """A torch stream (ExternalStream over fvo_stream_create_cu_mask) whose kernels run only
-    on the compute units listed in `cus` (indices into the device's CUs)."""
-    L = load()
-    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-    with torch.cuda.device(dev):
-        n = L.fvo_device_cu_count()
-        if n <= 0:
-            raise RuntimeError("fvo_device_cu_count failed")
-        words = (n + 31) // 32
-        mask = (ctypes.c_uint32 * words)()
-        for c in cus:
-            if not 0 <= c < n:
-                raise ValueError(f"CU {c} outside [0, {n})")
-            mask[c // 32] |= 1 << (c % 32)
-        h = ctypes.c_void_p()
-        if L.fvo_stream_create_cu_mask(mask, words, ctypes.byref(h)) != 0:
-            raise RuntimeError("fvo_stream_create_cu_mask failed")
-        s = torch.cuda.ExternalStream(h.value, device=dev)
-    s._fvo_handle = h  # released by the process (torch does not own external streams)
-    return s

@@ -339,23 +339,6 @@ int fvo_voxel_down_sample(fvo_ctx* c, const double* points, int64_t n_points, do
                    (hipStream_t)stream);
 }
 
-int fvo_stream_create_cu_mask(const uint32_t* cu_mask, int32_t words, fvo_stream* out) {
-  if (!cu_mask || words < 1 || !out) return -1;
-  hipStream_t s = nullptr;
-  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)words, cu_mask) != hipSuccess) return -1;
-  *out = (fvo_stream)s;
-  return 0;
-}
-
-int fvo_stream_destroy(fvo_stream s) { return s && hipStreamDestroy((hipStream_t)s) == hipSuccess ? 0 : -1; }
-
-int fvo_device_cu_count(void) {
-  int dev = 0, n = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return -1;
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
-  return n;
-}
-
 int fvo_kernel_count(void) { return KN_COUNT; }
 
 const char* fvo_kernel_name(int id) {

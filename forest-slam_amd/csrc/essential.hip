@@ -6,7 +6,7 @@
 // k_em_prep         one thread per frame: RANSAC subsets with OpenCV's RNG(-1) (ransac.h) and
 //                   the RANSAC state; normalised fp64 points written once per frame.
 // k_em_hyp          one lane per RANSAC iteration: the 5-point solver (null space of the 5x9
-//                   epipolar system by Householder QR, 10x20 cubic constraints, Gauss-Jordan,
+//                   epipolar system as OpenCV's JacobiSVD builds it, 10x20 cubic constraints, Gauss-Jordan,
 //                   degree-10 det B(z), Durand-Kerner roots as solvePoly, up to 10 models) and
 //                   the float32 Sampson-type error of every model over all points from LDS.
 // k_em_replay       the serial acceptance rule of RANSACPointSetRegistrator::run over
@@ -71,55 +71,130 @@ __device__ __forceinline__ void madd_ql(const double* q, const double* l, double
 }
 
 // ------------------------------------------------------------------ 5-point kernel
+// Null space of the 5x9 epipolar matrix as OpenCV's SVD::compute(Q, ..., FULL_UV) produces
+// it (oracle/essential_ref.cpp null_space_5x9, operation for operation): cyclic one-sided
+// Jacobi on the 5 rows (every pair index static, the sweep loop dynamic), rows sorted by
+// norm, then rows 5..8 built from RNG(0x12345678) sign vectors by two Gram-Schmidt passes
+// with L1 rescales and normalised.  All indices are compile-time, so A stays in VGPRs.
 __device__ void null_space_5x9(const double* Q, double* basis) {
-  double M[9][5];
+  constexpr int m = 9, n = 5;
+  const double eps = DBL_EPSILON * 10, minval = DBL_MIN;
+  double A[9][9];
 #pragma unroll
-  for (int i = 0; i < 9; ++i)
+  for (int i = 0; i < n; ++i)
 #pragma unroll
-    for (int j = 0; j < 5; ++j) M[i][j] = Q[j * 9 + i];
-  double V[5][9];
-  double beta[5];
+    for (int k = 0; k < m; ++k) A[i][k] = Q[i * 9 + k];
+  double W[n];
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    double nrm2 = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double sd = 0;
 #pragma unroll
-    for (int i = k; i < 9; ++i) nrm2 += M[i][k] * M[i][k];
-    double nrm = sqrt(nrm2);
-    double alpha = M[k][k] >= 0.0 ? -nrm : nrm;
+    for (int k = 0; k < m; ++k) sd += A[i][k] * A[i][k];
+    W[i] = sd;
+  }
+  for (int iter = 0; iter < 30; ++iter) {
+    bool changed = false;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) V[k][i] = i < k ? 0.0 : M[i][k];
-    V[k][k] -= alpha;
-    double vv = 0.0;
+    for (int i = 0; i < n - 1; ++i)
 #pragma unroll
-    for (int i = k; i < 9; ++i) vv += V[k][i] * V[k][i];
-    beta[k] = vv > 0.0 ? 2.0 / vv : 0.0;
+      for (int j = i + 1; j < n; ++j) {
+        double a = W[i], p = 0, b = W[j];
 #pragma unroll
-    for (int j = k; j < 5; ++j) {
-      double s = 0.0;
+        for (int k = 0; k < m; ++k) p += A[i][k] * A[j][k];
+        if (!(fabs(p) <= eps * sqrt(a * b))) {
+          p *= 2;
+          const double beta = a - b, gamma = hypot(p, beta);
+          double c, s;
+          if (beta < 0) {
+            const double delta = (gamma - beta) * 0.5;
+            s = sqrt(delta / gamma);
+            c = p / (gamma * s * 2);
+          } else {
+            c = sqrt((gamma + beta) / (gamma * 2));
+            s = p / (gamma * c * 2);
+          }
+          a = b = 0;
 #pragma unroll
-      for (int i = k; i < 9; ++i) s += V[k][i] * M[i][j];
-      s *= beta[k];
-#pragma unroll
-      for (int i = k; i < 9; ++i) M[i][j] -= s * V[k][i];
-    }
+          for (int k = 0; k < m; ++k) {
+            const double t0 = c * A[i][k] + s * A[j][k];
+            const double t1 = -s * A[i][k] + c * A[j][k];
+            A[i][k] = t0;
+            A[j][k] = t1;
+            a += t0 * t0;
+            b += t1 * t1;
+          }
+          W[i] = a;
+          W[j] = b;
+          changed = true;
+        }
+      }
+    if (!changed) break;
   }
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    double e[9];
+  for (int i = 0; i < n; ++i) {
+    double sd = 0;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) e[i] = i == 5 + c ? 1.0 : 0.0;
-#pragma unroll
-    for (int k = 4; k >= 0; --k) {
-      double s = 0.0;
-#pragma unroll
-      for (int i = k; i < 9; ++i) s += V[k][i] * e[i];
-      s *= beta[k];
-#pragma unroll
-      for (int i = k; i < 9; ++i) e[i] -= s * V[k][i];
-    }
-#pragma unroll
-    for (int i = 0; i < 9; ++i) basis[c * 9 + i] = e[i];
+    for (int k = 0; k < m; ++k) sd += A[i][k] * A[i][k];
+    W[i] = sqrt(sd);
   }
+  // selection sort, descending; the swaps are predicated register selects
+#pragma unroll
+  for (int i = 0; i < n - 1; ++i) {
+    int j = i;
+#pragma unroll
+    for (int k = i + 1; k < n; ++k)
+      if (W[j] < W[k]) j = k;
+#pragma unroll
+    for (int k = i + 1; k < n; ++k) {
+      if (j == k) {
+        const double tw = W[i]; W[i] = W[k]; W[k] = tw;
+#pragma unroll
+        for (int e = 0; e < m; ++e) { const double t = A[i][e]; A[i][e] = A[k][e]; A[k][e] = t; }
+      }
+    }
+  }
+  uint64_t rs = 0x12345678u;  // cv::RNG(0x12345678)
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    double sd = i < n ? W[i] : 0;
+    for (int ii = 0; ii < 100 && sd <= minval; ++ii) {
+      const double val0 = 1.0 / m;
+#pragma unroll
+      for (int k = 0; k < m; ++k) {
+        rs = (uint64_t)(unsigned)rs * 4164903690u + (unsigned)(rs >> 32);
+        A[i][k] = ((unsigned)rs & 256) != 0 ? val0 : -val0;
+      }
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+#pragma unroll
+        for (int j = 0; j < i; ++j) {
+          sd = 0;
+#pragma unroll
+          for (int k = 0; k < m; ++k) sd += A[i][k] * A[j][k];
+          double asum = 0;
+#pragma unroll
+          for (int k = 0; k < m; ++k) {
+            const double t = A[i][k] - sd * A[j][k];
+            A[i][k] = t;
+            asum += fabs(t);
+          }
+          asum = asum > eps * 100 ? 1 / asum : 0;
+#pragma unroll
+          for (int k = 0; k < m; ++k) A[i][k] *= asum;
+        }
+      sd = 0;
+#pragma unroll
+      for (int k = 0; k < m; ++k) sd += A[i][k] * A[i][k];
+      sd = sqrt(sd);
+    }
+    const double sc = sd > minval ? 1 / sd : 0.;
+#pragma unroll
+    for (int k = 0; k < m; ++k) A[i][k] *= sc;
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) basis[c * 9 + i] = A[5 + c][i];
 }
 
 template <int NA, int NB>
@@ -441,7 +516,7 @@ __global__ void k_em_prep(const float* __restrict__ p0all, const float* __restri
 
 // ---- the 5-point solver in three launches over the RANSAC subsets of one iteration range
 // (each a different mapping of the same arithmetic as five_point(), operation for operation):
-//   k_em_coef   lane per subset: 5x9 epipolar rows, null-space basis (Householder), the 10x20
+//   k_em_coef   lane per subset: 5x9 epipolar rows, null-space basis (JacobiSVD), the 10x20
 //               cubic-constraint matrix, row by row -> workspace.
 //   k_em_elim   16-lane group per subset: Gauss-Jordan on the 10x20 matrix with a row per lane
 //               (pivot = first maximum found by a group butterfly, rows swapped by relabelling,

@@ -897,6 +897,11 @@ int orb_init(fvo_ctx* ctx) {
   if (c.first_level != 0 || c.wta_k != 2 || c.score_type != 0 || c.patch_size != 31)
     return fvo_fail(ctx, "only firstLevel=0, WTA_K=2, HARRIS_SCORE, patchSize=31 are supported");
   if (c.width > 4095 || c.height > 4095) return fvo_fail(ctx, "image dimensions must be < 4096");
+  // k_angle reads the whole 31x31 square around a keypoint unguarded; keypoints are kept
+  // edgeThreshold px inside the level, so it must cover the half patch (k_brief stages its
+  // rotated patch with REFLECT_101 and needs no such bound)
+  if (c.edge_threshold < c.patch_size / 2)
+    return fvo_fail(ctx, "edgeThreshold must be >= patchSize/2 (15)");
   g.nlevels = c.nlevels;
   const double sf = (double)c.scale_factor;
   int64_t off = 0, coff = 0;

@@ -12,8 +12,9 @@
   shard start on one GPU but not here) are discarded — the previous rank owns those pairs.
   ``frame_shard`` / ``gather_relative_poses``.
 * ``SequenceRank`` — one rank's step of the multi-sequence run (bench.py, tests): the
-  front-end step, the latest BA window's landmarks (``fvo_ba_landmarks``) and the map
-  exchange (``exchange_window_map``).
+  front-end step, the latest BA window's landmarks (``fvo_ba_landmarks``), the map
+  exchange (``exchange_window_map``) and the multi-sequence map built from it
+  (``GlobalMap``).
 * Keyframe exchange for the multi-sequence map: ``allgather_keyframes`` (poses + landmark
   positions, tens of KB: latency-bound, one collective per window step).
 
@@ -68,18 +69,19 @@ def gather_relative_poses(T_local: torch.Tensor, status_local: torch.Tensor, n_p
     return T, S
 
 
-def exchange_window_map(T_step: torch.Tensor, lm_xyz: torch.Tensor, lm_count: torch.Tensor, group=None):
+def exchange_window_map(T_step: torch.Tensor, st_step: torch.Tensor, lm_xyz: torch.Tensor, lm_count: torch.Tensor,
+                        group=None):
     """The per-step map exchange of the multi-sequence run: every rank's
-    BA-refined relative poses of the step (f64 [B,4,4]) and its latest window's landmarks
-    (f64 [Lmax,3] + i32 [1] count, fixed size) are all-gathered over RCCL.  Fixed shapes and
-    device-side counts: no host synchronisation, the collectives queue behind the step's
-    kernels.  Returns (T [world,B,4,4], xyz [world,Lmax,3], counts [world,1]) on the inputs'
-    device.  Under the gloo backend (CPU tests, or GPU ranks sharing one card) the tensors
-    go through host copies."""
+    BA-refined relative poses of the step (f64 [B,4,4]) with their statuses (i32 [B]) and its
+    latest window's landmarks (f64 [Lmax,3] + i32 [1] count, fixed size) are all-gathered over
+    RCCL.  Fixed shapes and device-side counts: no host synchronisation, the collectives queue
+    behind the step's kernels.  Returns (T [world,B,4,4], st [world,B], xyz [world,Lmax,3],
+    counts [world,1]) on the inputs' device.  Under the gloo backend (CPU tests, or GPU ranks
+    sharing one card) the tensors go through host copies."""
     world = dist.get_world_size(group)
     host = dist.get_backend(group) == "gloo" and T_step.is_cuda
     dev = T_step.device
-    ins = [t.contiguous().cpu() if host else t.contiguous() for t in (T_step, lm_xyz, lm_count)]
+    ins = [t.contiguous().cpu() if host else t.contiguous() for t in (T_step, st_step, lm_xyz, lm_count)]
     outs = []
     for t in ins:
         o = [torch.empty_like(t) for _ in range(world)]
@@ -88,28 +90,112 @@ def exchange_window_map(T_step: torch.Tensor, lm_xyz: torch.Tensor, lm_count: to
     return tuple(outs)
 
 
+class MapChain:
+    """Host side of ``GlobalMap``: per rank the chain of the gathered relative poses, composed
+    left to right in float64 exactly as ``eval.chain`` (frames with status -1 or keypoint
+    overflow keep the previous pose, stereo_slam.py:292,306), and the pose that places a
+    step's landmarks.  A step's last BA window ends at frame e and starts at
+    s = max(0, e-K+1) (frame 0 = the primed pair); its landmarks are in camera-s
+    coordinates, and the reference maps points of camera f-1 with the chain through frame f
+    (pair f's points are back-projected from the previous image and transformed by the
+    cumulative pose that already includes T_f, stereo_slam.py:306-310), so they are placed
+    with the chain through s+1."""
+
+    def __init__(self, world: int, window: int):
+        self.world, self.K = int(world), int(window)
+        self.cums = [[np.eye(4)] for _ in range(self.world)]  # cums[r][f]: rank r's chain through frame f
+
+    def advance(self, T: np.ndarray, S: np.ndarray) -> np.ndarray:
+        """T f64 [world,n,4,4], S i32 [world,n] of one step -> landmark poses f64 [world,4,4]."""
+        from .vo import STATUS_KP_OVERFLOW
+        land = []
+        for r in range(self.world):
+            ch = self.cums[r]
+            for i in range(T.shape[1]):
+                ok = S[r, i] != -1 and S[r, i] != STATUS_KP_OVERFLOW
+                ch.append(np.dot(ch[-1], T[r, i]) if ok else ch[-1].copy())
+            e = len(ch) - 1
+            s = max(0, e - self.K + 1)
+            land.append(ch[min(s + 1, e)])
+        return np.stack(land)
+
+
+class GlobalMap:
+    """The multi-sequence map product built from ``exchange_window_map``'s
+    output: every rank's latest-window landmarks placed in its sequence's map frame
+    (``MapChain``) and appended to one ``mapping.PointMap`` -- the reference's
+    ``all_points_3D`` (stereo_slam.py:306-318) for all ranks' sequences at once, one
+    fvo_map_transform launch per step with the ranks' sets in rank order.
+
+    The gathered poses reach the host through pinned buffers copied asynchronously; a step
+    is placed ``lag`` steps later (its copy has long finished), so building the map never
+    stalls the rank's stream.  ``flush`` places what is still queued."""
+
+    def __init__(self, world: int, window: int, capacity: int, device, ctx=None, lag: int = 1):
+        from .mapping import PointMap
+        self.lag = int(lag)
+        self.chain = MapChain(world, window)
+        self.map = PointMap(capacity, device, ctx)
+        self.counts = []  # per placed step: i32 [world] device landmark counts (test / report)
+        self.queue = []
+
+    def push(self, gathered, n: int):
+        Tg, Sg, Xg, Cg = gathered
+        hT = torch.empty(Tg[:, :n].shape, dtype=torch.float64, pin_memory=True)
+        hS = torch.empty(Sg[:, :n].shape, dtype=torch.int32, pin_memory=True)
+        hT.copy_(Tg[:, :n], non_blocking=True)
+        hS.copy_(Sg[:, :n], non_blocking=True)
+        X32 = Xg.to(torch.float32)  # PointCloud2 / fvo_map_transform take float32 xyz
+        cnt = Cg.reshape(-1).to(torch.int32).clone()
+        ev = torch.cuda.current_stream(Tg.device).record_event() if Tg.is_cuda else None
+        self.queue.append((ev, hT, hS, X32, cnt, int(n)))
+        while len(self.queue) > self.lag:
+            self._place(self.queue.pop(0))
+
+    def flush(self):
+        while self.queue:
+            self._place(self.queue.pop(0))
+        return self.map
+
+    def _place(self, item):
+        ev, hT, hS, X32, cnt, n = item
+        if ev is not None:
+            ev.synchronize()
+        land = self.chain.advance(hT.numpy(), hS.numpy())
+        self.map.add_frames(X32, cnt, land)
+        self.counts.append(cnt)
+
+
 class SequenceRank:
     """One rank of the sequence-per-GPU run: ``step`` = the front end's step over the rank's
     next frames, then the exchange of the refined poses and of the latest BA window's
     landmarks with every other rank (``exchange_window_map``; skipped for world size 1 or
-    without local BA).  Returns (T, status, gathered) with gathered = None or the
-    (T, xyz, counts) all-gather result."""
+    without local BA) and, with ``map_capacity`` > 0, their placement in the multi-sequence
+    map (``GlobalMap``; ``self.gmap``).  Returns (T, status, gathered) with gathered = None or
+    the (T, st, xyz, counts) all-gather result."""
 
-    def __init__(self, frontend, group=None):
+    def __init__(self, frontend, group=None, map_capacity: int = 0):
         self.fe = frontend
         self.group = group
-        self.exchange = dist.is_available() and dist.is_initialized() and frontend.ba_window > 0
+        self.exchange = (dist.is_available() and dist.is_initialized() and frontend.ba_window > 0
+                         and dist.get_world_size(group) > 1)
+        self.gmap = None
         if self.exchange:
             dev = frontend.dev
             self.lm_out = (torch.empty((int(frontend.ctx.cfg.ba_max_landmarks), 3), dtype=torch.float64, device=dev),
                            torch.empty((1,), dtype=torch.int32, device=dev))
+            if map_capacity > 0:
+                self.gmap = GlobalMap(dist.get_world_size(group), frontend.ba_window, map_capacity, dev,
+                                      ctx=frontend.ctx)
 
     def step(self, L: torch.Tensor, R: torch.Tensor):
         T, st = self.fe.step(L, R)
         gathered = None
         if self.exchange:
             xyz, cnt = self.fe.ctx.ba_landmarks(L.shape[0] - 1, out=self.lm_out)
-            gathered = exchange_window_map(T, xyz, cnt, self.group)
+            gathered = exchange_window_map(T, st, xyz, cnt, self.group)
+            if self.gmap is not None:
+                self.gmap.push(gathered, L.shape[0])
         return T, st, gathered
 
 

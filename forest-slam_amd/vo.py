@@ -35,8 +35,7 @@ STATUS_KP_OVERFLOW = -3
 class StereoFrontEnd:
     def __init__(self, width: int, height: int, K: np.ndarray, dist: np.ndarray, baseline: float, batch: int,
                  nfeatures: int = 500, match_right: bool = True, device=None, ba_window: int = 10,
-                 ba_iters: int = 10, overlap_sgbm: bool = False, sgbm_priority: int = 0, sgbm_cus=None,
-                 sgbm_last: bool = False, **params):
+                 ba_iters: int = 10, overlap_sgbm: bool = False, **params):
         self.B = batch
         self.K = np.asarray(K, np.float64)
         self.dist = np.resize(np.asarray(dist, np.float64), 5)
@@ -102,15 +101,13 @@ class StereoFrontEnd:
         # bound) of step k, which runs on the caller's stream and joins the front stage first.
         # The step inputs must then be complete when step() is called (resident in HBM, or
         # pass inputs_ready).  Default: everything in order on the caller's stream.
+        # Under HIP-graph capture the front stage forks from the captured step's own start, so a
+        # replayed graph runs the step without the cross-step overlap (front stage of step k+1
+        # beside the back stage of step k): capture is for launch-bound callers, not for speed.
         self.overlap_sgbm = bool(overlap_sgbm)
-        # sgbm_last: order of the front stage -- ORB + BF first, SGBM last (the stage whose waves
-        # hold the most VGPRs then starts after the back stage of the previous step has begun)
-        self.sgbm_last = bool(sgbm_last)
-        # sgbm_cus: the compute units the front stream may use (None = all)
-        if self.overlap_sgbm and sgbm_cus is not None:
-            self.s_sgbm = _lib.cu_masked_stream(sgbm_cus, dev)
-        else:
-            self.s_sgbm = torch.cuda.Stream(dev, priority=sgbm_priority) if self.overlap_sgbm else None
+        self.s_sgbm = torch.cuda.Stream(dev) if self.overlap_sgbm else None
+        # prime() runs on the caller's stream: the first front stage after it waits for it
+        self.primed = None
         self.sg_lastL = e((height, width), torch.uint8)
         self.sg_lastR = e((height, width), torch.uint8)
         self.main_done = [None, None]
@@ -132,6 +129,9 @@ class StereoFrontEnd:
             self.hnkp[Kw - 2:Kw - 1].copy_(cnt[0:1])
             self.valid_from = Kw - 2
         self.has_prev = True
+        # prime's kernels and copies (ORB, last_*) are queued on the caller's stream; the next
+        # front stage reads their outputs on the front stream, so it waits for this event
+        self.primed = torch.cuda.current_stream(self.dev).record_event() if self.overlap_sgbm else None
 
     def step(self, L: torch.Tensor, R: torch.Tensor, inputs_ready=None):
         """L, R: u8 [n,H,W] device tensors, n <= B consecutive frames after the primed/last
@@ -155,6 +155,9 @@ class StereoFrontEnd:
                 # replays are stream-ordered, so no earlier step still reads its slot)
                 fs.wait_stream(main)
             else:
+                if self.primed is not None:  # the first step after prime(): its outputs first
+                    fs.wait_event(self.primed)
+                    self.primed = None
                 if inputs_ready is not None:
                     fs.wait_event(inputs_ready)
                 if self.main_done[slot] is not None:  # the back stage of step k-2 read this slot
@@ -163,8 +166,7 @@ class StereoFrontEnd:
                 R.record_stream(fs)
         with torch.cuda.stream(fs):
             # ---- front stage: SGBM of the previous pairs (needs only images), ORB + BF
-            if not self.sgbm_last:
-                disp = self._front_sgbm(L, R, n)
+            disp = self._front_sgbm(L, R, n)
             self.imgs[:n].copy_(L)
             self.imgs[n:2 * n].copy_(R)
             kp, desc, cnt = ctx.orb(self.imgs[:2 * n], out=(self.kp[:2 * n], self.desc[:2 * n], self.cnt[:2 * n]))
@@ -191,8 +193,6 @@ class StereoFrontEnd:
             self.last_desc[1].copy_(desc[2 * n - 1])
             self.last_cnt[0:1].copy_(cnt[n - 1:n])
             self.last_cnt[1:2].copy_(cnt[2 * n - 1:2 * n])
-            if self.sgbm_last:
-                disp = self._front_sgbm(L, R, n)
         if self.overlap_sgbm:
             main.wait_stream(fs)
         # ---- back stage: back-projection, PnP, local BA
@@ -204,7 +204,10 @@ class StereoFrontEnd:
         # ORB writes -(needed) when a frame has more keypoints than kp_capacity (its outputs
         # are then unspecified): mark the frame STATUS_KP_OVERFLOW instead of letting it pass
         # as a "fewer than 6 points" skip (device-side, no host sync)
-        st.masked_fill_((cnt[:n] < 0) | (self.q_cnt[:n] < 0), STATUS_KP_OVERFLOW)
+        over = (cnt[:n] < 0) | (self.q_cnt[:n] < 0)
+        if self.match_right:  # the right sets feed bf_match too
+            over |= (cnt[n:2 * n] < 0) | (self.q_cnt[n:2 * n] < 0)
+        st.masked_fill_(over, STATUS_KP_OVERFLOW)
         out = T
         if self.ba_window:
             out = self._local_ba(n, kp, cnt, m, nm, disp, T)
@@ -235,7 +238,9 @@ class StereoFrontEnd:
         Kw, ctx = self.ba_window, self.ctx
         a, b = Kw - 2, Kw - 1  # first pair slot, first new-frame slot
         self.hkp[b:b + n].copy_(kp[:n])
-        self.hnkp[b:b + n].copy_(cnt[:n])
+        # an overflowed frame (count -(needed), outputs unspecified) enters the BA history as a
+        # frame without keypoints: the BA kernels never see a negative count
+        self.hnkp[b:b + n].copy_(cnt[:n].clamp(min=0))
         self.hmatch[a:a + n].copy_(m[:n])
         self.hnmatch[a:a + n].copy_(nm[:n])
         self.hT[a:a + n].copy_(T[:n])

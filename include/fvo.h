@@ -93,8 +93,8 @@ typedef struct fvo_config {
   int32_t ba_window;        /* frames per BA window K (10); max 21 */
   int32_t ba_max_landmarks; /* per-window landmark cap (4096) */
   int32_t ba_max_obs;       /* per-window observation cap (32768) */
-  int32_t sgbm_max_batch;   /* max pairs per fvo_sgbm call (0 = max_batch): the SGBM cost
-                               volumes (3 x ~100 MB per pair at 600p) are sized by it */
+  int32_t sgbm_max_batch;   /* max pairs per fvo_sgbm call (0 = max_batch): the SGBM path
+                               volume (one u16 volume, ~100 MB per pair at 600p) is sized by it */
 } fvo_config;
 
 /* fvo_config.stages: a context only serves the stages it was created for (e.g. a
@@ -273,15 +273,6 @@ int fvo_map_transform(fvo_ctx* ctx, const float* points, int32_t point_stride, c
 int64_t fvo_voxel_workspace_bytes(int64_t n_points);
 int fvo_voxel_down_sample(fvo_ctx* ctx, const double* points, int64_t n_points, double voxel_size, void* workspace,
                           int64_t workspace_bytes, double* out, int32_t* n_out, int32_t* status, fvo_stream stream);
-
-/* Stream helpers for partitioning the GPU between concurrent stages: a HIP stream whose
- * kernels run only on the CUs set in cu_mask (bit i of word i/32 = CU i, `words` words), e.g.
- * the overlapped SGBM stream leaving CUs free for the latency-bound pose / BA kernels of the
- * other stream.  fvo_stream_destroy releases it. */
-int fvo_stream_create_cu_mask(const uint32_t* cu_mask, int32_t words, fvo_stream* out);
-int fvo_stream_destroy(fvo_stream stream);
-/* Number of compute units of the current device. */
-int fvo_device_cu_count(void);
 
 /* Test hook: KeyPointsFilter::retainBest on `n` float responses (device memory) with the
  * product's selection kernel.  idx_out [n] receives the surviving original indices in

@@ -24,13 +24,12 @@
 //     R2 = U W^T V^T, t = U[:,2], U and V proper rotations), DLT triangulation of every
 //     point against [I|0] and each of (R1,t) (R2,t) (R1,-t) (R2,-t), cheirality counts,
 //     first maximum in that order wins.
-// Numerical building blocks are this restatement's own (documented in DESIGN.md §2):
-// Householder null space instead of OpenCV's JacobiSVD (any orthonormal basis of the same
-// null space yields the same set of E solutions; only the order of a subset's models, and
-// therefore the winner of an exact inlier-count tie between two models of ONE subset, can
-// differ), the polynomial det B(z) by cofactor expansion, cross-product null vector of
-// B(z), Jacobi eigen-decomposition for the 3x3 SVD of E and one-sided Jacobi for the 4x4
-// triangulation SVD.  The HIP kernels (csrc/essential.hip) follow this file operation by
+// The 5-point null space follows OpenCV's SVD::compute -> JacobiSVDImpl_ step by step
+// (null_space_5x9 below: the basis is the RNG-seeded Gram-Schmidt complement of the row
+// space, so the models of a subset come out in OpenCV's order).  Numerical building blocks
+// that are this restatement's own (documented in DESIGN.md §2): the polynomial det B(z) by
+// cofactor expansion, cross-product null vector of B(z), Jacobi eigen-decomposition for the
+// 3x3 SVD of E and one-sided Jacobi for the 4x4 triangulation SVD.  The HIP kernels (csrc/essential.hip) follow this file operation by
 // operation.  Parity vs OpenCV: UNPINNED (no cv2, no reference fixtures).
 #include <algorithm>
 #include <cfloat>
@@ -107,43 +106,110 @@ static void madd_ql(const double* q, const double* l, double s, double* c) {
 }
 
 // ------------------------------------------------------------------ 5-point kernel
-// Null space (4 orthonormal 9-vectors, basis[k*9 + i]) of the 5x9 matrix Q (row-major):
-// Householder QR of Q^T; the null space is spanned by columns 5..8 of H0 H1 ... H4.
+// Null space of the 5x9 epipolar matrix Q as EMEstimatorCallback::runKernel obtains it:
+//   SVD::compute(Q, W, U, Vt, MODIFY_A | FULL_UV);  EE = Vt.t().colRange(5, 9)
+// [OCV, recalled; lapack.cpp _SVDcompute + JacobiSVDImpl_<double>]: Q is wider than tall, so
+// the SVD runs on At = Q (5 rows of length m = 9) inside a 9 x 9 buffer whose rows 5..8 are
+// zero, n = 5, n1 = 9 (FULL_UV), minval = DBL_MIN, eps = 10 DBL_EPSILON:
+//  1. W[i] = |At_i|^2; cyclic one-sided Jacobi over the row pairs (i < j), at most
+//     max(m, 30) = 30 sweeps, a pair skipped when |At_i . At_j| <= eps sqrt(W_i W_j), rotation
+//     (c, s) from beta = W_i - W_j, gamma = hypot(2p, beta) in the two-branch form, W_i / W_j
+//     re-accumulated from the rotated rows; stop after a sweep without a rotation.
+//  2. W[i] = sqrt(|At_i|^2); selection sort descending (rows swapped with their W).
+//  3. rows i = 0..8 normalised; a row whose singular value is <= minval (rows 5..8: the
+//     null space) is replaced by a vector of +-1/m with the signs from RNG(0x12345678)
+//     (bit 8 of each draw, one RNG per call), orthogonalised twice against every previous row
+//     (Gram-Schmidt, each projection followed by an L1 rescale) and normalised.
+// Vt = those 9 rows, so the basis is rows 5..8: the Gram-Schmidt complement of the row space
+// seeded by the fixed RNG.  The reduction orders are the scalar source's (OpenCV's SIMD
+// builds may accumulate the dot products in two lanes: ulp-level, unpinned).
 static void null_space_5x9(const double* Q, double* basis) {
-  double M[9][5];
+  const int m = 9, n = 5;
+  const double eps = DBL_EPSILON * 10, minval = DBL_MIN;
+  double A[9][9];
   for (int i = 0; i < 9; ++i)
-    for (int j = 0; j < 5; ++j) M[i][j] = Q[j * 9 + i];
-  double V[5][9];
-  double beta[5];
-  for (int k = 0; k < 5; ++k) {
-    double nrm2 = 0.0;
-    for (int i = k; i < 9; ++i) nrm2 += M[i][k] * M[i][k];
-    double nrm = std::sqrt(nrm2);
-    double alpha = M[k][k] >= 0.0 ? -nrm : nrm;
-    for (int i = 0; i < 9; ++i) V[k][i] = i < k ? 0.0 : M[i][k];
-    V[k][k] -= alpha;
-    double vv = 0.0;
-    for (int i = k; i < 9; ++i) vv += V[k][i] * V[k][i];
-    beta[k] = vv > 0.0 ? 2.0 / vv : 0.0;
-    // apply H_k to the remaining columns
-    for (int j = k; j < 5; ++j) {
-      double s = 0.0;
-      for (int i = k; i < 9; ++i) s += V[k][i] * M[i][j];
-      s *= beta[k];
-      for (int i = k; i < 9; ++i) M[i][j] -= s * V[k][i];
+    for (int k = 0; k < 9; ++k) A[i][k] = i < n ? Q[i * 9 + k] : 0.0;
+  double W[9];
+  for (int i = 0; i < n; ++i) {
+    double sd = 0;
+    for (int k = 0; k < m; ++k) sd += A[i][k] * A[i][k];
+    W[i] = sd;
+  }
+  for (int iter = 0; iter < 30; ++iter) {
+    bool changed = false;
+    for (int i = 0; i < n - 1; ++i)
+      for (int j = i + 1; j < n; ++j) {
+        double a = W[i], p = 0, b = W[j];
+        for (int k = 0; k < m; ++k) p += A[i][k] * A[j][k];
+        if (std::fabs(p) <= eps * std::sqrt(a * b)) continue;
+        p *= 2;
+        const double beta = a - b, gamma = std::hypot(p, beta);
+        double c, s;
+        if (beta < 0) {
+          const double delta = (gamma - beta) * 0.5;
+          s = std::sqrt(delta / gamma);
+          c = p / (gamma * s * 2);
+        } else {
+          c = std::sqrt((gamma + beta) / (gamma * 2));
+          s = p / (gamma * c * 2);
+        }
+        a = b = 0;
+        for (int k = 0; k < m; ++k) {
+          const double t0 = c * A[i][k] + s * A[j][k];
+          const double t1 = -s * A[i][k] + c * A[j][k];
+          A[i][k] = t0;
+          A[j][k] = t1;
+          a += t0 * t0;
+          b += t1 * t1;
+        }
+        W[i] = a;
+        W[j] = b;
+        changed = true;
+      }
+    if (!changed) break;
+  }
+  for (int i = 0; i < n; ++i) {
+    double sd = 0;
+    for (int k = 0; k < m; ++k) sd += A[i][k] * A[i][k];
+    W[i] = std::sqrt(sd);
+  }
+  for (int i = 0; i < n - 1; ++i) {
+    int j = i;
+    for (int k = i + 1; k < n; ++k)
+      if (W[j] < W[k]) j = k;
+    if (i != j) {
+      std::swap(W[i], W[j]);
+      for (int k = 0; k < m; ++k) std::swap(A[i][k], A[j][k]);
     }
   }
-  for (int c = 0; c < 4; ++c) {
-    double e[9];
-    for (int i = 0; i < 9; ++i) e[i] = i == 5 + c ? 1.0 : 0.0;
-    for (int k = 4; k >= 0; --k) {
-      double s = 0.0;
-      for (int i = k; i < 9; ++i) s += V[k][i] * e[i];
-      s *= beta[k];
-      for (int i = k; i < 9; ++i) e[i] -= s * V[k][i];
+  RNG rng(0x12345678u);
+  for (int i = 0; i < 9; ++i) {
+    double sd = i < n ? W[i] : 0;
+    for (int ii = 0; ii < 100 && sd <= minval; ++ii) {
+      const double val0 = 1.0 / m;
+      for (int k = 0; k < m; ++k) A[i][k] = (rng.next() & 256) != 0 ? val0 : -val0;
+      for (int it = 0; it < 2; ++it)
+        for (int j = 0; j < i; ++j) {
+          sd = 0;
+          for (int k = 0; k < m; ++k) sd += A[i][k] * A[j][k];
+          double asum = 0;
+          for (int k = 0; k < m; ++k) {
+            const double t = A[i][k] - sd * A[j][k];
+            A[i][k] = t;
+            asum += std::fabs(t);
+          }
+          asum = asum > eps * 100 ? 1 / asum : 0;
+          for (int k = 0; k < m; ++k) A[i][k] *= asum;
+        }
+      sd = 0;
+      for (int k = 0; k < m; ++k) sd += A[i][k] * A[i][k];
+      sd = std::sqrt(sd);
     }
-    for (int i = 0; i < 9; ++i) basis[c * 9 + i] = e[i];
+    const double sc = sd > minval ? 1 / sd : 0.;
+    for (int k = 0; k < m; ++k) A[i][k] *= sc;
   }
+  for (int c = 0; c < 4; ++c)
+    for (int i = 0; i < 9; ++i) basis[c * 9 + i] = A[5 + c][i];
 }
 
 // 10x20 constraint matrix from the basis X, Y, Z, W (E = xX + yY + zZ + W).

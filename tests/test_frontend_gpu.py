@@ -93,40 +93,58 @@ def _rank_worker(rank, world, port, out):
     torch.cuda.set_device(0)  # both ranks share the one card of the box
     seq, L, R = _frames(40 + rank, 7, start=60 * rank)
     fe = _fe(seq, 3, ba_window=3)
-    sr = fd.SequenceRank(fe)
-    assert sr.exchange
+    sr = fd.SequenceRank(fe, map_capacity=40000)
+    assert sr.exchange and sr.gmap is not None
+    local = fd.GlobalMap(1, 3, 40000, "cuda:0", ctx=fe.ctx)  # this rank's own map, built without the exchange
     fe.prime(L[0], R[0])
     res = []
     for s in (1, 4):
-        T, st, (Tg, Xg, Cg) = sr.step(L[s:s + 3], R[s:s + 3])
+        T, st, (Tg, Sg, Xg, Cg) = sr.step(L[s:s + 3], R[s:s + 3])
         xyz, cnt = fe.ctx.ba_landmarks(2)
+        local.push((T[None], st[None], xyz[None], cnt[None]), 3)
         torch.cuda.synchronize()
         c = int(cnt.item())
-        res.append(dict(T=T.cpu().numpy(), xyz=xyz[:c].cpu().numpy(), Tg=Tg.cpu().numpy(), Xg=Xg.cpu().numpy(),
-                        Cg=Cg.cpu().numpy()))
-    out[rank] = res
+        res.append(dict(T=T.cpu().numpy(), st=st.cpu().numpy(), xyz=xyz[:c].cpu().numpy(), Tg=Tg.cpu().numpy(),
+                        Sg=Sg.cpu().numpy(), Xg=Xg.cpu().numpy(), Cg=Cg.cpu().numpy()))
+    g, lo = sr.gmap.flush(), local.flush()
+    torch.cuda.synchronize()
+    out[rank] = dict(steps=res, gmap=g.cloud64(), gmap32=g.cloud32(), local=lo.cloud64(), local32=lo.cloud32())
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_two_ranks_exchange_window_maps():
-    """the bench's multi-rank step (dist.SequenceRank: front-end step ->
-    fvo_ba_landmarks -> exchange_window_map) with two ranks on the box's one GPU (gloo
-    exchanging host copies).  Each rank's gathered poses / landmarks equal what the other
-    rank computed."""
+    """the bench's multi-rank step (dist.SequenceRank:
+    front-end step -> fvo_ba_landmarks -> exchange_window_map -> GlobalMap) with two ranks on
+    the box's one GPU (gloo exchanging host copies).  Each rank's gathered poses / statuses /
+    landmarks equal what the other rank computed; both ranks hold byte-identical global maps,
+    equal to the union (step by step, in rank order) of the maps each rank builds from its
+    own poses and landmarks alone (stereo_slam.py:306-318 per sequence)."""
     import torch.multiprocessing as mp
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_rank_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     for step in range(2):
         for r in range(2):
-            g = out[r][step]
+            g = out[r]["steps"][step]
             for o in range(2):
-                mine = out[o][step]
-                assert np.array_equal(g["Tg"][o], mine["T"])
+                mine = out[o]["steps"][step]
+                assert np.array_equal(g["Tg"][o], mine["T"]) and np.array_equal(g["Sg"][o], mine["st"])
                 c = int(g["Cg"][o][0])
                 assert c == len(mine["xyz"]) and c > 0
                 assert np.array_equal(g["Xg"][o][:c], mine["xyz"])
+    assert np.array_equal(out[0]["gmap"], out[1]["gmap"]) and np.array_equal(out[0]["gmap32"], out[1]["gmap32"])
+    # union of the local maps: step-major, rank-minor segments
+    segs, segs32, pos = [], [], [0, 0]
+    for step in range(2):
+        for r in range(2):
+            c = len(out[r]["steps"][step]["xyz"])
+            segs.append(out[r]["local"][pos[r]:pos[r] + c])
+            segs32.append(out[r]["local32"][pos[r]:pos[r] + c])
+            pos[r] += c
+    assert pos == [len(out[0]["local"]), len(out[1]["local"])]
+    assert np.array_equal(out[0]["gmap"], np.concatenate(segs))
+    assert np.array_equal(out[0]["gmap32"], np.concatenate(segs32))
 
 
 def test_frontend_step_captured_in_hip_graph_replays_bit_identically():
@@ -179,17 +197,18 @@ def test_overlapped_frontend_step_in_hip_graph():
         assert np.array_equal(T.cpu().numpy(), want[k]), k
 
 
-def test_cu_masked_sgbm_stream_gives_same_poses():
-    """fvo_stream_create_cu_mask: the overlapped SGBM branch on a stream restricted to half of
-    the CUs gives the in-order results bit for bit."""
-    from forest_slam_amd import _lib
+def test_overlapped_step_waits_for_prime_without_sync():
+    """prime() queues ORB and the last_* copies on the caller's stream, and the
+    overlapped front stage reads them on its own stream.  With a slow kernel queued on the
+    caller's stream ahead of prime() and no synchronisation before step(), the first step
+    must still see prime's outputs: results equal the in-order front end's bit for bit."""
     seq, L, R = _frames(35, 5, start=20)
     ref = _fe(seq, 2, ba_window=3)
     ref.prime(L[0], R[0])
     want = [ref.step(L[s:s + 2], R[s:s + 2])[0].cpu().numpy().copy() for s in (1, 3)]
-    ncu = _lib.load().fvo_device_cu_count()
-    assert ncu > 0
-    fe = _fe(seq, 2, ba_window=3, overlap_sgbm=True, sgbm_cus=list(range(0, ncu, 2)))
+    fe = _fe(seq, 2, ba_window=3, overlap_sgbm=True)
+    torch.cuda.synchronize()
+    torch.cuda._sleep(200_000_000)  # ~0.1 s of spinning on the caller's stream
     fe.prime(L[0], R[0])
     got = [fe.step(L[s:s + 2], R[s:s + 2])[0].cpu().numpy().copy() for s in (1, 3)]
     for w, g in zip(want, got):

@@ -294,3 +294,12 @@ def test_sgbm_ragged_geometries_bit_exact(oracle_mod, W, H, nd):
         want = oracle_mod.sgbm(img, R, num_disp=nd)
         bad = np.argwhere(d[i].cpu().numpy() != want)
         assert len(bad) == 0, f"{W}x{H}/{nd} image {i}: {len(bad)} px differ, first {bad[:5]}"
+
+
+def test_orb_rejects_edge_threshold_below_half_patch():
+    """k_angle reads the 31x31 square around a keypoint unguarded, so a context
+    whose edgeThreshold does not cover the half patch is refused at creation."""
+    from forest_slam_amd import _lib
+    with pytest.raises(RuntimeError, match="fvo_create"):
+        _lib.Context(320, 200, edge_threshold=10, stages=_lib.STAGE_ORB)
+    _lib.Context(320, 200, edge_threshold=15, stages=_lib.STAGE_ORB).close()

