@@ -76,6 +76,8 @@ __device__ __forceinline__ void madd_ql(const double* q, const double* l, double
 // Jacobi on the 5 rows (every pair index static, the sweep loop dynamic), rows sorted by
 // norm, then rows 5..8 built from RNG(0x12345678) sign vectors by two Gram-Schmidt passes
 // with L1 rescales and normalised.  All indices are compile-time, so A stays in VGPRs.
+// hypot(2p, beta) is sqrt(4p^2 + beta^2) on both sides (the device libm's hypot differs from
+// glibc's by an ulp, which the root solve amplifies to ~2e-9 in E).
 __device__ void null_space_5x9(const double* Q, double* basis) {
   constexpr int m = 9, n = 5;
   const double eps = DBL_EPSILON * 10, minval = DBL_MIN;
@@ -103,7 +105,7 @@ __device__ void null_space_5x9(const double* Q, double* basis) {
         for (int k = 0; k < m; ++k) p += A[i][k] * A[j][k];
         if (!(fabs(p) <= eps * sqrt(a * b))) {
           p *= 2;
-          const double beta = a - b, gamma = hypot(p, beta);
+          const double beta = a - b, gamma = sqrt(p * p + beta * beta);  // hypot: see above
           double c, s;
           if (beta < 0) {
             const double delta = (gamma - beta) * 0.5;

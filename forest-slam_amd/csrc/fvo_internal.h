@@ -80,12 +80,10 @@ struct fvo_ctx {
   int32_t* bf_sdist = nullptr;
   int32_t* bf_tidx = nullptr;
   // SGBM workspace
-  uint16_t* sg_C = nullptr;     // 7x7 cost C, [B][HG][width1][16][D] (16-row bands)
-  uint16_t* sg_V = nullptr;     // top-down path V, same layout
+  uint16_t* sg_V = nullptr;     // top-down path V, [B][HG4 + nstripes][width1][4][D] (4-row groups)
+  uint16_t* sg_M = nullptr;     // min over d of each V row, [B][HG4 + nstripes][width1][4]
   uint32_t* sg_ckpt = nullptr;  // [B][4-row blocks][nck][64 lanes][ckw] left->right path checkpoints
   int16_t* sg_raw = nullptr;    // [B][H][W] pre-median disparity
-  hipStream_t sg_s2 = nullptr;  // second stream for chunked (pipelined) SGBM batches
-  hipEvent_t sg_fork = nullptr, sg_join = nullptr;
   // pose workspace
   double* pnp_hyp = nullptr;      // [B][cap][2] normalised inlier points (refinement)
   int32_t* pnp_sub = nullptr;     // [B][cap] inlier indices

@@ -2,30 +2,36 @@
 // get_disparity_map (ros_ws/src/stereo_slam.py:108-117): numDisparities 96, minDisparity 0,
 // blockSize 7, P1 392, P2 1568, 3-way aggregation, 4 fixed stripes, then medianBlur(3).
 //
-// Two cost-volume-sized buffers cross HBM per pair, written once and read by the row pass:
-// the 7x7 cost C and the top-down path V, u16 [HG4][x1][4][d] (4-row groups interleaved per
-// column, so the 4 rows of a group at one column are 4*D*2 contiguous bytes and a wave of the
-// row pass streams contiguous memory; x1 = x - max(maxD,0) in [0,width1), d in [0,D)).
+// One cost-volume-sized buffer crosses HBM per pair: the top-down path V, u16
+// [HG4 + nstripes][x1][4][d] (4-row groups interleaved per column, so the 4 rows of a group at
+// one column are 4*D*2 contiguous bytes and a wave of the row pass streams contiguous memory;
+// x1 = x - max(maxD,0) in [0,width1), d in [0,D)); the extra nstripes groups hold, per stripe
+// s > 0, the path's row first_out(s) - 1 (an overlap row the previous stripe outputs).  The
+// 7x7 cost C is not stored: the recurrence V(y) = C(y) + min(V(y-1)[d], V(y-1)[d+-1] + P1,
+// minV(y-1) + P2) - minV(y-1) is inverted exactly (u16 modular arithmetic) from V(y) and
+// V(y-1), which the row pass reads anyway -- one volume write and two reads per pair instead
+// of two writes and three reads.
 // Kernels
 //   k_sg_costvert<D,CB,G> block of CB columns (G lanes per column, D/G disparities per lane)
 //                  marching down a stripe: BT pixel cost of both channels in one u16x2 word
 //                  from LDS-staged rows, 7x7 box sum (7-column sum from LDS, 7-row running
 //                  sum over a VGPR shift register, rows clamped to the stripe's first row and to
 //                  H-1 -- the overlap rule of OpenCV's 4 stripes), fused with the top->down
-//                  path; stores C and V
-//   k_sg_rows<D>   wave per 4 rows (16 lanes per row, D/16 disparities per lane): left->right
-//                  path over C storing its state every 8 columns (checkpoints), then segments
-//                  of 8 columns right->left: the left->right path recomputed over the segment
-//                  from its checkpoint, the right->left path, S = L + R + V, first-minimum WTA,
-//                  integer sub-pixel, right-view keys by LDS atomicMin, the pseudo left-right
-//                  check -- the L + V volume the forward pass would otherwise store and re-read
-//                  never exists
+//                  path; stores V
+//   k_sg_rows<D>   wave per 4 rows (16 lanes per row, D/16 disparities per lane): C derived
+//                  from V and the previous V row, left->right path over C storing its state
+//                  every 8 columns (checkpoints), then segments of 8 columns right->left: the
+//                  left->right path recomputed over the segment from its checkpoint, the
+//                  right->left path, S = L + R + V, first-minimum WTA, integer sub-pixel,
+//                  right-view keys by LDS atomicMin, the pseudo left-right check -- the L + V
+//                  volume the forward pass would otherwise store and re-read never exists
 //   k_sg_median    3x3 median (replicated border) -> int16 disparity*16
 // Path states are packed u16x2 VGPRs (v_pk_add/sub/min_u16, v_alignbit for d-1 / d+1);
 // neighbours across lanes come from DPP.  Integer arithmetic only; bit-identical to
 // oracle/sgbm_ref.cpp.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "fvo_internal.h"
 
@@ -77,6 +83,22 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
 }
 
+// min / or with a DPP-permuted copy of v: the permute's old value is the operation's identity,
+// so the compiler folds the move into the VALU op (v_min_u32_dpp / v_or_b32_dpp)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dmin(uint32_t v) {
+  return min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dor(uint32_t v) {
+  return v | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+// the value of a DPP-shifted lane, `old` where the shift has no source lane (row edges)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dshift(uint32_t v, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, 0xF, 0xF, false);
+}
+
 template <int NV4>
 __device__ __forceinline__ void load_run(const uint16_t* base, uint32_t* out) {
   const uint4* p4 = reinterpret_cast<const uint4*>(base);
@@ -110,9 +132,9 @@ __device__ __forceinline__ uint32_t hstepG(uint32_t* st, const uint32_t* c, int 
   for (int k = 0; k < PQ; ++k) mn = vmin(mn, as_v(sgm_pair<PQ>(st, k, oldk, c[k], P1, mp2, mpv, lo0, hiN)));
   uint32_t m = as_u(mn);
   m = min(m & 0xFFFFu, m >> 16);
-  m = min(m, qperm<kQX1>(m));
-  m = min(m, qperm<kQX2>(m));
-  if (G == 8) m = min(m, (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  m = dmin<kQX1>(m);
+  m = dmin<kQX2>(m);
+  if (G == 8) m = dmin<0x141>(m);  // row_half_mirror
   return m;
 }
 
@@ -123,6 +145,23 @@ __device__ __forceinline__ void load_run2(const uint16_t* base, uint32_t* out) {
   for (int i = 0; i < NV2; ++i) {
     uint2 q = p2[i];
     out[2 * i] = q.x; out[2 * i + 1] = q.y;
+  }
+}
+
+// PQ packed words (4*PQ bytes) through a buffer descriptor: per-lane byte offset + a
+// wave-uniform (SGPR) byte offset; out-of-range offsets read zeros.
+template <int PQ>
+__device__ __forceinline__ void bload(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, uint32_t* out) {
+  if constexpr (PQ == 2) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+    out[0] = v[0]; out[1] = v[1];
+  } else if constexpr (PQ == 3) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, voff, soff, 0);
+    out[0] = v[0]; out[1] = v[1]; out[2] = v[2];
+  } else {
+    static_assert(PQ == 4, "D = 64, 96 or 128");
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+    out[0] = v[0]; out[1] = v[1]; out[2] = v[2]; out[3] = v[3];
   }
 }
 
@@ -141,8 +180,8 @@ __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q
   for (int k = 0; k < PQ; ++k) mn = vmin(mn, as_v(sgm_pair<PQ>(st, k, oldk, c[k], P1, mp2, mpv, lo0, hiN)));
   uint32_t m = as_u(mn);
   m = min(m & 0xFFFFu, m >> 16);
-  m = min(m, qperm<kQX1>(m));
-  m = min(m, qperm<kQX2>(m));
+  m = dmin<kQX1>(m);
+  m = dmin<kQX2>(m);
   return m;
 }
 
@@ -160,8 +199,8 @@ __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q
 // wait for the stores).  Integer arithmetic as oracle/sgbm_ref.cpp (order-independent sums).
 template <int D, int CB, int G>
 __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
-                                                    int64_t stride, int pitch, SgParams p, uint16_t* __restrict__ Cvol,
-                                                    uint16_t* __restrict__ Vvol) {
+                                                    int64_t stride, int pitch, SgParams p, uint16_t* __restrict__ Vvol,
+                                                    uint16_t* __restrict__ Mvol) {
   constexpr int DQ = D / G, PQ = DQ / 2, NV2 = DQ / 4;
   constexpr int NT = G * CB;                // threads: G lanes per column
   constexpr int kCX = CB + 6;               // pixel-cost columns (7-wide box apron)
@@ -315,7 +354,7 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
   const u16x2 P1 = splat(p.P1);
   const int x1 = c0 + col;
   const int64_t plane = (int64_t)p.width1 * D;
-  const int64_t colofs = (int64_t)b * p.HG4 * 4 * plane + (int64_t)x1 * 4 * D + q * DQ;
+  const int64_t colofs = (int64_t)b * (p.HG4 + p.nstripes) * 4 * plane + (int64_t)x1 * 4 * D + q * DQ;
   for (int y = start; y < end; ++y) {
     if (y > start) {  // window [y-3, y+3] clamped to [start, H-1]: out clamp(y-4), in clamp(y+3)
       uint32_t nw[PQ];
@@ -337,16 +376,19 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
     minPrev = hstepG<PQ, G>(st, crun, q, P1, minPrev, p.P2);
 #pragma unroll
     for (int k = 0; k < PER; ++k) asm volatile("" : "+v"(pre[k]) :: "memory");
-    if (y >= first_out && x1 < p.width1) {
-      const int64_t yo = (int64_t)(y >> 2) * 4 * plane + (y & 3) * D;
-      uint2* cp = reinterpret_cast<uint2*>(Cvol + colofs + yo);
+    // output rows, and for s > 0 the row above the stripe's first output row (the row pass
+    // inverts the recurrence at first_out from it): group HG4 + s, sub-row 0
+    const bool out_row = y >= first_out, top_row = s > 0 && y == first_out - 1;
+    if ((out_row || top_row) && x1 < p.width1) {
+      const int64_t yo = out_row ? (int64_t)(y >> 2) * 4 * plane + (y & 3) * D : (int64_t)(p.HG4 + s) * 4 * plane;
       uint2* vp = reinterpret_cast<uint2*>(Vvol + colofs + yo);
 #pragma unroll
       for (int i = 0; i < NV2; ++i) {
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        __builtin_nontemporal_store(u32x2{crun[2 * i], crun[2 * i + 1]}, reinterpret_cast<u32x2*>(cp + i));
         __builtin_nontemporal_store(u32x2{st[2 * i], st[2 * i + 1]}, reinterpret_cast<u32x2*>(vp + i));
       }
+      // min over d of this V row (the next row's minPrev): the row pass's inversion needs it
+      if (q == 0) Mvol[(colofs - q * DQ + yo) / D] = (uint16_t)minPrev;
     }
   }
 }
@@ -374,10 +416,9 @@ __host__ __device__ constexpr int sg_ring_raw(int D) { return sg_pow2(D + 16); }
 template <int PQ>
 __device__ __forceinline__ uint32_t step16(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
                                            uint32_t P2) {
-  const uint32_t prevLast = rdpp<kRShr1>(st[PQ - 1]);
-  const uint32_t nextFirst = rdpp<kRShl1>(st[0]);
-  const uint32_t lo0 = q == 0 ? (kSent << 16) : prevLast;
-  const uint32_t hiN = q == 15 ? kSent : nextFirst;
+  // a row's lanes 0 / 15 have no left / right neighbour: the shift leaves the sentinel there
+  const uint32_t lo0 = dshift<kRShr1>(st[PQ - 1], kSent << 16);
+  const uint32_t hiN = dshift<kRShl1>(st[0], kSent);
   const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
   u16x2 mn = splat(0xFFFF);
   uint32_t oldk = 0;
@@ -385,10 +426,10 @@ __device__ __forceinline__ uint32_t step16(uint32_t* st, const uint32_t* c, int 
   for (int k = 0; k < PQ; ++k) mn = vmin(mn, as_v(sgm_pair<PQ>(st, k, oldk, c[k], P1, mp2, mpv, lo0, hiN)));
   uint32_t m = as_u(mn);
   m = min(m & 0xFFFFu, m >> 16);
-  m = min(m, qperm<kQX1>(m));
-  m = min(m, qperm<kQX2>(m));
-  m = min(m, rdpp<kRHalfMirror>(m));
-  m = min(m, rdpp<kRMirror>(m));
+  m = dmin<kQX1>(m);
+  m = dmin<kQX2>(m);
+  m = dmin<kRHalfMirror>(m);
+  m = dmin<kRMirror>(m);
   return m;
 }
 
@@ -396,6 +437,29 @@ template <int PQ>
 __device__ __forceinline__ void vadd(uint32_t* a, const uint32_t* b) {
 #pragma unroll
   for (int k = 0; k < PQ; ++k) a[k] = as_u(as_v(a[k]) + as_v(b[k]));
+}
+
+// C of one column from the top-down path: V(y) = C + min(Vp[d], Vp[d-1] + P1, Vp[d+1] + P1,
+// min Vp + P2) - min Vp with Vp = V(y-1) of the same stripe's path (zero above its first
+// row), so C = V(y) - (that minimum) + min Vp -- the cost pass's u16 arithmetic undone
+// exactly (modular).  16 lanes per row as step16; m = min Vp (stored by the cost pass).
+template <int PQ>
+__device__ __forceinline__ void derive16(const uint32_t* vp, const uint32_t* v, uint32_t* c, uint32_t m, u16x2 P1,
+                                         uint32_t P2) {
+  // a row's lanes 0 / 15 have no left / right neighbour: the shift leaves the sentinel there
+  const uint32_t lo0 = dshift<kRShr1>(vp[PQ - 1], kSent << 16);
+  const uint32_t hiN = dshift<kRShl1>(vp[0], kSent);
+  const u16x2 mp2 = splat(m + P2), mpv = splat(m);
+#pragma unroll
+  for (int k = 0; k < PQ; ++k) {
+    const uint32_t cur = vp[k];
+    const uint32_t lo = k > 0 ? vp[k - 1] : lo0;
+    const uint32_t hi = k < PQ - 1 ? vp[k + 1] : hiN;
+    const u16x2 dm = as_v(__builtin_amdgcn_alignbit(cur, lo, 16));
+    const u16x2 dp = as_v(__builtin_amdgcn_alignbit(hi, cur, 16));
+    const u16x2 mm = vmin(vmin(dm + P1, dp + P1), vmin(as_v(cur), mp2));
+    c[k] = as_u(as_v(v[k]) - mm + mpv);
+  }
 }
 
 // Wave per 4 rows (one block), 16 lanes per row, D/16 disparities per lane.  Sweep 1 walks
@@ -408,18 +472,26 @@ __device__ __forceinline__ void vadd(uint32_t* a, const uint32_t* b) {
 // by an LDS atomicMin -- the serial rule "replace iff disp2cost > cost" of sgbm_ref.cpp (the
 // smallest cost wins, among equal costs the largest x1, the first one the scan visits).  The
 // pseudo left-right check then runs on the LDS row and writes the row-major raw disparity.
+#ifndef FVO_SG_PD
+#define FVO_SG_PD 4
+#endif
 template <int D>
-__global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvol, const uint16_t* __restrict__ Vvol,
-                                                SgParams p, uint32_t* __restrict__ ckpt, int nck,
-                                                int16_t* __restrict__ raw) {
-  constexpr int DQ = D / 16, PQ = DQ / 2, SEG = 8, PF = 8;
+__global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t* __restrict__ Vvol,
+                                                                 const uint16_t* __restrict__ Mvol, SgParams p,
+                                                                 uint32_t* __restrict__ ckpt, int nck,
+                                                                 int16_t* __restrict__ raw) {
+  constexpr int DQ = D / 16, PQ = DQ / 2, SEG = 8, PF = 8, PD = FVO_SG_PD;
   constexpr int CKW = PQ + 1 <= 4 ? 4 : 8;
   constexpr int XS = 2 * D;  // u32 words per column of a 4-row group
   constexpr int RK = sg_ring_keys(D), RS = sg_ring_raw(D);
   __shared__ uint32_t s_key[4][RK];  // right-view keys of the live x2 window (ring, by x2)
   __shared__ int16_t s_raw[4][RS];   // raw disparities awaiting their check (ring, by x1)
   const int lane = threadIdx.x, q = lane & 15, r = lane >> 4;
-  const int y = blockIdx.x * 4 + r, b = blockIdx.y;
+  // consecutive row groups on one XCD: a group's first row reads the previous group's last
+  // V row, which that group's wave streams at about the same time (an L2 hit)
+  const XcdBlock xb = xcd_block();
+  const int blk = xb.x, b = xb.y;
+  const int y = blk * 4 + r;
   const int H = p.H, W = p.W, W1 = p.width1;
   const bool rowok = y < H;
   const int yy = min(y, H - 1);  // rows past H walk the last row's volumes (never output)
@@ -457,39 +529,72 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
   // lanes with no pixel to check store into this lane's words of the dummy checkpoint slot, so
   // every segment issues the same global stores: with a conditional store the compiler's vmcnt
   // bookkeeping falls back to draining every load in flight at the next segment
-  int16_t* const sink = reinterpret_cast<int16_t*>(ckpt + ((((int64_t)b * gridDim.x + blockIdx.x) * nck + nck - 1) * 64 + lane) * (PQ + 1 <= 4 ? 4 : 8));
+  int16_t* const sink = reinterpret_cast<int16_t*>(ckpt + ((((int64_t)b * gridDim.x + blk) * nck + nck - 1) * 64 + lane) * (PQ + 1 <= 4 ? 4 : 8));
   int next_chk = W1 - 1;  // highest pixel not yet checked
-  const int64_t rowofs = (((int64_t)b * p.HG4 + (yy >> 2)) * W1 * (4 * D) + (yy & 3) * D + q * DQ) / 2;
-  const uint32_t* Cr = reinterpret_cast<const uint32_t*>(Cvol) + rowofs;
-  const uint32_t* Vr = reinterpret_cast<const uint32_t*>(Vvol) + rowofs;
+  // V of this row and of the previous row of the same stripe's path: inside the stripe the
+  // row above, at its first output row (s > 0) the overlap row the cost pass kept in group
+  // HG4 + s, above row 0 nothing (a zero state: C = V there)
+  const int64_t plane4 = (int64_t)W1 * (4 * D);  // u16 per 4-row group
+  const int stripe = yy / p.ss;
+  const bool ptop = yy == stripe * p.ss, pzero = yy == 0;
+  const int yp = ptop ? 0 : yy - 1;
+  const int64_t prow = ptop ? (int64_t)(p.HG4 + stripe) * plane4 : (int64_t)(yp >> 2) * plane4 + (yp & 3) * D;
+  // the pair's volume through one buffer descriptor (built from wave-uniform values): a lane's
+  // row / disparity offset in a VGPR, the column offset x * 4D * 2 bytes in an SGPR; above
+  // row 0 the offset points past the buffer, so the previous row reads as zeros
+  const uint16_t* vpair = Vvol + (int64_t)b * (p.HG4 + p.nstripes) * plane4;
+  const uint32_t vbytes = (uint32_t)((p.HG4 + p.nstripes) * plane4 * 2);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)vpair)) |
+              ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)vpair >> 32)) << 32)),
+      (short)0, (int)__builtin_amdgcn_readfirstlane((int)vbytes), 0x00020000);
+  const uint32_t voffV = (uint32_t)(((int64_t)(yy >> 2) * plane4 + (yy & 3) * D + q * DQ) * 2);
+  const uint32_t voffP = pzero ? 0x80000000u : (uint32_t)((prow + q * DQ) * 2);
+  // the previous row's minimum over d, [group][x1][4] u16 (zero above row 0)
+  const uint16_t* mpair = Mvol + (int64_t)b * (p.HG4 + p.nstripes) * W1 * 4;
+  const uint32_t mbytes = (uint32_t)((p.HG4 + p.nstripes) * W1 * 8);
+  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)mpair)) |
+              ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)mpair >> 32)) << 32)),
+      (short)0, (int)__builtin_amdgcn_readfirstlane((int)mbytes), 0x00020000);
+  const int pgrp = ptop ? p.HG4 + stripe : yp >> 2, psub = ptop ? 0 : yp & 3;
+  const uint32_t voffM = pzero ? 0x80000000u : (uint32_t)(((int64_t)pgrp * W1 * 4 + psub) * 2);
   const u16x2 P1 = splat(p.P1);
-  const int64_t ckbase = ((int64_t)b * gridDim.x + blockIdx.x) * nck;
-  auto ld = [&](const uint32_t* base, int x, uint32_t* out) {
-#pragma unroll
-    for (int k = 0; k < PQ; ++k) out[k] = __builtin_nontemporal_load(base + (int64_t)x * XS + k);
+  const int64_t ckbase = ((int64_t)b * gridDim.x + blk) * nck;
+  auto ld = [&](int x, uint32_t* out) { bload<PQ>(vrs, voffV, (uint32_t)x * (XS * 4), out); };
+  auto ldp = [&](int x, uint32_t* out) { bload<PQ>(vrs, voffP, (uint32_t)x * (XS * 4), out); };
+  auto ldm = [&](int x) -> uint32_t {
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(mrs, voffM, (uint32_t)x * 8, 0);
   };
 
   // ---- sweep 1: left -> right, checkpoints.  Loads are unconditional (clamped columns) so
   // the compiler's vmcnt waits stay precise; the checkpoint of each 8-column block is picked
   // by a register select and stored once per block (slot nck-1 is a dummy for blocks that
   // hold none).
-  uint32_t st[PQ], cb[PF][PQ], ck[PF / SEG][PQ + 1];
+  // V and the previous row PD columns ahead (a ring of PD column buffers)
+  uint32_t st[PQ], vb[PD][PQ], pb[PD][PQ], mb[PD], ck[PF / SEG][PQ + 1];
   uint32_t minPrev = 0;
 #pragma unroll
   for (int k = 0; k < PQ; ++k) st[k] = 0;
 #pragma unroll
-  for (int j = 0; j < PF; ++j) ld(Cr, min(j, W1 - 1), cb[j]);
+  for (int j = 0; j < PD; ++j) {
+    ld(min(j, W1 - 1), vb[j]);
+    ldp(min(j, W1 - 1), pb[j]);
+    mb[j] = ldm(min(j, W1 - 1));
+  }
   static_assert(PF % SEG == 0, "whole checkpoints per prefetch block");
   const int jck = (W1 - 1 - SEG) & (SEG - 1);  // checkpoint columns of a block: jck + SEG*m
+#pragma unroll 1
   for (int x0 = 0; x0 < W1; x0 += PF) {
     const bool full = x0 + PF <= W1;
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       const int x = x0 + j;
       uint32_t c[PQ];
-#pragma unroll
-      for (int k = 0; k < PQ; ++k) c[k] = cb[j][k];
-      ld(Cr, min(x + PF, W1 - 1), cb[j]);
+      derive16<PQ>(pb[j % PD], vb[j % PD], c, mb[j % PD], P1, p.P2);
+      ld(min(x + PD, W1 - 1), vb[j % PD]);
+      ldp(min(x + PD, W1 - 1), pb[j % PD]);
+      mb[j % PD] = ldm(min(x + PD, W1 - 1));
       if (full || x < W1) minPrev = step16<PQ>(st, c, q, P1, minPrev, p.P2);
       const bool here = (j & (SEG - 1)) == jck;
       uint32_t* ckm = ck[j / SEG];
@@ -517,51 +622,61 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
   uint32_t minR = 0;
 #pragma unroll
   for (int k = 0; k < PQ; ++k) Rst[k] = 0;
-  // C and V of a segment loaded at its start (C double-buffered one segment ahead measured the
-  // same at 3 waves/SIMD; single buffers and an 8-column prefetch in sweep 1 give 106 VGPRs,
-  // 4 waves/SIMD, which leaves room for the main stream's kernels on the same CUs)
-  uint32_t Cs[2][SEG][PQ], Vs[SEG][PQ];
-  auto ldseg = [&](const uint32_t* base, int sg, uint32_t (*cs)[PQ]) {
+  // V and the previous V row of segment sg + 1 are loaded column by column inside segment
+  // sg's R path, each into the registers of a column that path has just finished (the next L
+  // recompute consumes the columns in the reverse order, so the first one it needs is loaded
+  // first); its checkpoint is loaded as the R path starts
+  uint32_t Vn[SEG][PQ], Pn[SEG][PQ], Mn[SEG], ckn[CKW];
+  auto ldck = [&](int sg) {
+    const int slot = SEG * (sg + 1) > W1 - 1 ? nck - 1 : sg;
+    const uint32_t* cp = ckpt + ((ckbase + slot) * 64 + lane) * CKW;
 #pragma unroll
-    for (int i = 0; i < SEG; ++i) ld(base, max(W1 - 1 - (SEG * sg + i), 0), cs[i]);
+    for (int kk = 0; kk < CKW; kk += 4) {
+      const uint4 w4 = *reinterpret_cast<const uint4*>(cp + kk);
+      ckn[kk] = w4.x; ckn[kk + 1] = w4.y; ckn[kk + 2] = w4.z; ckn[kk + 3] = w4.w;
+    }
   };
-  for (int s0 = 0; s0 < nseg; s0 += 2) {
+  auto ldcol = [&](int sg, int i) {
+    const int xx = max(W1 - 1 - (SEG * sg + i), 0);
+    ld(xx, Vn[i]);
+    ldp(xx, Pn[i]);
+    Mn[i] = ldm(xx);
+  };
+  auto ldseg = [&](int sg) {
+    ldck(sg);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int sg = s0 + h;  // may be nseg (an empty segment: every step below is skipped)
-      // the checkpoint first, then C, then V: the L recompute needs the first two only
-      uint32_t lst[PQ], Ls[SEG][PQ];
-      const bool zero = SEG * (sg + 1) > W1 - 1;
-      uint32_t v[CKW];
-      {
-        const uint32_t* cp = ckpt + ((ckbase + (zero ? nck - 1 : sg)) * 64 + lane) * CKW;
-#pragma unroll
-        for (int kk = 0; kk < CKW; kk += 4) {
-          const uint4 w4 = *reinterpret_cast<const uint4*>(cp + kk);
-          v[kk] = w4.x; v[kk + 1] = w4.y; v[kk + 2] = w4.z; v[kk + 3] = w4.w;
-        }
-      }
-      ldseg(Cr, sg, Cs[h]);
-      ldseg(Vr, sg, Vs);
-      const int ihi = min(SEG - 1, W1 - 1 - SEG * sg);  // valid i: x' < W1
+    for (int i = SEG - 1; i >= 0; --i) ldcol(sg, i);
+  };
+  ldseg(0);
+  // one segment; FULL (every segment but the last): 8 valid columns and a checkpoint, so the
+  // body has no per-column conditions
+  auto segment = [&](int sg, auto full_t) {
+    constexpr bool FULL = decltype(full_t)::value;
+    {
+      uint32_t lst[PQ], Ls[SEG][PQ], Cs[SEG][PQ];
+      const bool zero = FULL ? false : SEG * (sg + 1) > W1 - 1;
+      const int ihi = FULL ? SEG - 1 : min(SEG - 1, W1 - 1 - SEG * sg);  // valid i: x' < W1
       // L over the segment (i descending = real x ascending) from the checkpoint at the real
-      // column left of it, x' = SEG*(sg+1); zero state when the segment starts at x = 0
+      // column left of it, x' = SEG*(sg+1); zero state when the segment starts at x = 0.  C of
+      // each column is derived as the L path reaches it.
 #pragma unroll
-      for (int kk = 0; kk < PQ; ++kk) lst[kk] = zero ? 0u : v[kk];
-      minPrev = zero ? 0u : v[PQ];
+      for (int kk = 0; kk < PQ; ++kk) lst[kk] = zero ? 0u : ckn[kk];
+      minPrev = zero ? 0u : ckn[PQ];
       uint32_t lmin = minPrev;
 #pragma unroll
       for (int i = SEG - 1; i >= 0; --i) {
-        if (i <= ihi) lmin = step16<PQ>(lst, Cs[h][i], q, P1, lmin, p.P2);
+        derive16<PQ>(Pn[i], Vn[i], Cs[i], Mn[i], P1, p.P2);
+        if (i <= ihi) lmin = step16<PQ>(lst, Cs[i], q, P1, lmin, p.P2);
         // L + V at once (u16 sums, order-free): V's registers are free before the R path
 #pragma unroll
-        for (int kk = 0; kk < PQ; ++kk) Ls[i][kk] = as_u(as_v(lst[kk]) + as_v(Vs[i][kk]));
+        for (int kk = 0; kk < PQ; ++kk) Ls[i][kk] = as_u(as_v(lst[kk]) + as_v(Vn[i][kk]));
       }
+      ldck(sg + 1);
+      uint32_t wk = 0, wn = 0;
 #pragma unroll
       for (int i = 0; i < SEG; ++i) {
-        if (i > ihi) break;
-        const int x1 = W1 - 1 - (SEG * sg + i);
-        minR = step16<PQ>(Rst, Cs[h][i], q, P1, minR, p.P2);
+        if (i > ihi) break;  // only in the last segment (no next one to load)
+        minR = step16<PQ>(Rst, Cs[i], q, P1, minR, p.P2);
         // first minimum over d as one u32 min of (S << 7 | d) across the row's lanes
         uint32_t Sw[PQ];
         uint32_t kmin = 0xFFFFFFFFu;
@@ -572,11 +687,11 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
           kmin = min(kmin, ((Sw[kk] & 0xFFFFu) << 7) | d0);
           kmin = min(kmin, ((Sw[kk] >> 16) << 7) | (d0 + 1));
         }
-        kmin = min(kmin, qperm<kQX1>(kmin));
-        kmin = min(kmin, qperm<kQX2>(kmin));
-        kmin = min(kmin, rdpp<kRHalfMirror>(kmin));
-        kmin = min(kmin, rdpp<kRMirror>(kmin));
-        const int best = (int)(kmin >> 7), d = (int)(kmin & 127u);
+        kmin = dmin<kQX1>(kmin);
+        kmin = dmin<kQX2>(kmin);
+        kmin = dmin<kRHalfMirror>(kmin);
+        kmin = dmin<kRMirror>(kmin);
+        const int d = (int)(kmin & 127u);
         // S[d-1] << 16 | S[d+1] from the lanes that hold them (OR across the row)
         uint32_t nb = 0;
         {
@@ -590,15 +705,27 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
           if (im >= 0 && im < DQ) nb |= ((im & 1) ? (wm >> 16) : (wm & 0xFFFFu)) << 16;
           if (ip >= 0 && ip < DQ) nb |= (ip & 1) ? (wp >> 16) : (wp & 0xFFFFu);
         }
-        nb |= qperm<kQX1>(nb);
-        nb |= qperm<kQX2>(nb);
-        nb |= rdpp<kRHalfMirror>(nb);
-        nb |= rdpp<kRMirror>(nb);
-        if (q == 0) {
-          const int sm1 = (int)(nb >> 16), sp1 = (int)(nb & 0xFFFFu);
-          // the lowest x2 this column can reach enters the key window: reset its ring slot
-          // (it last held x2 + RK, whose readers were all checked RK - 2D columns ago)
-          key[(x1 + p.minX1 - p.minD - (D - 1)) & (RK - 1)] = 0xFFFFFFFFu;
+        nb = dor<kQX1>(nb);
+        nb = dor<kQX2>(nb);
+        nb = dor<kRHalfMirror>(nb);
+        nb = dor<kRMirror>(nb);
+        // every lane of the row holds the reduced key and neighbours: lane q keeps column q's
+        wk = q == i ? kmin : wk;
+        wn = q == i ? nb : wn;
+        ldcol(sg + 1, SEG - 1 - i);  // clamped columns past the row's start: harmless reads
+      }
+      // the segment's columns, one lane each (lane q of a row = column q of the segment), so
+      // the sub-pixel division and the key updates run once per segment, not once per column.
+      // Every ring slot reset comes before any key update: the slot column i resets (the
+      // lowest x2 it can reach) is reachable only from columns i, i+1, ... (further left), so
+      // the final keys equal the serial order's.
+      {
+        const bool colv = q < SEG && q <= ihi;
+        const int x1 = W1 - 1 - (SEG * sg + q);
+        if (colv) key[(x1 + p.minX1 - p.minD - (D - 1)) & (RK - 1)] = 0xFFFFFFFFu;
+        if (colv) {
+          const int best = (int)(wk >> 7), d = (int)(wk & 127u);
+          const int sm1 = (int)(wn >> 16), sp1 = (int)(wn & 0xFFFFu);
           const int x2 = x1 + p.minX1 - d - p.minD;
           if (x2 >= 0 && x2 < W && best < 0x7FFF)  // disp2cost starts at SHRT_MAX
             atomicMin(&key[x2 & (RK - 1)], ((uint32_t)best << 16) | (uint32_t)(0xFFFF - x1));
@@ -622,7 +749,10 @@ __global__ __launch_bounds__(64) void k_sg_rows(const uint16_t* __restrict__ Cvo
         if (cnt > 0) next_chk -= cnt;
       }
     }
-  }
+  };
+#pragma unroll 1
+  for (int sg = 0; sg < nseg - 1; ++sg) segment(sg, std::true_type{});
+  segment(nseg - 1, std::false_type{});
   for (int x1 = next_chk - q; x1 >= 0; x1 -= 16) check(x1);  // the last D (+ < SEG) pixels
 }
 
@@ -649,10 +779,9 @@ __global__ void k_sg_median(const int16_t* __restrict__ raw, int16_t* __restrict
   out[((int64_t)b * H + y) * W + x] = (int16_t)v[4];
 }
 
-// Experiment / tuning knobs (read per launch): FVO_SG_G lanes per column in the cost pass
-// (4 or 8), FVO_SG_CB columns per cost-pass block (G=4: 32/64; G=8: 16/32), FVO_SG_CHUNKS
-// batch chunks alternated over the caller's stream and a second stream (the cost pass of
-// one chunk overlaps the row pass of the other).  All variants are bit-identical.
+// Launch-shape knobs of the cost pass (read per launch; every variant is bit-identical and
+// parity-tested): FVO_SG_G lanes per column (4 or 8), FVO_SG_CB columns per block (G=4: 32/64;
+// G=8: 16/32).
 int env_int(const char* name, int def) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : def;
@@ -686,45 +815,22 @@ int sg_ckw(int D) { return D / 32 + 1 <= 4 ? 4 : 8; }
 int sg_nblk(const SgParams& p) { return (p.H + 3) / 4; }
 
 template <int D>
-void launch_chunk(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_t* R, int nb, int64_t stride,
-                  int pitch, uint16_t* C, uint16_t* V, uint32_t* ck, int16_t* raw, int16_t* disp, int cb, int g,
-                  hipStream_t s) {
-  const dim3 gcv((p.width1 + cb - 1) / cb, p.nstripes, nb);
-  FVO_TIMED(ctx, KN_SG_VERT, s, {
-    if (g == 8 && cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 8>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, C, V);
-    else if (g == 8) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 16, 8>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, C, V);
-    else if (cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 4>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, C, V);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 64, 4>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, C, V);
-  });
-  FVO_TIMED(ctx, KN_SG_ROWS, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_rows<D>), dim3(sg_nblk(p), nb), dim3(64), 0, s,
-                                                   C, V, p, ck, sg_nck(p), raw));
-  FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.W + 255) / 256, p.H, nb), dim3(256), 0, s,
-                                                     raw, disp, p.W, p.H));
-}
-
-template <int D>
-void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_t* R, int batch, int64_t stride,
+void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_t* R, int nb, int64_t stride,
                  int pitch, int16_t* disp, hipStream_t s) {
   const int g = env_int("FVO_SG_G", 8), cb = env_int("FVO_SG_CB", g == 8 ? 32 : 64);
-  const int nch = std::max(1, std::min(env_int("FVO_SG_CHUNKS", 1), batch));
-  const int64_t vol = (int64_t)p.HG4 * 4 * p.width1 * D, img = (int64_t)p.H * p.W;
-  const int64_t ckp = (int64_t)sg_nblk(p) * sg_nck(p) * 64 * sg_ckw(D);
-  if (nch > 1) {
-    (void)hipEventRecord(ctx->sg_fork, s);
-    (void)hipStreamWaitEvent(ctx->sg_s2, ctx->sg_fork, 0);
-  }
-  for (int k = 0; k < nch; ++k) {
-    const int b0 = (int)((int64_t)batch * k / nch), b1 = (int)((int64_t)batch * (k + 1) / nch);
-    if (b1 <= b0) continue;
-    hipStream_t sk = (k & 1) ? ctx->sg_s2 : s;
-    launch_chunk<D>(ctx, p, L + b0 * stride, R + b0 * stride, b1 - b0, stride, pitch, ctx->sg_C + b0 * vol,
-                    ctx->sg_V + b0 * vol, ctx->sg_ckpt + b0 * ckp, ctx->sg_raw + b0 * img, disp + b0 * img, cb, g,
-                    sk);
-  }
-  if (nch > 1) {
-    (void)hipEventRecord(ctx->sg_join, ctx->sg_s2);
-    (void)hipStreamWaitEvent(s, ctx->sg_join, 0);
-  }
+  uint16_t* V = ctx->sg_V;
+  uint16_t* M = ctx->sg_M;
+  const dim3 gcv((p.width1 + cb - 1) / cb, p.nstripes, nb);
+  FVO_TIMED(ctx, KN_SG_VERT, s, {
+    if (g == 8 && cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 8>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, V, M);
+    else if (g == 8) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 16, 8>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, V, M);
+    else if (cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 4>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, V, M);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 64, 4>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, V, M);
+  });
+  FVO_TIMED(ctx, KN_SG_ROWS, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_rows<D>), dim3(sg_nblk(p), nb), dim3(64), 0, s,
+                                                   V, M, p, ctx->sg_ckpt, sg_nck(p), ctx->sg_raw));
+  FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.W + 255) / 256, p.H, nb), dim3(256), 0, s,
+                                                     ctx->sg_raw, disp, p.W, p.H));
 }
 
 }  // namespace
@@ -741,16 +847,16 @@ int sgbm_init(fvo_ctx* ctx) {
   const int64_t B = c.sgbm_max_batch > 0 ? std::min(c.sgbm_max_batch, c.max_batch) : c.max_batch;
   const int64_t plane = (int64_t)p.width1 * p.D;
   int rc;
-  // sg_C: cost C, sg_V: top-down path V, each [B][HG4][width1][4][D] u16; sg_ckpt: the
-  // left->right path checkpoints; sg_raw: pre-median disparity [B][H][W]
-  const int64_t vol = (int64_t)p.HG4 * 4 * plane;
+  // sg_V: top-down path V [B][HG4 + nstripes][width1][4][D] u16 (the extra groups: the
+  // stripes' overlap rows); sg_ckpt: the left->right path checkpoints; sg_raw: pre-median
+  // disparity [B][H][W]
+  const int64_t vol = (int64_t)(p.HG4 + p.nstripes) * 4 * plane;
   const int64_t ckp = (int64_t)sg_nblk(p) * sg_nck(p) * 64 * sg_ckw(p.D);
-  if ((rc = fvo_alloc(ctx, &ctx->sg_C, B * vol)) || (rc = fvo_alloc(ctx, &ctx->sg_V, B * vol)) ||
-      (rc = fvo_alloc(ctx, &ctx->sg_ckpt, B * ckp)) || (rc = fvo_alloc(ctx, &ctx->sg_raw, B * p.H * p.W)))
+  // sg_M: min over d of every stored V row, [B][HG4 + nstripes][width1][4] u16
+  if ((rc = fvo_alloc(ctx, &ctx->sg_V, B * vol)) || (rc = fvo_alloc(ctx, &ctx->sg_M, B * vol / p.D)) ||
+      (rc = fvo_alloc(ctx, &ctx->sg_ckpt, B * ckp)) ||
+      (rc = fvo_alloc(ctx, &ctx->sg_raw, B * p.H * p.W)))
     return rc;
-  FVO_HIP(ctx, hipStreamCreateWithFlags(&ctx->sg_s2, hipStreamNonBlocking));
-  FVO_HIP(ctx, hipEventCreateWithFlags(&ctx->sg_fork, hipEventDisableTiming));
-  FVO_HIP(ctx, hipEventCreateWithFlags(&ctx->sg_join, hipEventDisableTiming));
   return 0;
 }
 

@@ -122,7 +122,11 @@ static void madd_ql(const double* q, const double* l, double s, double* c) {
 //     (Gram-Schmidt, each projection followed by an L1 rescale) and normalised.
 // Vt = those 9 rows, so the basis is rows 5..8: the Gram-Schmidt complement of the row space
 // seeded by the fixed RNG.  The reduction orders are the scalar source's (OpenCV's SIMD
-// builds may accumulate the dot products in two lanes: ulp-level, unpinned).
+// builds may accumulate the dot products in two lanes: ulp-level, unpinned).  hypot(2p, beta)
+// is evaluated as sqrt(4p^2 + beta^2) -- within an ulp of libm's hypot (no overflow at these
+// magnitudes) and, unlike hypot, the same correctly rounded operations on the host and the
+// device: an ulp of difference in one rotation grows to ~2e-9 in E through the degree-10
+// root solve (measured against the device libm's hypot), above the tests' 1e-9.
 static void null_space_5x9(const double* Q, double* basis) {
   const int m = 9, n = 5;
   const double eps = DBL_EPSILON * 10, minval = DBL_MIN;
@@ -143,7 +147,7 @@ static void null_space_5x9(const double* Q, double* basis) {
         for (int k = 0; k < m; ++k) p += A[i][k] * A[j][k];
         if (std::fabs(p) <= eps * std::sqrt(a * b)) continue;
         p *= 2;
-        const double beta = a - b, gamma = std::hypot(p, beta);
+        const double beta = a - b, gamma = std::sqrt(p * p + beta * beta);  // hypot: see above
         double c, s;
         if (beta < 0) {
           const double delta = (gamma - beta) * 0.5;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """SGBM alone on the GPU: B=64 synthetic 960x600 pairs, per-kernel times (HIP events) and
-the whole-call time, for the launch variant selected by FVO_SG_CB / FVO_SG_PF /
-FVO_SG_CHUNKS.  Prints one JSON line."""
+the whole-call time, for the cost-pass launch variant selected by FVO_SG_G / FVO_SG_CB.
+Prints one JSON line."""
 import json
 import os
 import sys
@@ -35,8 +35,9 @@ def main():
     torch.cuda.synchronize()
     st = {k: round(v[0] / n, 4) for k, v in ctx.timing_read().items()}
     ctx.timing_enable([])
-    var = {k: os.environ.get(k, "") for k in ("FVO_SG_G", "FVO_SG_CB", "FVO_SG_PF", "FVO_SG_CHUNKS")}
-    print(json.dumps({"variant": var, "call_ms": round(call_ms, 3), "kernels_ms": st}), flush=True)
+    var = {k: os.environ.get(k, "") for k in ("FVO_SG_G", "FVO_SG_CB")}
+    print(json.dumps({"variant": var, "call_ms": round(call_ms, 3), "kernels_ms": st,
+                      "workspace_gb": round(ctx.workspace_bytes / 1e9, 2)}), flush=True)
 
 
 if __name__ == "__main__":
