@@ -79,7 +79,7 @@ void fvo_config_default(fvo_config* c, int32_t width, int32_t height) {
 
 static void release(fvo_ctx* c) {
   void* ptrs[] = {c->pyr,        c->blur,      c->score,     c->rowcnt,   c->rowoff,  c->cand,     c->hel,
-                  c->ncand,      c->nsel1,     c->nsel2,     c->koff,     c->scratch, c->rt.xofs,  c->rt.xc1,
+                  c->ncand,      c->nsel1,     c->nsel2,     c->koff,     c->scratch, c->fast_rec, c->rt.xofs,  c->rt.xc1,
                   c->rt.yofs,    c->rt.yc1,    c->umax,      c->bf_sidx,  c->bf_sdist, c->bf_tidx, c->sg_ckpt,
                   c->sg_V,      c->sg_M,      c->sg_raw,    c->pnp_hyp,  c->pnp_good,
                   c->pnp_sub,    c->rs_table, c->pnp_models, c->pnp_ws, c->pnp_state, c->ba_ws, c->keepbits,
@@ -381,7 +381,9 @@ int fvo_debug_buffer(fvo_ctx* c, int which, void** ptr, int64_t* bytes) {
     case 1:  // computed on request from the last call's pyramid (not part of the hot path)
       if (orb_blur_debug(c)) return -1;
       *ptr = c->blur; *bytes = B * c->g.total_px; return 0;
-    case 2: *ptr = c->score; *bytes = B * c->g.total_px; return 0;
+    case 2:  // computed on request from the last call's pyramid (not part of the hot path)
+      if (orb_score_debug(c)) return -1;
+      *ptr = c->score; *bytes = B * c->g.total_px; return 0;
     case 3: *ptr = c->ncand; *bytes = B * c->g.nlevels * 4; return 0;
     case 4: *ptr = c->nsel1; *bytes = B * c->g.nlevels * 4; return 0;
     case 5: *ptr = c->nsel2; *bytes = B * c->g.nlevels * 4; return 0;

@@ -95,6 +95,7 @@ struct fvo_ctx {
   void* pnp_state = nullptr;      // [B] PnpState
   int32_t pnp_max_iters = 0;
   uint64_t* keepbits = nullptr;   // [B][total_rows][keep_words] FAST+NMS keep bits
+  uint8_t* fast_rec = nullptr;    // [B][tiles][2*32 + 1024] per FAST tile: row keep prefixes + kept scores
   int keep_words = 0;
   // local BA workspace (per window w < max_batch; strides in ba_* counts)
   void* ba_ws = nullptr;          // one allocation, carved per window (ba.hip)
@@ -149,6 +150,7 @@ int sgbm_run(fvo_ctx* ctx, const uint8_t* L, const uint8_t* R, int batch, int64_
 int pose_init(fvo_ctx* ctx);
 int ransac_table_init(fvo_ctx* ctx);
 int orb_blur_debug(fvo_ctx* ctx);
+int orb_score_debug(fvo_ctx* ctx);
 int backproject_run(fvo_ctx* ctx, const int16_t* disp, const float* kp0, const float* kp1, const int32_t* matches,
                     const int32_t* nmatch, int batch, int cap, const double* K, double baseline, float* P3, float* p2,
                     int32_t* npts, hipStream_t s);

@@ -121,14 +121,18 @@ __constant__ int c_cdx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2,
 __constant__ int c_cdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 
 // ------------------------------------------------------------------ FAST + NMS (tiled)
-// One block per 64 x 16 tile of a level: the image patch (tile + 4-px apron) is staged in
+// One block per 64 x 32 tile of a level: the image patch (tile + 4-px apron) is staged in
 // LDS; the FAST test runs on the tile + 1-px halo, the positions that pass are packed into
 // an LDS list so cornerScore<16> runs on dense lanes (textured frames make ~80 % of waves
 // contain a corner, so per-pixel scoring ran the score code on nearly every wave); then the
 // strict 3x3 NMS + border filter of the tile is evaluated from the LDS score tile.  Output:
-// the full score map (debug / tests), one keep bit per pixel (a 64-bit word per tile row)
-// and per-row keep counts.
+// one keep bit per pixel (a 64-bit word per tile row), per-row keep counts, and the scores of
+// the kept pixels only -- per tile a record of the rows' keep prefixes (32 u16) followed by
+// the kept scores in row-major order -- so no full-level score map crosses HBM (the score map
+// itself is produced only on request, by the SCOREMAP instance, for the debug hook).
 constexpr int kTW = 64, kTH = 32;
+constexpr int kTRec = 2 * kTH + kTH * kTW / 2;  // tile record: u16 row prefixes + <= 1024 kept scores
+
 constexpr int kFW = kTW + 2, kFH = kTH + 2;     // FAST region (NMS halo)
 constexpr int kIW = kTW + 8, kIH = kTH + 8;     // image patch (FAST radius 3 + halo)
 
@@ -140,10 +144,11 @@ __device__ __forceinline__ int tile_level(const OrbDev& G, int t) {
   return l;
 }
 
+template <bool SCOREMAP>
 __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t* __restrict__ pyr,
                                                   uint8_t* __restrict__ score, uint64_t* __restrict__ keep,
-                                                  int32_t* __restrict__ rowcnt, int64_t total, int thr, int edge,
-                                                  int kw) {
+                                                  int32_t* __restrict__ rowcnt, uint8_t* __restrict__ trec,
+                                                  int64_t total, int thr, int edge, int kw, int ntiles) {
   __shared__ uint8_t s_img[kIH][kIW];
   __shared__ uint8_t s_sc[kFH][kFW];
   __shared__ uint16_t s_list[kFH * kFW];
@@ -258,35 +263,64 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   // NMS + border filter of the tile; one wave row = 64 pixels = one keep word
   const int c = threadIdx.x & 63;
   const int x = x0 + c;
+  __shared__ unsigned long long s_m[kTH];
+  __shared__ int s_rp[kTH];
   for (int rr = threadIdx.x >> 6; rr < kTH; rr += 4) {
     const int y = y0 + rr;
-    if (y >= h) break;  // uniform per wave
-    const int s = s_sc[rr + 1][c + 1];
     bool k = false;
-    if (x < w) {
-      score[b * total + G.off[l] + (int64_t)y * w + x] = (uint8_t)s;
-      k = s && x >= edge && x < w - edge && y >= edge && y < h - edge && s > s_sc[rr][c] && s > s_sc[rr][c + 1] &&
-          s > s_sc[rr][c + 2] && s > s_sc[rr + 1][c] && s > s_sc[rr + 1][c + 2] && s > s_sc[rr + 2][c] &&
-          s > s_sc[rr + 2][c + 1] && s > s_sc[rr + 2][c + 2];
+    int sv = 0;
+    if (y < h && x < w) {  // y < h is uniform per wave
+      sv = s_sc[rr + 1][c + 1];
+      k = sv && x >= edge && x < w - edge && y >= edge && y < h - edge && sv > s_sc[rr][c] && sv > s_sc[rr][c + 1] &&
+          sv > s_sc[rr][c + 2] && sv > s_sc[rr + 1][c] && sv > s_sc[rr + 1][c + 2] && sv > s_sc[rr + 2][c] &&
+          sv > s_sc[rr + 2][c + 1] && sv > s_sc[rr + 2][c + 2];
+    }
+    if (SCOREMAP) {
+      if (y < h && x < w) score[b * total + G.off[l] + (int64_t)y * w + x] = (uint8_t)sv;
+      continue;
     }
     const unsigned long long m = __ballot(k);
     if (c == 0) {
-      const int grow = G.row0[l] + y;
-      keep[((int64_t)b * G.total_rows + grow) * kw + tx] = m;
-      if (m) atomicAdd(&rowcnt[(int64_t)b * G.total_rows + grow], __popcll(m));
+      s_m[rr] = m;
+      if (y < h) {
+        const int grow = G.row0[l] + y;
+        keep[((int64_t)b * G.total_rows + grow) * kw + tx] = m;
+        if (m) atomicAdd(&rowcnt[(int64_t)b * G.total_rows + grow], __popcll(m));
+      }
     }
+  }
+  if (SCOREMAP) return;
+  __syncthreads();
+  // tile-local prefix of the rows' keep counts (rows past the level's end hold none)
+  if (threadIdx.x < 64) {
+    const int v = threadIdx.x < kTH ? __popcll(s_m[threadIdx.x]) : 0;
+    int inc = v;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      const int u = __shfl_up(inc, o, 64);
+      if (c >= o) inc += u;
+    }
+    if (threadIdx.x < kTH) s_rp[threadIdx.x] = inc - v;
+  }
+  __syncthreads();
+  uint8_t* rec = trec + ((int64_t)b * ntiles + t) * kTRec;
+  if (threadIdx.x < kTH) reinterpret_cast<uint16_t*>(rec)[threadIdx.x] = (uint16_t)s_rp[threadIdx.x];
+  for (int rr = threadIdx.x >> 6; rr < kTH; rr += 4) {
+    const unsigned long long m = s_m[rr];
+    if ((m >> c) & 1ull) rec[2 * kTH + s_rp[rr] + __popcll(m & ((1ull << c) - 1ull))] = s_sc[rr + 1][c + 1];
   }
 }
 
-// ordered (row-major) compaction of the kept pixels: one wave per row
-__global__ __launch_bounds__(64) void k_keep_compact(const OrbDev G, const uint8_t* __restrict__ score,
+// ordered (row-major) compaction of the kept pixels: one wave per row; the scores come from
+// the tile records k_fast_nms wrote
+__global__ __launch_bounds__(64) void k_keep_compact(const OrbDev G, const uint8_t* __restrict__ trec,
                                                      const uint64_t* __restrict__ keep,
                                                      const int32_t* __restrict__ rowoff, uint32_t* __restrict__ cand,
-                                                     int64_t total, int64_t cand_total, int edge, int kw) {
+                                                     int64_t cand_total, int edge, int kw, int ntiles) {
   const int r = blockIdx.x, b = blockIdx.y;
   const int l = level_of_row(G, r);
   const int y = r - G.row0[l];
-  const int w = G.w[l], h = G.h[l];
+  const int h = G.h[l];
   if (y < edge || y >= h - edge) return;
   const int lane = threadIdx.x, ntx = G.ntx[l];
   const uint64_t* kr = keep + ((int64_t)b * G.total_rows + r) * kw;
@@ -299,16 +333,21 @@ __global__ __launch_bounds__(64) void k_keep_compact(const OrbDev G, const uint8
     if (lane >= o) inc += v;
   }
   const int pre_lane = inc - cnt;
+  // this row's records: tile (y / kTH, lane) of the level; the row's prefix inside it
+  const uint8_t* myrec = trec + ((int64_t)b * ntiles + G.tile0[l] + (y / kTH) * ntx + min(lane, ntx - 1)) * kTRec;
+  const int rpre = word ? reinterpret_cast<const uint16_t*>(myrec)[y % kTH] : 0;
   const int base = rowoff[(int64_t)b * G.total_rows + r];
-  const uint8_t* sc = score + b * total + G.off[l] + (int64_t)y * w;
   uint32_t* out = cand + b * cand_total + G.cand_off[l];
   for (int j = 0; j < ntx; ++j) {
     const unsigned long long wj = __shfl(word, j, 64);
+    if (!wj) continue;  // uniform
     const int pj = __shfl(pre_lane, j, 64);
+    const int rj = __shfl(rpre, j, 64);
     if ((wj >> lane) & 1ull) {
       const int x = 64 * j + lane;
-      out[base + pj + __popcll(wj & ((1ull << lane) - 1ull))] =
-          ((uint32_t)sc[x] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+      const int rank = __popcll(wj & ((1ull << lane) - 1ull));
+      const uint8_t* rec = trec + ((int64_t)b * ntiles + G.tile0[l] + (y / kTH) * ntx + j) * kTRec;
+      out[base + pj + rank] = ((uint32_t)rec[2 * kTH + rj + rank] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
     }
   }
 }
@@ -890,6 +929,10 @@ static int cv_round_f(float v) { return (int)lrintf(v); }
 
 }  // namespace
 
+namespace {
+OrbDev make_dev(const OrbGeom& g);
+}
+
 int orb_init(fvo_ctx* ctx) {
   const fvo_config& c = ctx->cfg;
   OrbGeom& g = ctx->g;
@@ -997,8 +1040,8 @@ int orb_init(fvo_ctx* ctx) {
   int64_t maxcand = 0;
   for (int l = 0; l < c.nlevels; ++l) maxcand = std::max<int64_t>(maxcand, g.cand_off[l + 1] - g.cand_off[l]);
   ctx->scratch_per = 2 * maxcand;
-  if ((rc = fvo_alloc(ctx, &ctx->pyr, B * g.total_px)) ||
-      (rc = fvo_alloc(ctx, &ctx->score, B * g.total_px)) || (rc = fvo_alloc(ctx, &ctx->rowcnt, B * g.total_rows)) ||
+  // (the full FAST score map, ctx->score, is allocated on first debug request)
+  if ((rc = fvo_alloc(ctx, &ctx->pyr, B * g.total_px)) || (rc = fvo_alloc(ctx, &ctx->rowcnt, B * g.total_rows)) ||
       (rc = fvo_alloc(ctx, &ctx->rowoff, B * g.total_rows)) || (rc = fvo_alloc(ctx, &ctx->cand, B * g.cand_total)) ||
       (rc = fvo_alloc(ctx, &ctx->hel, B * g.cand_total)) || (rc = fvo_alloc(ctx, &ctx->ncand, B * c.nlevels)) ||
       (rc = fvo_alloc(ctx, &ctx->nsel1, B * c.nlevels)) || (rc = fvo_alloc(ctx, &ctx->nsel2, B * c.nlevels)) ||
@@ -1008,6 +1051,7 @@ int orb_init(fvo_ctx* ctx) {
   ctx->keep_words = (g.w[0] + kTW - 1) / kTW;
   if (ctx->keep_words > 64) return fvo_fail(ctx, "ORB: image wider than 4096 px");
   if ((rc = fvo_alloc(ctx, &ctx->keepbits, B * g.total_rows * ctx->keep_words))) return rc;
+  if ((rc = fvo_alloc(ctx, &ctx->fast_rec, B * make_dev(g).tile0[g.nlevels] * kTRec))) return rc;
   return 0;
 }
 
@@ -1069,12 +1113,14 @@ int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride
                        ctx->rt.xofs + ctx->rt.xoff[l], ctx->rt.xc1 + ctx->rt.xoff[l], ctx->rt.yofs + ctx->rt.yoff[l],
                        ctx->rt.yc1 + ctx->rt.yoff[l]));
   FVO_HIP(ctx, hipMemsetAsync(ctx->rowcnt, 0, sizeof(int32_t) * (size_t)batch * g.total_rows, s));
-  FVO_TIMED(ctx, KN_ORB_FAST, s, hipLaunchKernelGGL(k_fast_nms, dim3(ntiles, batch), dim3(256), 0, s, G, ctx->pyr, ctx->score,
-                     ctx->keepbits, ctx->rowcnt, total, thr, c.edge_threshold, ctx->keep_words));
+  FVO_TIMED(ctx, KN_ORB_FAST, s, hipLaunchKernelGGL(k_fast_nms<false>, dim3(ntiles, batch), dim3(256), 0, s, G, ctx->pyr,
+                     nullptr, ctx->keepbits, ctx->rowcnt, ctx->fast_rec, total, thr, c.edge_threshold,
+                     ctx->keep_words, ntiles));
   FVO_TIMED(ctx, KN_ORB_ROW_SCAN, s, hipLaunchKernelGGL(k_row_scan, dim3(L, batch), dim3(256), 0, s, G, ctx->rowcnt, ctx->rowoff, ctx->ncand, g.total_rows,
                      L));
-  FVO_TIMED(ctx, KN_ORB_COMPACT, s, hipLaunchKernelGGL(k_keep_compact, dim3(g.total_rows, batch), dim3(64), 0, s, G, ctx->score, ctx->keepbits,
-                     ctx->rowoff, ctx->cand, total, g.cand_total, c.edge_threshold, ctx->keep_words));
+  FVO_TIMED(ctx, KN_ORB_COMPACT, s, hipLaunchKernelGGL(k_keep_compact, dim3(g.total_rows, batch), dim3(64), 0, s, G, ctx->fast_rec,
+                     ctx->keepbits, ctx->rowoff, ctx->cand, g.cand_total, c.edge_threshold, ctx->keep_words,
+                     ntiles));
   FVO_TIMED(ctx, KN_ORB_SELECT1, s, hipLaunchKernelGGL(k_select<ElemFast>, dim3(L, batch), dim3(kSelThreads), 0, s, G, ctx->cand, ctx->ncand, ctx->nsel1,
                      ctx->scratch, ctx->scratch_per, g.cand_total, L, 2));
   FVO_TIMED(ctx, KN_ORB_HARRIS, s, hipLaunchKernelGGL(k_harris, dim3(32, L, batch), dim3(256), 0, s, G, ctx->pyr, ctx->cand, ctx->nsel1, ctx->hel, total,
@@ -1103,6 +1149,27 @@ int orb_blur_debug(fvo_ctx* ctx) {
     const OrbDev G = make_dev(g);
     hipLaunchKernelGGL(k_blur, dim3(G.btile0[g.nlevels], ctx->orb_last_batch), dim3(256), 0, 0, G, ctx->pyr, ctx->blur,
                        g.total_px);
+    FVO_LAUNCH_CHECK(ctx);
+  }
+  FVO_HIP(ctx, hipDeviceSynchronize());
+  return 0;
+}
+
+// Debug hook (fvo_debug_buffer 2): the FAST score map of the last call's pyramid, which the hot
+// path does not write (k_fast_nms keeps only the kept pixels' scores).
+int orb_score_debug(fvo_ctx* ctx) {
+  if (!ctx->pyr) return fvo_fail(ctx, "orb stage not enabled");
+  const OrbGeom& g = ctx->g;
+  if (!ctx->score) {
+    int rc = fvo_alloc(ctx, &ctx->score, (int64_t)ctx->cfg.max_batch * g.total_px);
+    if (rc) return rc;
+  }
+  if (ctx->orb_last_batch > 0) {
+    const OrbDev G = make_dev(g);
+    const int ntiles = G.tile0[g.nlevels];
+    hipLaunchKernelGGL(k_fast_nms<true>, dim3(ntiles, ctx->orb_last_batch), dim3(256), 0, 0, G, ctx->pyr, ctx->score,
+                       nullptr, nullptr, nullptr, g.total_px, ctx->cfg.fast_threshold, ctx->cfg.edge_threshold,
+                       ctx->keep_words, ntiles);
     FVO_LAUNCH_CHECK(ctx);
   }
   FVO_HIP(ctx, hipDeviceSynchronize());

@@ -197,8 +197,11 @@ __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q
 // row's image bytes are loaded right after the current row is staged and taken before the
 // row's C / V stores (vmcnt retires in order: a wait for them behind the stores would also
 // wait for the stores).  Integer arithmetic as oracle/sgbm_ref.cpp (order-independent sums).
+#ifndef FVO_SG_CW
+#define FVO_SG_CW 1
+#endif
 template <int D, int CB, int G>
-__global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
+__global__ __launch_bounds__(G * CB, FVO_SG_CW) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
                                                     int64_t stride, int pitch, SgParams p, uint16_t* __restrict__ Vvol,
                                                     uint16_t* __restrict__ Mvol) {
   constexpr int DQ = D / G, PQ = DQ / 2, NV2 = DQ / 4;
@@ -326,7 +329,7 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
     // has passed this row's later barriers, i.e. finished reading sImg / sCh / sW / sPC
   };
 
-  // window shift register: win[k] = hsum(clamp(y - 3 + k)), k = 0..6, for the output row y
+  // window: win[k] = hsum(clamp(start - 3 + k)), k = 0..6, for the output row start
   uint32_t win[7][PQ], crun[PQ], st[PQ];
   fetch(start);
   hs_row(win[6], start + 1 <= H - 1 ? start + 1 : -1);
@@ -355,24 +358,8 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
   const int x1 = c0 + col;
   const int64_t plane = (int64_t)p.width1 * D;
   const int64_t colofs = (int64_t)b * (p.HG4 + p.nstripes) * 4 * plane + (int64_t)x1 * 4 * D + q * DQ;
-  for (int y = start; y < end; ++y) {
-    if (y > start) {  // window [y-3, y+3] clamped to [start, H-1]: out clamp(y-4), in clamp(y+3)
-      uint32_t nw[PQ];
-      if (y + 3 <= H - 1) {
-        hs_row(nw, y + 4 <= H - 1 ? y + 4 : -1);
-      } else {
-#pragma unroll
-        for (int j = 0; j < PQ; ++j) nw[j] = win[6][j];
-      }
-#pragma unroll
-      for (int j = 0; j < PQ; ++j) crun[j] = as_u(as_v(crun[j]) - as_v(win[0][j]) + as_v(nw[j]));
-#pragma unroll
-      for (int k = 0; k < 6; ++k)
-#pragma unroll
-        for (int j = 0; j < PQ; ++j) win[k][j] = win[k + 1][j];
-#pragma unroll
-      for (int j = 0; j < PQ; ++j) win[6][j] = nw[j];
-    }
+  // V step + stores of output row y
+  auto vrow = [&](int y) {
     minPrev = hstepG<PQ, G>(st, crun, q, P1, minPrev, p.P2);
 #pragma unroll
     for (int k = 0; k < PER; ++k) asm volatile("" : "+v"(pre[k]) :: "memory");
@@ -389,6 +376,32 @@ __global__ __launch_bounds__(G * CB) void k_sg_costvert(const uint8_t* __restric
       }
       // min over d of this V row (the next row's minPrev): the row pass's inversion needs it
       if (q == 0) Mvol[(colofs - q * DQ + yo) / D] = (uint16_t)minPrev;
+    }
+  };
+  vrow(start);
+  // rows start+1, ...: the 7-row window is a ring -- row y = start + t replaces slot (t-1) mod 7
+  // (the row leaving, y-4) by the row entering (y+3); the loop is unrolled by 7 so every slot
+  // index is static (no register shuffling).  Below H-1 the entering row is clamped, i.e. the
+  // last one entered (slot (t-2) mod 7).
+#pragma unroll 1
+  for (int y0 = start + 1; y0 < end; y0 += 7) {
+#pragma unroll
+    for (int ph = 0; ph < 7; ++ph) {
+      const int y = y0 + ph;
+      if (y >= end) break;
+      uint32_t nw[PQ];
+      if (y + 3 <= H - 1) {
+        hs_row(nw, y + 4 <= H - 1 ? y + 4 : -1);
+      } else {
+#pragma unroll
+        for (int j = 0; j < PQ; ++j) nw[j] = win[(ph + 6) % 7][j];
+      }
+#pragma unroll
+      for (int j = 0; j < PQ; ++j) {
+        crun[j] = as_u(as_v(crun[j]) - as_v(win[ph][j]) + as_v(nw[j]));
+        win[ph][j] = nw[j];
+      }
+      vrow(y);
     }
   }
 }
@@ -650,70 +663,114 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
   ldseg(0);
   // one segment; FULL (every segment but the last): 8 valid columns and a checkpoint, so the
   // body has no per-column conditions
+  // WTA of column i of a segment from its S words: first minimum over d as one u32 min of
+  // (S << 7 | d) across the row's lanes, then S[d-1] << 16 | S[d+1] from the lanes that hold
+  // them (OR across the row); every lane of the row ends with both, lane q keeps column q's
+  auto ihi_of = [&](int sg) { return min(SEG - 1, W1 - 1 - SEG * sg); };  // valid i: x' < W1
+  uint32_t wk = 0, wn = 0;
+  auto wta = [&](int i, const uint32_t* Sw) {
+    uint32_t kmin = 0xFFFFFFFFu;
+#pragma unroll
+    for (int kk = 0; kk < PQ; ++kk) {
+      const uint32_t d0 = (uint32_t)(q * DQ + 2 * kk);
+      kmin = min(kmin, ((Sw[kk] & 0xFFFFu) << 7) | d0);
+      kmin = min(kmin, ((Sw[kk] >> 16) << 7) | (d0 + 1));
+    }
+    kmin = dmin<kQX1>(kmin);
+    kmin = dmin<kQX2>(kmin);
+    kmin = dmin<kRHalfMirror>(kmin);
+    kmin = dmin<kRMirror>(kmin);
+    const int d = (int)(kmin & 127u);
+    uint32_t nb = 0;
+    {
+      const int im = d - 1 - q * DQ, ip = d + 1 - q * DQ;
+      uint32_t wm = 0, wp = 0;
+#pragma unroll
+      for (int kk = 0; kk < PQ; ++kk) {
+        wm = (im >> 1) == kk ? Sw[kk] : wm;
+        wp = (ip >> 1) == kk ? Sw[kk] : wp;
+      }
+      if (im >= 0 && im < DQ) nb |= ((im & 1) ? (wm >> 16) : (wm & 0xFFFFu)) << 16;
+      if (ip >= 0 && ip < DQ) nb |= (ip & 1) ? (wp >> 16) : (wp & 0xFFFFu);
+    }
+    nb = dor<kQX1>(nb);
+    nb = dor<kQX2>(nb);
+    nb = dor<kRHalfMirror>(nb);
+    nb = dor<kRMirror>(nb);
+    wk = q == i ? kmin : wk;
+    wn = q == i ? nb : wn;
+  };
+  // one segment.  FULL (every segment but the last: 8 valid columns and a checkpoint): the L
+  // recompute (columns 7 -> 0 = real x ascending) and the R path (0 -> 7) run interleaved --
+  // step t advances L on column 7-t and R on column t, two independent dependency chains --
+  // and each column's S is formed when its second path reaches it (the first one's state is
+  // kept as path + V).  The next segment's inputs are loaded into the registers of the
+  // columns finished at steps 4..7, its first-needed columns (7 and 0) first.  The last
+  // segment (partial) runs L, then R, column by column.
   auto segment = [&](int sg, auto full_t) {
     constexpr bool FULL = decltype(full_t)::value;
-    {
+    if constexpr (FULL) {
+      uint32_t lst[PQ], Cs[SEG][PQ], part[SEG][PQ];
+#pragma unroll
+      for (int kk = 0; kk < PQ; ++kk) lst[kk] = ckn[kk];
+      uint32_t lmin = ckn[PQ];
+      ldck(sg + 1);
+#pragma unroll
+      for (int t = 0; t < SEG; ++t) {
+        const int a = SEG - 1 - t, c = t;  // L column, R column
+        if (t < SEG / 2) {
+          derive16<PQ>(Pn[a], Vn[a], Cs[a], Mn[a], P1, p.P2);
+          derive16<PQ>(Pn[c], Vn[c], Cs[c], Mn[c], P1, p.P2);
+        }
+        lmin = step16<PQ>(lst, Cs[a], q, P1, lmin, p.P2);
+        minR = step16<PQ>(Rst, Cs[c], q, P1, minR, p.P2);
+        if (t < SEG / 2) {  // first path at both columns: keep path + V
+#pragma unroll
+          for (int kk = 0; kk < PQ; ++kk) {
+            part[a][kk] = as_u(as_v(lst[kk]) + as_v(Vn[a][kk]));
+            part[c][kk] = as_u(as_v(Rst[kk]) + as_v(Vn[c][kk]));
+          }
+        } else {  // second path: S = L + R + V
+          uint32_t Sa[PQ], Sc[PQ];
+#pragma unroll
+          for (int kk = 0; kk < PQ; ++kk) {
+            Sa[kk] = as_u(as_v(part[a][kk]) + as_v(lst[kk]));
+            Sc[kk] = as_u(as_v(part[c][kk]) + as_v(Rst[kk]));
+          }
+          wta(a, Sa);
+          wta(c, Sc);
+          const int u = t - SEG / 2;  // next segment: columns 7-u and u
+          ldcol(sg + 1, SEG - 1 - u);
+          ldcol(sg + 1, u);
+        }
+      }
+    } else {
       uint32_t lst[PQ], Ls[SEG][PQ], Cs[SEG][PQ];
-      const bool zero = FULL ? false : SEG * (sg + 1) > W1 - 1;
-      const int ihi = FULL ? SEG - 1 : min(SEG - 1, W1 - 1 - SEG * sg);  // valid i: x' < W1
+      const bool zero = SEG * (sg + 1) > W1 - 1;
       // L over the segment (i descending = real x ascending) from the checkpoint at the real
-      // column left of it, x' = SEG*(sg+1); zero state when the segment starts at x = 0.  C of
-      // each column is derived as the L path reaches it.
+      // column left of it, x' = SEG*(sg+1); zero state when the segment starts at x = 0.
 #pragma unroll
       for (int kk = 0; kk < PQ; ++kk) lst[kk] = zero ? 0u : ckn[kk];
-      minPrev = zero ? 0u : ckn[PQ];
-      uint32_t lmin = minPrev;
+      uint32_t lmin = zero ? 0u : ckn[PQ];
 #pragma unroll
       for (int i = SEG - 1; i >= 0; --i) {
         derive16<PQ>(Pn[i], Vn[i], Cs[i], Mn[i], P1, p.P2);
-        if (i <= ihi) lmin = step16<PQ>(lst, Cs[i], q, P1, lmin, p.P2);
-        // L + V at once (u16 sums, order-free): V's registers are free before the R path
+        if (i <= ihi_of(sg)) lmin = step16<PQ>(lst, Cs[i], q, P1, lmin, p.P2);
 #pragma unroll
         for (int kk = 0; kk < PQ; ++kk) Ls[i][kk] = as_u(as_v(lst[kk]) + as_v(Vn[i][kk]));
       }
-      ldck(sg + 1);
-      uint32_t wk = 0, wn = 0;
 #pragma unroll
       for (int i = 0; i < SEG; ++i) {
-        if (i > ihi) break;  // only in the last segment (no next one to load)
+        if (i > ihi_of(sg)) break;
         minR = step16<PQ>(Rst, Cs[i], q, P1, minR, p.P2);
-        // first minimum over d as one u32 min of (S << 7 | d) across the row's lanes
         uint32_t Sw[PQ];
-        uint32_t kmin = 0xFFFFFFFFu;
 #pragma unroll
-        for (int kk = 0; kk < PQ; ++kk) {
-          Sw[kk] = as_u(as_v(Ls[i][kk]) + as_v(Rst[kk]));
-          const uint32_t d0 = (uint32_t)(q * DQ + 2 * kk);
-          kmin = min(kmin, ((Sw[kk] & 0xFFFFu) << 7) | d0);
-          kmin = min(kmin, ((Sw[kk] >> 16) << 7) | (d0 + 1));
-        }
-        kmin = dmin<kQX1>(kmin);
-        kmin = dmin<kQX2>(kmin);
-        kmin = dmin<kRHalfMirror>(kmin);
-        kmin = dmin<kRMirror>(kmin);
-        const int d = (int)(kmin & 127u);
-        // S[d-1] << 16 | S[d+1] from the lanes that hold them (OR across the row)
-        uint32_t nb = 0;
-        {
-          const int im = d - 1 - q * DQ, ip = d + 1 - q * DQ;
-          uint32_t wm = 0, wp = 0;
-#pragma unroll
-          for (int kk = 0; kk < PQ; ++kk) {
-            wm = (im >> 1) == kk ? Sw[kk] : wm;
-            wp = (ip >> 1) == kk ? Sw[kk] : wp;
-          }
-          if (im >= 0 && im < DQ) nb |= ((im & 1) ? (wm >> 16) : (wm & 0xFFFFu)) << 16;
-          if (ip >= 0 && ip < DQ) nb |= (ip & 1) ? (wp >> 16) : (wp & 0xFFFFu);
-        }
-        nb = dor<kQX1>(nb);
-        nb = dor<kQX2>(nb);
-        nb = dor<kRHalfMirror>(nb);
-        nb = dor<kRMirror>(nb);
-        // every lane of the row holds the reduced key and neighbours: lane q keeps column q's
-        wk = q == i ? kmin : wk;
-        wn = q == i ? nb : wn;
-        ldcol(sg + 1, SEG - 1 - i);  // clamped columns past the row's start: harmless reads
+        for (int kk = 0; kk < PQ; ++kk) Sw[kk] = as_u(as_v(Ls[i][kk]) + as_v(Rst[kk]));
+        wta(i, Sw);
       }
+    }
+    {
+      const int ihi = FULL ? SEG - 1 : ihi_of(sg);
       // the segment's columns, one lane each (lane q of a row = column q of the segment), so
       // the sub-pixel division and the key updates run once per segment, not once per column.
       // Every ring slot reset comes before any key update: the slot column i resets (the
