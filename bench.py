@@ -256,6 +256,102 @@ def pmc_valu(shape: str):
                         for r in rows if r["kernel"].startswith(hot)}}
 
 
+def main_frames(args):
+    """--shard frames: one sequence of steps x B frame pairs split over the ranks by contiguous
+    frame-pair shards (dist.frame_shard, K-1 halo for the local BA), SURVEY §8e's strong-scaling
+    path.  Each rank renders its shard plus the halo before it, runs its
+    shard in `steps` steps of ceil(B / world) frames, then the relative poses are all-gathered
+    and chained left to right (dist.gather_relative_poses + eval.chain) -- inside the timed
+    region (W untimed passes over the shard first).  value = the sequence's frames / the
+    max-over-ranks time."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    tdist = None
+    if world > 1:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    import forest_slam_amd.build as fbuild
+    from forest_slam_amd import dist as fdist
+    from forest_slam_amd import eval as ev
+    from forest_slam_amd import synth, vo
+    if not os.path.exists(fbuild.OUT):
+        raise SystemExit("libfvo.so missing: run __graft_entry__.build() first")
+    W, H, K = args.width, args.height, args.ba_window
+    b = -(-args.batch // world)  # frames per rank per step
+    n_pairs = args.steps * args.batch
+    s, e = fdist.frame_shard(n_pairs, rank, world)
+    halo = K - 1 if K else 0
+    first = max(1, s - halo)  # pairs run before the timed shard: the BA halo
+    # the rank's frames: images first-1 .. e-1 of the one sequence (seed 0, same scene on every rank)
+    seq = synth.StereoSequence(seed=0, n_frames=n_pairs + 1, W=W, H=H, device=dev)
+    L_all, R_all = seq.frames(range(first - 1, e))
+    torch.cuda.synchronize()
+    ba_caps = {k: v for k, v in (("ba_max_landmarks", args.ba_max_landmarks), ("ba_max_obs", args.ba_max_obs)) if v}
+    fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=b, nfeatures=args.nfeatures, device=dev,
+                           ba_window=K, overlap_sgbm=bool(args.overlap_sgbm), **ba_caps)
+
+    def run():
+        fe.prime(L_all[0], R_all[0])
+        # the pairs before the shard (local indices 1 .. s-first): BA halo and warm-up
+        for a in range(1, s - first + 1, b):
+            fe.step(L_all[a:min(a + b, s - first + 1)], R_all[a:min(a + b, s - first + 1)])
+        torch.cuda.synchronize()
+        if tdist is not None:
+            tdist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        Ts, sts = [], []
+        for a in range(s - first + 1, e - first + 1, b):
+            z = min(a + b, e - first + 1)
+            T, st = fe.step(L_all[a:z], R_all[a:z])
+            Ts.append(T.clone())
+            sts.append(st.clone())
+        T_loc = torch.cat(Ts) if Ts else torch.zeros((0, 4, 4), dtype=torch.float64, device=dev)
+        st_loc = torch.cat(sts) if sts else torch.zeros((0,), dtype=torch.int32, device=dev)
+        if tdist is not None:
+            T_all, S_all = fdist.gather_relative_poses(T_loc, st_loc, n_pairs)
+        else:
+            T_all, S_all = T_loc.cpu().numpy(), st_loc.cpu().numpy()
+        cum = ev.chain(T_all, S_all != -1)
+        torch.cuda.synchronize()
+        if tdist is not None:
+            tdist.barrier()
+        return time.perf_counter() - t0, cum
+
+    for _ in range(max(args.warmup, 1)):  # whole untimed passes (rank 0's shard starts the sequence)
+        run()
+    elapsed, cum = run()
+    if tdist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        out = {
+            "metric": "stereo frames/sec (extract+match+local-BA) at 600p, 1/8 MI355X; ATE RMSE",
+            "value": round(n_pairs / elapsed, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None,
+            "dtype": "mixed: u8/u16 integer (FAST, BRIEF, Hamming, SGM), f32 (ORB angle/Harris, back-projection), "
+                     "f64 (PnP, BA incl. its Schur GEMM on f64 MFMA)",
+            "data": "synthetic: ray-cast forest stereo along the 1018_00 GT path (one sequence, seed 0)",
+            "config": {"workload": f"ONE stereo sequence of {n_pairs} frame pairs split by frame pairs over {world} "
+                                   f"GPU(s): {W}x{H}, ORB nfeatures={args.nfeatures}, BF-Hamming xcheck (L+R), "
+                                   f"SGBM-3way 96 disp, back-projection, PnP-RANSAC"
+                                   + (f", local BA K={K} ({halo}-pair halo per shard)" if K else ""),
+                       "frames_per_step": args.batch, "frames_per_step_per_gpu": b, "width": W, "height": H,
+                       "nfeatures": args.nfeatures, "parallelism": f"frame-shard x{world}"},
+            "chained_poses": int(len(cum)),
+        }
+        print(json.dumps(out), flush=True)
+    if tdist is not None:
+        tdist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -272,7 +368,12 @@ def main():
     ap.add_argument("--overlap-sgbm", type=int, default=1, help="SGBM of step k+1 on a side stream during step k")
     ap.add_argument("--ba-max-landmarks", type=int, default=0, help="per-window landmark cap (0 = library default)")
     ap.add_argument("--ba-max-obs", type=int, default=0, help="per-window observation cap (0 = library default)")
+    ap.add_argument("--shard", choices=("sequences", "frames"), default="sequences",
+                    help="sequences: one sequence per GPU, B frames per GPU per step (weak scaling, the default); "
+                         "frames: ONE sequence of steps x B frames split by frame pairs over the GPUs (strong scaling)")
     args = ap.parse_args()
+    if args.shard == "frames":
+        return main_frames(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -10,7 +10,8 @@
   before its last one: ``frame_shard(..., halo=K-1)`` starts the rank's front end K-1 images
   earlier and ``warmup_pairs`` of its first results (the windows that reach back past the
   shard start on one GPU but not here) are discarded — the previous rank owns those pairs.
-  ``frame_shard`` / ``gather_relative_poses``.
+  ``frame_shard`` / ``gather_relative_poses``; ``run_sequence_sharded`` is the whole
+  single-sequence run (bench.py --shard frames).
 * ``SequenceRank`` — one rank's step of the multi-sequence run (bench.py, tests): the
   front-end step, the latest BA window's landmarks (``fvo_ba_landmarks``), the map
   exchange (``exchange_window_map``) and the multi-sequence map built from it
@@ -53,7 +54,9 @@ def gather_relative_poses(T_local: torch.Tensor, status_local: torch.Tensor, n_p
     """All-gather every rank's relative transforms (f64 [n_r,4,4]) and statuses into the
     full per-pair arrays (rank order == frame order)."""
     world = dist.get_world_size(group)
-    dev = T_local.device
+    # gloo (CPU tests, or GPU ranks sharing one card) all-gathers host tensors
+    dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else T_local.device
+    T_local, status_local = T_local.to(dev), status_local.to(dev)
     counts = [frame_shard(n_pairs, r, world) for r in range(world)]
     maxn = max(e - s for s, e in counts)
     padT = torch.zeros((maxn, 4, 4), dtype=torch.float64, device=dev)
@@ -67,6 +70,44 @@ def gather_relative_poses(T_local: torch.Tensor, status_local: torch.Tensor, n_p
     T = np.concatenate([outT[r][:e - s].cpu().numpy() for r, (s, e) in enumerate(counts)])
     S = np.concatenate([outS[r][:e - s].cpu().numpy() for r, (s, e) in enumerate(counts)])
     return T, S
+
+
+def run_sequence_sharded(make_frontend, L_all: torch.Tensor, R_all: torch.Tensor, stamps=None, use_ba: bool = True,
+                         group=None):
+    """One sequence split over the ranks by frame pairs (the strong-scaling
+    path): rank r runs the pairs frame_shard(n-1, r, world) on its own front end
+    (``make_frontend()``), starting K-1 pairs early when local BA is on (``frame_shard(...,
+    halo=K-1)``, so every owned pair's BA window spans the same K frames as on one GPU) and
+    dropping those warm-up results; the relative poses and statuses are all-gathered
+    (``gather_relative_poses``) and every rank composes the chain left to right in float64
+    (stereo_slam.py:306, ``eval.chain``).  Returns what ``vo.run_sequence`` returns on one
+    GPU for the whole sequence: (TUM rows, relative T, statuses) -- bit-identical to it."""
+    from . import eval as ev
+    from .vo import _check_overflow
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    n_pairs = L_all.shape[0] - 1
+    fe = make_frontend()
+    halo = fe.ba_window - 1 if (fe.ba_window and use_ba) else 0
+    s, e = frame_shard(n_pairs, rank, world, halo=halo)
+    drop = warmup_pairs(n_pairs, rank, world, halo)
+    Ts, sts = [], []
+    if e > s:
+        fe.prime(L_all[s - 1], R_all[s - 1])
+        for a in range(s, e, fe.B):
+            b = min(a + fe.B, e)
+            T, st = fe.step(L_all[a:b], R_all[a:b])
+            Ts.append((T if use_ba else fe.T[:b - a]).clone())
+            sts.append(st.clone())
+    dev = L_all.device
+    T_local = torch.cat(Ts)[drop:] if Ts else torch.zeros((0, 4, 4), dtype=torch.float64, device=dev)
+    st_local = torch.cat(sts)[drop:] if sts else torch.zeros((0,), dtype=torch.int32, device=dev)
+    T, S = gather_relative_poses(T_local, st_local, n_pairs, group)
+    _check_overflow(S)
+    valid = S != -1
+    cum = ev.chain(T, valid)
+    if stamps is None:
+        stamps = np.arange(n_pairs + 1, dtype=np.float64)
+    return ev.tum_rows(np.asarray(stamps)[1:][valid], cum), T, S
 
 
 def exchange_window_map(T_step: torch.Tensor, st_step: torch.Tensor, lm_xyz: torch.Tensor, lm_count: torch.Tensor,

@@ -213,3 +213,41 @@ def test_overlapped_step_waits_for_prime_without_sync():
     got = [fe.step(L[s:s + 2], R[s:s + 2])[0].cpu().numpy().copy() for s in (1, 3)]
     for w, g in zip(want, got):
         assert np.array_equal(w, g)
+
+
+def _shard_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from forest_slam_amd import dist as fd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    seq, L, R = _frames(36, 15, start=90)
+    res = {}
+    for ba in (3, 0):
+        rows, T, S = fd.run_sequence_sharded(lambda: _fe(seq, 4, ba_window=ba), L, R, stamps=seq.t)
+        res[ba] = (rows, T, S)
+    out[rank] = res
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_frame_sharded_sequence_equals_single_gpu_run():
+    """dist.run_sequence_sharded -- one sequence's frame pairs split over two
+    ranks (on the box's one GPU, gloo), K-1 halo for the local BA, all-gather of the relative
+    poses, left-to-right chain -- gives vo.run_sequence's TUM rows, transforms and statuses bit
+    for bit, with local BA (K = 3) and PnP only."""
+    import torch.multiprocessing as mp
+    from forest_slam_amd import vo
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_shard_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    seq, L, R = _frames(36, 15, start=90)
+    for ba in (3, 0):
+        rows, T, S = vo.run_sequence(_fe(seq, 4, ba_window=ba), L, R, stamps=seq.t, use_ba=bool(ba))
+        for r in range(2):
+            g_rows, g_T, g_S = out[r][ba]
+            assert np.array_equal(g_S, S) and np.array_equal(g_T, T), (ba, r)
+            assert np.array_equal(g_rows, rows), (ba, r)
