@@ -117,6 +117,29 @@ __device__ int block_scan(int v, int* s_tmp, int* total) {
   return pre + x - v;
 }
 
+// the same for a block of NT threads
+template <int NT>
+__device__ int block_scan_n(int v, int* s_tmp, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_tmp[wid] = x;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NT / 64; ++k) {
+    if (k < wid) pre += s_tmp[k];
+    tot += s_tmp[k];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
 // deterministic block sum of doubles (fixed tree); result valid in every thread
 __device__ double block_sum(double v, double* s_red) {
   v = wave_sum(v);
@@ -242,10 +265,17 @@ __device__ __forceinline__ bool ba_outlier(const double* T, const double* X, con
 }
 
 // ------------------------------------------------------------------ problem construction
-__global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims dm, int first_end, int first_valid) {
-  extern __shared__ uint8_t s_tracked[];  // [cap]
+// One 512-thread block per window.  The forward match maps of the window's frames live in
+// LDS as u16 (LMAP; the global v.next copy when they do not fit), so following a track -- a
+// chain of dependent lookups up to K-1 long -- costs LDS latency, not L2 / HBM latency; each
+// candidate records its chain in registers on the first walk, and the keypoints along it are
+// then loaded all at once.
+constexpr int kBuildBlock = 512;
+template <bool LMAP>
+__global__ __launch_bounds__(kBuildBlock) void k_ba_build(BaIn in, void* ws, BaDims dm, int first_end, int first_valid) {
+  extern __shared__ uint8_t s_dyn[];  // LMAP: [K-1][cap] u16 maps, then [cap] tracked flags
   __shared__ double sT[kKMax][12];
-  __shared__ int s_tmp[kBlock / 64];
+  __shared__ int s_tmp[kBuildBlock / 64];
   __shared__ int s_L, s_O, s_stop;
   const int w = blockIdx.x, tid = threadIdx.x;
   const int e = first_end + w;
@@ -254,6 +284,15 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
   BaWin v = view(ws, dm, w);
   BaState* S = v.st;
   const int cap = dm.cap;
+  uint16_t* s_next = reinterpret_cast<uint16_t*>(s_dyn);
+  uint8_t* s_tracked = LMAP ? s_dyn + 2 * (dm.K - 1) * cap : s_dyn;
+  auto nxt = [&](int k, int b) -> int {
+    if (LMAP) {
+      const int r = s_next[k * cap + b];
+      return r == 0xFFFF ? -1 : r;
+    }
+    return v.next[k * cap + b];
+  };
   if (tid == 0) {
     S->L = 0;
     S->O = 0;
@@ -275,52 +314,64 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
   }
   // forward match maps of frames s..e-1
   for (int k = 0; k + 1 < n; ++k)
-    for (int i = tid; i < cap; i += kBlock) v.next[k * cap + i] = -1;
+    for (int i = tid; i < cap; i += kBuildBlock) {
+      if (LMAP) s_next[k * cap + i] = 0xFFFF;
+      else v.next[k * cap + i] = -1;
+    }
   __syncthreads();
   for (int k = 0; k + 1 < n; ++k) {
     const int f = s + k, M = min(max(in.nmatch[f], 0), cap);
     const int32_t* m = in.matches + (int64_t)f * cap * 3;
-    for (int r = tid; r < M; r += kBlock) v.next[k * cap + m[3 * r]] = m[3 * r + 1];
+    for (int r = tid; r < M; r += kBuildBlock) {
+      if (LMAP) s_next[k * cap + m[3 * r]] = (uint16_t)m[3 * r + 1];
+      else v.next[k * cap + m[3 * r]] = m[3 * r + 1];
+    }
   }
   __syncthreads();
   for (int j = 0; j + 1 < n; ++j) {
     const int f = s + j;
-    for (int i = tid; i < cap; i += kBlock) s_tracked[i] = 0;
+    for (int i = tid; i < cap; i += kBuildBlock) s_tracked[i] = 0;
     __syncthreads();
     if (j > 0) {
       const int Mp = min(max(in.nmatch[f - 1], 0), cap);
       const int32_t* mp = in.matches + (int64_t)(f - 1) * cap * 3;
-      for (int r = tid; r < Mp; r += kBlock) s_tracked[mp[3 * r + 1]] = 1;
+      for (int r = tid; r < Mp; r += kBuildBlock) s_tracked[mp[3 * r + 1]] = 1;
     }
     __syncthreads();
     const int M = min(max(in.nmatch[f], 0), cap);
     const int32_t* m = in.matches + (int64_t)f * cap * 3;
     const double* Tj = sT[j];
-    for (int base = 0; base < M; base += kBlock) {
+    for (int base = 0; base < M; base += kBuildBlock) {
       if (s_stop) break;  // uniform: written before the last barrier
       const int r = base + tid;
       bool cand = false;
-      int len = 0, q = 0, t = 0;
+      int len = 0, q = 0;
+      int bs[kKMax - 1];  // the track's keypoint in frames j+1, j+2, ... (static indices only)
       float4 sp = make_float4(0.f, 0.f, 0.f, 0.f);
       if (r < M) {
         q = m[3 * r];
-        t = m[3 * r + 1];
+        bs[0] = m[3 * r + 1];
         sp = in.stereo[(int64_t)f * cap + q];
         cand = !s_tracked[q] && sp.z > 0.f;
       }
       if (cand) {
         len = 2;
-        int b = t;
-        for (int k = j + 1; k + 1 < n; ++k) {
-          const int nb = v.next[k * cap + b];
-          if (nb < 0) break;
-          b = nb;
-          ++len;
+        bool go = true;
+#pragma unroll
+        for (int kk = 1; kk < kKMax - 1; ++kk) {  // frame j + kk + 1 from frame j + kk
+          const int k = j + kk;
+          if (go && k + 1 < n) {
+            const int nb = nxt(k, bs[kk - 1]);
+            if (nb < 0) go = false;
+            else { bs[kk] = nb; ++len; }
+          } else {
+            go = false;
+          }
         }
       }
       // one scan of (observations << 10 | candidate): len <= 21, so both sums fit
       int tp;
-      const int packed = block_scan((len << 10) | (cand ? 1 : 0), s_tmp, &tp);
+      const int packed = block_scan_n<kBuildBlock>((len << 10) | (cand ? 1 : 0), s_tmp, &tp);
       const int lid = packed & 1023, oof = packed >> 10, tl = tp & 1023, to = tp >> 10;
       const int L0 = s_L, O0 = s_O;
       // creation stops at the first landmark that does not fit (the failing rows are a
@@ -340,19 +391,25 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
         const float* kq = in.kp + ((int64_t)f * cap + q) * FVO_KP_STRIDE;
         const int oq = min(max((int)kq[5], 0), in.nlev - 1);
         v.obs[o++] = BaObs{id, (short)j, (short)oq, kq[0], kq[1], kq[0] - sp.w};
-        int b = t;
-        for (int k = j + 1;; ++k) {
-          const float* kb = in.kp + ((int64_t)(s + k) * cap + b) * FVO_KP_STRIDE;
-          const int ob = min(max((int)kb[5], 0), in.nlev - 1);
-          v.obs[o++] = BaObs{id, (short)k, (short)ob, kb[0], kb[1], __builtin_nanf("")};
-          if (k + 1 >= n) break;
-          const int nb = v.next[k * cap + b];
-          if (nb < 0) break;
-          b = nb;
-        }
+        // the track's keypoints: every load issued before the first observation is written
+        float ku[kKMax - 1], kvv[kKMax - 1], ko[kKMax - 1];
+#pragma unroll
+        for (int kk = 0; kk < kKMax - 1; ++kk)
+          if (kk < len - 1) {
+            const float* kb = in.kp + ((int64_t)(s + j + 1 + kk) * cap + bs[kk]) * FVO_KP_STRIDE;
+            ku[kk] = kb[0];
+            kvv[kk] = kb[1];
+            ko[kk] = kb[5];
+          }
+#pragma unroll
+        for (int kk = 0; kk < kKMax - 1; ++kk)
+          if (kk < len - 1) {
+            const int ob = min(max((int)ko[kk], 0), in.nlev - 1);
+            v.obs[o++] = BaObs{id, (short)(j + 1 + kk), (short)ob, ku[kk], kvv[kk], __builtin_nanf("")};
+          }
       }
       int tot_ok = to;
-      if (!allfit) (void)block_scan(ok ? len : 0, s_tmp, &tot_ok);
+      if (!allfit) (void)block_scan_n<kBuildBlock>(ok ? len : 0, s_tmp, &tot_ok);
       if (tid == 0) {
         s_L = L0 + nok;
         s_O = O0 + tot_ok;
@@ -366,13 +423,13 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
   __syncthreads();
   const int L = s_L, O = s_O;
   // per-frame observation lists (stable, landmark-major order inside a frame): a counting
-  // sort -- frame sizes by LDS atomics, then per 256-observation chunk every wave ranks its
+  // sort -- frame sizes by LDS atomics, then per 512-observation chunk every wave ranks its
   // lanes within each frame by ballots, the waves' counts give the chunk's offsets (three
   // barriers per chunk instead of two per frame per chunk)
-  __shared__ int s_fcnt[kKMax], s_foff[kKMax], s_wcnt[kBlock / 64][kKMax];
+  __shared__ int s_fcnt[kKMax], s_foff[kKMax], s_wcnt[kBuildBlock / 64][kKMax];
   if (tid < kKMax) s_fcnt[tid] = 0;
   __syncthreads();
-  for (int i = tid; i < O; i += kBlock) atomicAdd(&s_fcnt[v.obs[i].frame], 1);
+  for (int i = tid; i < O; i += kBuildBlock) atomicAdd(&s_fcnt[v.obs[i].frame], 1);
   __syncthreads();
   if (tid == 0) {
     int acc = 0;
@@ -386,7 +443,7 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
   __syncthreads();
   const int lane = tid & 63, wid = tid >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  for (int base = 0; base < O; base += kBlock) {
+  for (int base = 0; base < O; base += kBuildBlock) {
     const int i = base + tid;
     const int f = i < O ? (int)v.obs[i].frame : -1;
     int rank = 0;
@@ -404,7 +461,7 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
     __syncthreads();
     if (tid < n) {
       int c = 0;
-      for (int w2 = 0; w2 < kBlock / 64; ++w2) c += s_wcnt[w2][tid];
+      for (int w2 = 0; w2 < kBuildBlock / 64; ++w2) c += s_wcnt[w2][tid];
       s_foff[tid] += c;
     }
     __syncthreads();
@@ -421,7 +478,7 @@ __global__ __launch_bounds__(kBlock) void k_ba_build(BaIn in, void* ws, BaDims d
     S->cost = 0.0;
     S->cost0 = 0.0;
   }
-  for (int i = tid; i < n * 12; i += kBlock) S->T[i / 12][i % 12] = sT[i / 12][i % 12];
+  for (int i = tid; i < n * 12; i += kBuildBlock) S->T[i / 12][i % 12] = sT[i / 12][i % 12];
 }
 
 // ------------------------------------------------------------------ LM iteration kernels
@@ -642,8 +699,9 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
   }
 }
 
-// reduced camera system, Cholesky, pose step and tentative poses
-__global__ __launch_bounds__(kBlock) void k_ba_solve(void* ws, BaDims dm) {
+// reduced camera system, Cholesky, pose step and tentative poses; 512 threads per window
+constexpr int kSolveBlock = 512, kSGA = 16, kSGB = 32;  // kSGA x kSGB thread grid over (i, j)
+__global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
   extern __shared__ double sS[];  // [np*np] + rhs[np]
   const BaWin v = view(ws, dm, blockIdx.x);
   BaState* S = v.st;
@@ -654,29 +712,45 @@ __global__ __launch_bounds__(kBlock) void k_ba_solve(void* ws, BaDims dm) {
   const int nch0 = (L + dm.LPC - 1) / dm.LPC, nch = nch0 < dm.NPART ? nch0 : dm.NPART;  // partials used
   const double lam = S->lam;
   double* rhs = sS + np * np;
-  // S = H_pp + lam diag + 1e-6 I - sum_c G_c (upper triangle computed, mirrored); 16 x 16
-  // thread grid over (a, b), no integer division
-  const int ta = tid >> 4, tb = tid & 15;
-  for (int a = ta; a < np; a += 16) {
+  // S = H_pp + lam diag + 1e-6 I - sum_c G_c (upper triangle, mirrored).  A thread takes 4
+  // consecutive columns b0..b0+3 of a row a (b0 from the row's diagonal 16 x 16 tile, which
+  // k_ba_lin writes in full) and loads the 4-wide slices of every partial before summing, so
+  // the partials' reads are all in flight at once.  Partial order kept (c ascending).
+  const int nq = (np + 3) / 4;  // column quads per row
+  for (int t = tid; t < np * nq; t += kSolveBlock) {
+    const int a = t / nq, b0 = 4 * (t - a * nq);
+    if (b0 + 3 < a) continue;
+    typedef double d4 __attribute__((ext_vector_type(4)));
+    d4 gs = {0.0, 0.0, 0.0, 0.0};
+    const d4* gp = reinterpret_cast<const d4*>(v.Gp + a * NR + b0);
+#pragma unroll
+    for (int c0 = 0; c0 < kLinParts; c0 += 8) {  // 8 slices in flight per batch (VGPR budget)
+      d4 part[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (c0 + c < nch) part[c] = gp[(int64_t)(c0 + c) * NR * NR / 4];
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (c0 + c < nch) gs += part[c];
+    }
     const int fa = a / 6 + 1, ia = a - 6 * (fa - 1);
-    for (int b = a + tb; b < np; b += 16) {
-      const int fb = b / 6 + 1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int bb = b0 + u;
+      if (bb < a || bb >= np) continue;
+      const int fb = bb / 6 + 1;
       double hv = 0.0;
       if (fa == fb) {
-        const int i = ia, j = b - 6 * (fb - 1);
+        const int i = ia, j = bb - 6 * (fb - 1);
         const int q = i * 6 - i * (i - 1) / 2 + (j - i);
         hv = S->Hpp[fa][q];
         if (i == j) hv += lam * hv + 1e-6;
       }
-      double gs = 0.0;  // chunk order kept; the loads are issued 8 ahead of the adds
-      const double* gp = v.Gp + a * NR + b;
-#pragma unroll 8
-      for (int c = 0; c < nch; ++c) gs += gp[(int64_t)c * NR * NR];
-      sS[a * np + b] = hv - gs;
-      sS[b * np + a] = hv - gs;
+      sS[a * np + bb] = hv - gs[u];
+      sS[bb * np + a] = hv - gs[u];
     }
   }
-  for (int a = tid; a < np; a += kBlock) {
+  for (int a = tid; a < np; a += kSolveBlock) {
     double gs = 0.0;
     const double* gp = v.Gp + a * NR + NR - 1;
 #pragma unroll 8
@@ -684,6 +758,7 @@ __global__ __launch_bounds__(kBlock) void k_ba_solve(void* ws, BaDims dm) {
     rhs[a] = -S->Hpp[a / 6 + 1][21 + a % 6] + gs;
   }
   __syncthreads();
+  const int ta = tid / kSGB, tb = tid % kSGB;
   // Right-looking Cholesky by panels of kChol columns, two barriers per panel: (A) every
   // thread factors the panel's diagonal block itself (identical arithmetic everywhere, so
   // the pivots need no broadcast), (B) one thread per row below solves the row's panel
@@ -718,7 +793,7 @@ __global__ __launch_bounds__(kBlock) void k_ba_solve(void* ws, BaDims dm) {
       }
     }
     if (fail) break;  // uniform: every thread computed the same pivots
-    for (int i = k + pw + tid; i < np; i += kBlock) {
+    for (int i = k + pw + tid; i < np; i += kSolveBlock) {
       double x[kChol];
 #pragma unroll
       for (int a2 = 0; a2 < kChol; ++a2) {
@@ -733,11 +808,11 @@ __global__ __launch_bounds__(kBlock) void k_ba_solve(void* ws, BaDims dm) {
       }
     }
     __syncthreads();
-    for (int i = k + pw + ta; i < np; i += 16) {
+    for (int i = k + pw + ta; i < np; i += kSGA) {
       double li[kChol];
 #pragma unroll
       for (int a2 = 0; a2 < kChol; ++a2) li[a2] = a2 < pw ? sS[i * np + k + a2] : 0.0;
-      for (int j = k + pw + tb; j <= i; j += 16) {
+      for (int j = k + pw + tb; j <= i; j += kSGB) {
         double v2 = sS[i * np + j];
 #pragma unroll
         for (int a2 = 0; a2 < kChol; ++a2)
@@ -788,7 +863,7 @@ __global__ __launch_bounds__(kBlock) void k_ba_solve(void* ws, BaDims dm) {
     if (r1 < np) rhs[r1] = x1;
   }
   __syncthreads();
-  for (int a = tid; a < 6 * n; a += kBlock) S->dp[a] = a < 6 ? 0.0 : rhs[a - 6];
+  for (int a = tid; a < 6 * n; a += kSolveBlock) S->dp[a] = a < 6 ? 0.0 : rhs[a - 6];
   if (tid < n) {
     const int f = tid;
     double* Tt = S->Tt[f];
@@ -964,6 +1039,12 @@ BaDims make_dims(const fvo_ctx* ctx) {
   return d;
 }
 
+// k_ba_build's dynamic LDS: the u16 match maps + tracked flags when they fit (and cap < 65535),
+// else the flags alone (maps in the global workspace)
+size_t build_shm(const BaDims& d) {
+  const size_t maps = (size_t)2 * (d.K - 1) * d.cap + d.cap;
+  return (d.cap < 0xFFFF && maps <= 156 * 1024) ? maps : (size_t)d.cap;  // + ~4 KB static <= 160 KiB
+}
 size_t lin_shm(const BaDims& d) { return (size_t)8 * (3 * d.LPC * (d.NR + 2) + 9 * d.LPC * d.K + 6 * d.LPC); }
 size_t solve_shm(int K) {
   const int np = 6 * (K - 1);
@@ -982,7 +1063,13 @@ int ba_init(fvo_ctx* ctx) {
   int rc = fvo_alloc(ctx, &p, (size_t)d.win * c.max_batch);
   if (rc) return rc;
   ctx->ba_ws = p;
-  // dynamic LDS above 64 KiB: the MFMA slice always, the reduced system for K > 11
+  FVO_HIP(ctx, hipStreamCreateWithFlags(&ctx->ba_s2, hipStreamNonBlocking));
+  FVO_HIP(ctx, hipEventCreateWithFlags(&ctx->ba_fork, hipEventDisableTiming));
+  FVO_HIP(ctx, hipEventCreateWithFlags(&ctx->ba_join, hipEventDisableTiming));
+  // dynamic LDS above 64 KiB: the MFMA slice always, the reduced system for K > 11, the match maps
+  if (build_shm(d) > 65536)
+    FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_build<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)build_shm(d)));
   FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_lin, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lin_shm(d)));
   if (solve_shm(c.ba_window) > 65536)
@@ -1002,6 +1089,37 @@ int ba_stereo_run(fvo_ctx* ctx, const int16_t* disp, const float* kp, const int3
   return 0;
 }
 
+namespace {
+// build + LM iterations + final transform of windows [w0, w0 + nw) on stream s
+void ba_windows_launch(fvo_ctx* ctx, const BaIn& in, const BaCam& cam, const BaDims& d, int w0, int nw, int first_end,
+                       int first_valid, int iters, double* Tout, double* stats, hipStream_t s) {
+  void* ws = static_cast<char*>(ctx->ba_ws) + (int64_t)d.win * w0;
+  const int fe = first_end + w0;
+  const size_t shb = build_shm(d);
+  if (shb > (size_t)d.cap)
+    hipLaunchKernelGGL(k_ba_build<true>, dim3(nw), dim3(kBuildBlock), shb, s, in, ws, d, fe, first_valid);
+  else
+    hipLaunchKernelGGL(k_ba_build<false>, dim3(nw), dim3(kBuildBlock), shb, s, in, ws, d, fe, first_valid);
+  const dim3 gcu(nw, d.NCU), gch(nw, d.NPART), gfr(nw, d.K - 1);
+  const size_t shl = lin_shm(d), shs = solve_shm(d.K);
+  hipLaunchKernelGGL(k_ba_cost, gcu, dim3(kBlock), 0, s, in, ws, d, cam, 0);
+  hipLaunchKernelGGL(k_ba_setcost, dim3(nw), dim3(64), 0, s, ws, d, 1);
+  for (int it = 0; it < iters; ++it) {
+    if (it == iters / 2 && iters >= 2) {  // outlier rejection, then the cost of the kept set
+      hipLaunchKernelGGL(k_ba_cost, gcu, dim3(kBlock), 0, s, in, ws, d, cam, 1);
+      hipLaunchKernelGGL(k_ba_setcost, dim3(nw), dim3(64), 0, s, ws, d, 0);
+    }
+    hipLaunchKernelGGL(k_ba_pp, gfr, dim3(kBlock), 0, s, in, ws, d, cam);
+    hipLaunchKernelGGL(k_ba_lin, gch, dim3(kLinBlock), shl, s, in, ws, d, cam);
+    hipLaunchKernelGGL(k_ba_solve, dim3(nw), dim3(kSolveBlock), shs, s, ws, d);
+    hipLaunchKernelGGL(k_ba_upd, gcu, dim3(kBlock), 0, s, in, ws, d, cam);
+    hipLaunchKernelGGL(k_ba_accept, dim3(nw), dim3(64), 0, s, ws, d);
+  }
+  hipLaunchKernelGGL(k_ba_final, dim3(nw), dim3(64), 0, s, in.Trel, ws, d, fe, Tout + 16 * (int64_t)w0,
+                     stats + 6 * (int64_t)w0);
+}
+}  // namespace
+
 int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* matches, const int32_t* nmatch,
            const float* stereo, const double* Trel, int nframes, int cap, int first_end, int nwin, int first_valid,
            const double* K, double baseline, const double* inv_sigma2, int nlev, int iters, double* Tout,
@@ -1016,26 +1134,22 @@ int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* mat
   BaIn in{kp, nkp, matches, nmatch, reinterpret_cast<const float4*>(stereo), Trel, {}, nlev};
   for (int i = 0; i < nlev; ++i) in.isig2[i] = inv_sigma2[i];
   const BaCam cam{K[0], K[4], K[2], K[5], baseline};
-  void* ws = ctx->ba_ws;
-  FVO_TIMED(ctx, KN_BA_BUILD, s,
-            hipLaunchKernelGGL(k_ba_build, dim3(nwin), dim3(kBlock), (size_t)cap, s, in, ws, d, first_end, first_valid));
-  const dim3 gcu(nwin, d.NCU), gch(nwin, d.NPART), gfr(nwin, d.K - 1);
-  const size_t shl = lin_shm(d), shs = solve_shm(d.K);
+  // The windows are independent: the batch is split in two halves whose LM sequences run on
+  // two streams, so one half's latency-bound kernels (build, the per-window solve on one
+  // block each) overlap the other half's whole-GPU kernels instead of leaving most CUs idle.
+  const int nh = nwin >= 8 ? (nwin + 1) / 2 : nwin;
+  const bool two = nh < nwin;
+  if (two) {
+    FVO_HIP(ctx, hipEventRecord(ctx->ba_fork, s));
+    FVO_HIP(ctx, hipStreamWaitEvent(ctx->ba_s2, ctx->ba_fork, 0));
+  }
   FVO_TIMED(ctx, KN_BA_SOLVE, s, {
-    hipLaunchKernelGGL(k_ba_cost, gcu, dim3(kBlock), 0, s, in, ws, d, cam, 0);
-    hipLaunchKernelGGL(k_ba_setcost, dim3(nwin), dim3(64), 0, s, ws, d, 1);
-    for (int it = 0; it < iters; ++it) {
-      if (it == iters / 2 && iters >= 2) {  // outlier rejection, then the cost of the kept set
-        hipLaunchKernelGGL(k_ba_cost, gcu, dim3(kBlock), 0, s, in, ws, d, cam, 1);
-        hipLaunchKernelGGL(k_ba_setcost, dim3(nwin), dim3(64), 0, s, ws, d, 0);
-      }
-      hipLaunchKernelGGL(k_ba_pp, gfr, dim3(kBlock), 0, s, in, ws, d, cam);
-      hipLaunchKernelGGL(k_ba_lin, gch, dim3(kLinBlock), shl, s, in, ws, d, cam);
-      hipLaunchKernelGGL(k_ba_solve, dim3(nwin), dim3(kBlock), shs, s, ws, d);
-      hipLaunchKernelGGL(k_ba_upd, gcu, dim3(kBlock), 0, s, in, ws, d, cam);
-      hipLaunchKernelGGL(k_ba_accept, dim3(nwin), dim3(64), 0, s, ws, d);
+    ba_windows_launch(ctx, in, cam, d, 0, nh, first_end, first_valid, iters, Tout, stats, s);
+    if (two) ba_windows_launch(ctx, in, cam, d, nh, nwin - nh, first_end, first_valid, iters, Tout, stats, ctx->ba_s2);
+    if (two) {
+      (void)hipEventRecord(ctx->ba_join, ctx->ba_s2);
+      (void)hipStreamWaitEvent(s, ctx->ba_join, 0);
     }
-    hipLaunchKernelGGL(k_ba_final, dim3(nwin), dim3(64), 0, s, Trel, ws, d, first_end, Tout, stats);
   });
   FVO_LAUNCH_CHECK(ctx);
   return 0;

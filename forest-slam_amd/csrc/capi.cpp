@@ -86,6 +86,9 @@ static void release(fvo_ctx* c) {
                   c->em_x, c->em_models, c->em_good, c->em_nmod, c->em_state, c->em_ws};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (c->ba_s2) (void)hipStreamDestroy(c->ba_s2);
+  if (c->ba_fork) (void)hipEventDestroy(c->ba_fork);
+  if (c->ba_join) (void)hipEventDestroy(c->ba_join);
 }
 
 int fvo_create(int device, const fvo_config* cfg, fvo_ctx** out) {

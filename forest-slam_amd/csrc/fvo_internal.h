@@ -100,6 +100,8 @@ struct fvo_ctx {
   // local BA workspace (per window w < max_batch; strides in ba_* counts)
   void* ba_ws = nullptr;          // one allocation, carved per window (ba.hip)
   int64_t ba_win_bytes = 0;
+  hipStream_t ba_s2 = nullptr;    // second stream: half of the windows' LM sequences (ba.hip)
+  hipEvent_t ba_fork = nullptr, ba_join = nullptr;
   // mono (essential matrix) workspace
   double* em_x = nullptr;         // [B][cap][4] normalised (x1, y1, x2, y2)
   double* em_models = nullptr;    // [B][max_iters][10][9] 5-point solutions
