@@ -12,7 +12,9 @@ import numpy as np
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfvo.so")
+# FVO_LIB: an alternative build of the same library (launch-shape experiments, tools/
+# build_variant.py); the product path is the in-tree libfvo.so
+LIB_PATH = os.environ.get("FVO_LIB") or os.path.join(_HERE, "libfvo.so")
 
 KP_STRIDE = 8
 DESC_BYTES = 32

@@ -48,7 +48,13 @@ constexpr int kBlock = 256;
 // k_ba_lin: blocks per window; block p reduces the landmark chunks p, p + kLinParts, ... into
 // one partial Schur product (MFMA accumulators kept across its chunks), so k_ba_solve sums
 // kLinParts partials instead of one per chunk.  Fixed chunk order: deterministic.
-constexpr int kLinParts = 16;
+#ifndef FVO_BA_PARTS
+#define FVO_BA_PARTS 16
+#endif
+#ifndef FVO_BA_LPC64
+#define FVO_BA_LPC64 64
+#endif
+constexpr int kLinParts = FVO_BA_PARTS;
 // k_ba_lin runs 16 waves per block: its LDS slice (up to 150 KB) allows one block per CU, so
 // the block's own waves are all the latency hiding the CU gets
 constexpr int kLinWaves = 16, kLinBlock = 64 * kLinWaves;
@@ -1012,7 +1018,9 @@ BaDims make_dims(const fvo_ctx* ctx) {
   d.K = c.ba_window;
   d.cap = ctx->kp_cap;
   d.NR = 6 * (d.K - 1) < 63 ? 64 : 128;
-  d.LPC = d.NR == 64 ? 64 : 32;  // LDS slice 3 LPC x (NR + 2) doubles <= 99 KB
+  // landmarks per k_ba_lin chunk: LDS slice 3 LPC x (NR + 2) doubles <= 99 KB (+ the chunk's
+  // observation terms); measured: halving LPC (two blocks per CU) is slower at both shapes
+  d.LPC = d.NR == 64 ? FVO_BA_LPC64 : FVO_BA_LPC64 / 2;
   d.NCH = (d.Lmax + d.LPC - 1) / d.LPC;
   d.NPART = d.NCH < kLinParts ? d.NCH : kLinParts;
   d.NCU = (d.Lmax + kBlock - 1) / kBlock;
