@@ -1145,7 +1145,10 @@ int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* mat
   // The windows are independent: the batch is split in two halves whose LM sequences run on
   // two streams, so one half's latency-bound kernels (build, the per-window solve on one
   // block each) overlap the other half's whole-GPU kernels instead of leaving most CUs idle.
-  const int nh = nwin >= 8 ? (nwin + 1) / 2 : nwin;
+#ifndef FVO_BA_SPLIT
+#define FVO_BA_SPLIT 1
+#endif
+  const int nh = (FVO_BA_SPLIT && nwin >= 8) ? (nwin + 1) / 2 : nwin;
   const bool two = nh < nwin;
   if (two) {
     FVO_HIP(ctx, hipEventRecord(ctx->ba_fork, s));

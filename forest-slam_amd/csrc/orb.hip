@@ -149,8 +149,8 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
                                                   uint8_t* __restrict__ score, uint64_t* __restrict__ keep,
                                                   int32_t* __restrict__ rowcnt, uint8_t* __restrict__ trec,
                                                   int64_t total, int thr, int edge, int kw, int ntiles) {
-  __shared__ uint8_t s_img[kIH][kIW];
-  __shared__ uint8_t s_sc[kFH][kFW];
+  __shared__ __attribute__((aligned(16))) uint8_t s_img[kIH][kIW];
+  __shared__ __attribute__((aligned(16))) uint8_t s_sc[kFH][kFW];
   __shared__ uint16_t s_list[kFH * kFW];
   __shared__ uint16_t s_pre[kFH * kFW];
   __shared__ int s_n, s_npre;
@@ -164,12 +164,25 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   const int x0 = tx * kTW, y0 = ty * kTH;
   const int w = G.w[l], h = G.h[l];
   const uint8_t* im = pyr + b * total + G.off[l];
-  for (int i = threadIdx.x; i < kIH * kIW; i += 256) {
-    const int r = i / kIW, c = i % kIW;
-    const int y = min(max(y0 - 4 + r, 0), h - 1), x = min(max(x0 - 4 + c, 0), w - 1);
-    s_img[r][c] = im[(int64_t)y * w + x];
+  if (x0 >= 4 && x0 + kTW + 8 <= w && y0 >= 4 && y0 + kTH + 4 <= h) {
+    // interior tile: the staged rows and the aligned dwords around them lie inside the level
+    // row (4 px of slack on the right), so a row's 72 bytes come from 19 aligned dwords,
+    // byte-aligned by v_alignbyte
+    for (int i = threadIdx.x; i < kIH * (kIW / 4); i += 256) {
+      const int r = i / (kIW / 4), k = i % (kIW / 4);
+      const uint8_t* p = im + (int64_t)(y0 - 4 + r) * w + x0 - 4 + 4 * k;
+      const uint32_t* a = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
+      const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+      *reinterpret_cast<uint32_t*>(&s_img[r][4 * k]) = __builtin_amdgcn_alignbyte(a[1], a[0], sh);
+    }
+  } else {
+    for (int i = threadIdx.x; i < kIH * kIW; i += 256) {
+      const int r = i / kIW, c = i % kIW;
+      const int y = min(max(y0 - 4 + r, 0), h - 1), x = min(max(x0 - 4 + c, 0), w - 1);
+      s_img[r][c] = im[(int64_t)y * w + x];
+    }
   }
-  for (int i = threadIdx.x; i < kFH * kFW; i += 256) (&s_sc[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < kFH * kFW / 4; i += 256) reinterpret_cast<uint32_t*>(&s_sc[0][0])[i] = 0;
   if (threadIdx.x == 0) { s_n = 0; s_npre = 0; }
   __syncthreads();
   // FAST-9 on the tile + halo in two compacted stages.  (1) A 9-arc of the 16-circle always
