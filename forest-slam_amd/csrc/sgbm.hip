@@ -61,7 +61,8 @@ __device__ __forceinline__ uint32_t sgm_pair(uint32_t* st, int k, uint32_t& old_
   uint32_t hi = k < NPL - 1 ? st[k + 1] : hiN;
   u16x2 dm = as_v(__builtin_amdgcn_alignbit(cur, lo, 16));  // (prev[2k-1], prev[2k])
   u16x2 dp = as_v(__builtin_amdgcn_alignbit(hi, cur, 16));  // (prev[2k+1], prev[2k+2])
-  u16x2 m = vmin(vmin(dm + P1, dp + P1), vmin(as_v(cur), mp2));
+  // min(dm + P1, dp + P1) = min(dm, dp) + P1: no path value + P1 wraps (sgbm_init bounds them)
+  u16x2 m = vmin(vmin(dm, dp) + P1, vmin(as_v(cur), mp2));
   uint32_t nv = as_u(as_v(c) + m - mpv);
   old_km1 = cur;
   st[k] = nv;
@@ -470,7 +471,7 @@ __device__ __forceinline__ void derive16(const uint32_t* vp, const uint32_t* v, 
     const uint32_t hi = k < PQ - 1 ? vp[k + 1] : hiN;
     const u16x2 dm = as_v(__builtin_amdgcn_alignbit(cur, lo, 16));
     const u16x2 dp = as_v(__builtin_amdgcn_alignbit(hi, cur, 16));
-    const u16x2 mm = vmin(vmin(dm + P1, dp + P1), vmin(as_v(cur), mp2));
+    const u16x2 mm = vmin(vmin(dm, dp) + P1, vmin(as_v(cur), mp2));
     c[k] = as_u(as_v(v[k]) - mm + mpv);
   }
 }
@@ -485,6 +486,9 @@ __device__ __forceinline__ void derive16(const uint32_t* vp, const uint32_t* v, 
 // by an LDS atomicMin -- the serial rule "replace iff disp2cost > cost" of sgbm_ref.cpp (the
 // smallest cost wins, among equal costs the largest x1, the first one the scan visits).  The
 // pseudo left-right check then runs on the LDS row and writes the row-major raw disparity.
+#ifndef FVO_SG_EXP
+#define FVO_SG_EXP 0  // timing-only experiments: 1 = sweep 1 alone, 2 = sweep 2 alone
+#endif
 #ifndef FVO_SG_PD
 #define FVO_SG_PD 4
 #endif
@@ -574,59 +578,71 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
   const uint32_t voffM = pzero ? 0x80000000u : (uint32_t)(((int64_t)pgrp * W1 * 4 + psub) * 2);
   const u16x2 P1 = splat(p.P1);
   const int64_t ckbase = ((int64_t)b * gridDim.x + blk) * nck;
-  auto ld = [&](int x, uint32_t* out) { bload<PQ>(vrs, voffV, (uint32_t)x * (XS * 4), out); };
-  auto ldp = [&](int x, uint32_t* out) { bload<PQ>(vrs, voffP, (uint32_t)x * (XS * 4), out); };
+  // column offsets are wave-uniform (readfirstlane keeps them in SGPRs: a VGPR soffset would
+  // make the compiler wrap each load in a waterfall loop)
+  auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+  auto ld = [&](int x, uint32_t* out) { bload<PQ>(vrs, voffV, uni((uint32_t)x * (XS * 4)), out); };
+  auto ldp = [&](int x, uint32_t* out) { bload<PQ>(vrs, voffP, uni((uint32_t)x * (XS * 4)), out); };
   auto ldm = [&](int x) -> uint32_t {
-    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(mrs, voffM, (uint32_t)x * 8, 0);
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(mrs, voffM, uni((uint32_t)x * 8), 0);
   };
 
-  // ---- sweep 1: left -> right, checkpoints.  Loads are unconditional (clamped columns) so
-  // the compiler's vmcnt waits stay precise; the checkpoint of each 8-column block is picked
-  // by a register select and stored once per block (slot nck-1 is a dummy for blocks that
-  // hold none).
+  // ---- sweep 1: left -> right, checkpoints, in blocks of SEG columns that end at the
+  // checkpoint columns x = W1-1-SEG*m, so every block is full and its checkpoint is its last
+  // state (stored once per block; slot nck-1 is a dummy for the last block, which holds none).
+  // The first block starts at xs <= 0: its columns left of 0 step with C = 0, which keeps the
+  // zero start state exactly (C + min(0, P1, P2) - 0 = 0).  Loads are unconditional (clamped
+  // columns) so the compiler's vmcnt waits stay precise, and the block body has no branches,
+  // so the scheduler overlaps one column's serial min-reduction with the next column's work.
   // V and the previous row PD columns ahead (a ring of PD column buffers)
-  uint32_t st[PQ], vb[PD][PQ], pb[PD][PQ], mb[PD], ck[PF / SEG][PQ + 1];
+  static_assert(PF == SEG && SEG % PD == 0, "ring slots line up across blocks");
+  uint32_t st[PQ], vb[PD][PQ], pb[PD][PQ], mb[PD];
   uint32_t minPrev = 0;
+  const int xs = ((W1 - 1) & (SEG - 1)) - (SEG - 1);
 #pragma unroll
   for (int k = 0; k < PQ; ++k) st[k] = 0;
 #pragma unroll
   for (int j = 0; j < PD; ++j) {
-    ld(min(j, W1 - 1), vb[j]);
-    ldp(min(j, W1 - 1), pb[j]);
-    mb[j] = ldm(min(j, W1 - 1));
+    const int xx = min(max(xs + j, 0), W1 - 1);
+    ld(xx, vb[j]);
+    ldp(xx, pb[j]);
+    mb[j] = ldm(xx);
   }
-  static_assert(PF % SEG == 0, "whole checkpoints per prefetch block");
-  const int jck = (W1 - 1 - SEG) & (SEG - 1);  // checkpoint columns of a block: jck + SEG*m
-#pragma unroll 1
-  for (int x0 = 0; x0 < W1; x0 += PF) {
-    const bool full = x0 + PF <= W1;
+  auto block1 = [&](int x0, auto first_t) {
+    constexpr bool FIRST = decltype(first_t)::value;
 #pragma unroll
-    for (int j = 0; j < PF; ++j) {
+    for (int j = 0; j < SEG; ++j) {
       const int x = x0 + j;
       uint32_t c[PQ];
       derive16<PQ>(pb[j % PD], vb[j % PD], c, mb[j % PD], P1, p.P2);
-      ld(min(x + PD, W1 - 1), vb[j % PD]);
-      ldp(min(x + PD, W1 - 1), pb[j % PD]);
-      mb[j % PD] = ldm(min(x + PD, W1 - 1));
-      if (full || x < W1) minPrev = step16<PQ>(st, c, q, P1, minPrev, p.P2);
-      const bool here = (j & (SEG - 1)) == jck;
-      uint32_t* ckm = ck[j / SEG];
+      if (FIRST) {
 #pragma unroll
-      for (int k = 0; k < PQ; ++k) ckm[k] = here ? st[k] : ckm[k];
-      ckm[PQ] = here ? minPrev : ckm[PQ];
+        for (int k = 0; k < PQ; ++k) c[k] = x < 0 ? 0u : c[k];
+      }
+      const int xn = FIRST ? min(max(x + PD, 0), W1 - 1) : min(x + PD, W1 - 1);
+      ld(xn, vb[j % PD]);
+      ldp(xn, pb[j % PD]);
+      mb[j % PD] = ldm(xn);
+      minPrev = step16<PQ>(st, c, q, P1, minPrev, p.P2);
     }
+    const int rem = W1 - 1 - SEG - (x0 + SEG - 1);
+    const int slot = rem >= 0 ? rem / SEG : nck - 1;
+    uint32_t* cp = ckpt + ((ckbase + slot) * 64 + lane) * CKW;
+    uint32_t v[CKW];
 #pragma unroll
-    for (int m = 0; m < PF / SEG; ++m) {
-      const int xc = x0 + SEG * m + jck, rem = W1 - 1 - SEG - xc;
-      const int slot = rem >= 0 && xc < W1 ? rem / SEG : nck - 1;
-      uint32_t* cp = ckpt + ((ckbase + slot) * 64 + lane) * CKW;
-      uint32_t v[CKW];
+    for (int kk = 0; kk < CKW; ++kk) v[kk] = kk < PQ ? st[kk] : kk == PQ ? minPrev : 0u;
 #pragma unroll
-      for (int kk = 0; kk < CKW; ++kk) v[kk] = kk <= PQ ? ck[m][kk] : 0u;
-#pragma unroll
-      for (int kk = 0; kk < CKW; kk += 4) *reinterpret_cast<uint4*>(cp + kk) = make_uint4(v[kk], v[kk + 1], v[kk + 2], v[kk + 3]);
-    }
-  }
+    for (int kk = 0; kk < CKW; kk += 4) *reinterpret_cast<uint4*>(cp + kk) = make_uint4(v[kk], v[kk + 1], v[kk + 2], v[kk + 3]);
+  };
+#if FVO_SG_EXP != 2
+  block1(xs, std::true_type{});
+#pragma unroll 1
+  for (int x0 = xs + SEG; x0 < W1; x0 += SEG) block1(x0, std::false_type{});
+#endif
+#if FVO_SG_EXP == 1
+  if (minPrev == 0x12345678u) raw[0] = 1;
+  return;
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the checkpoints, re-read below by the lanes that stored them
 
   // ---- sweep 2: segments s of reflected columns x' = SEG*s + i (x1 = W1-1-x'), right to left
@@ -901,6 +917,11 @@ int sgbm_init(fvo_ctx* ctx) {
   if (c.sgbm_stripes < 1) return fvo_fail(ctx, "SGBM: stripes must be >= 1");
   SgParams p = make_params(c);
   if (p.width1 <= 0) return fvo_fail(ctx, "SGBM: image narrower than numDisparities");
+  // path values are at most C + P2 with C <= 49 x the largest BT pixel cost (2 ftzero + 255/4);
+  // the kernels add P1 to them in u16 (min(a, b) + P1 for min(a + P1, b + P1)), so that sum
+  // must not wrap -- OpenCV's 16-bit CostType carries the same assumption
+  if (49 * (2 * p.ftzero + 63) + p.P2 + p.P1 > 0xFFFF)
+    return fvo_fail(ctx, "SGBM: P1/P2/preFilterCap too large for 16-bit path costs");
   const int64_t B = c.sgbm_max_batch > 0 ? std::min(c.sgbm_max_batch, c.max_batch) : c.max_batch;
   const int64_t plane = (int64_t)p.width1 * p.D;
   int rc;
