@@ -605,8 +605,14 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
   d4 acc[kLinMaxTiles][2];
 #pragma unroll
   for (int lt = 0; lt < kLinMaxTiles; ++lt) acc[lt][0] = acc[lt][1] = d4{0.0, 0.0, 0.0, 0.0};
+  // s_act[g]: bit I set when rows 4g .. 4g+3 of the chunk's Yt hold a non-zero entry in the
+  // columns of tile I (a landmark's rows are non-zero only in the pose columns of the frames
+  // observing it, a few of the window's K-1 frames); a 4-row MFMA step of tile (I, J) whose rows
+  // are zero in tile I's or J's columns adds exactly zero and is skipped
+  __shared__ uint32_t s_act[64];
   for (int c = part; c * LPC < L; c += dm.NPART) {
     for (int i = threadIdx.x; i < rows * NRP; i += kLinBlock) sY[i] = 0.0;
+    if (threadIdx.x < 64) s_act[threadIdx.x] = 0u;
     __syncthreads();
     // the chunk's observations are contiguous (landmark-major): [ob0, ob1)
     const int lc0 = c * LPC, lc1 = min(L, lc0 + LPC);
@@ -659,6 +665,11 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
       const int f = o.frame;
       if (f == 0) continue;
       const int tl = o.lm - lc0;
+      {
+        const uint32_t bits = (1u << (6 * (f - 1) / 16)) | (1u << ((6 * (f - 1) + 5) / 16));
+        atomicOr(&s_act[3 * tl / 4], bits);
+        if ((3 * tl + 2) / 4 != 3 * tl / 4) atomicOr(&s_act[(3 * tl + 2) / 4], bits);
+      }
       const double* sl = sLf + 6 * tl;
       const double l00 = sl[0], l10 = sl[1], l11 = sl[2], l20 = sl[3], l21 = sl[4], l22 = sl[5];
       const double* Wo = v.W + (int64_t)(ob0 + i) * 18;
@@ -674,7 +685,10 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
       }
     }
     __syncthreads();
-    // G += Yt^T Yt on MFMA: A[i][k] = Yt[k][16I + i], B[k][j] = Yt[k][16J + j], lane holds k = lane >> 4
+    // G += Yt^T Yt on MFMA: A[i][k] = Yt[k][16I + i], B[k][j] = Yt[k][16J + j], lane holds k = lane >> 4;
+    // the active 4-row steps of the tile (every row's z column is live: J = NT-1 always
+    // counts), ascending, alternately into two accumulators by step parity (fixed order)
+    const uint32_t actl = lane < rows / 4 ? s_act[lane] : 0u;
 #pragma unroll
     for (int lt = 0; lt < kLinMaxTiles; ++lt) {
       const int k = kLinWaves * lt + wid;
@@ -683,9 +697,13 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
         lin_tile(k, ntu, NT, I, J);
         const double* ya = sY + (lane >> 4) * NRP + 16 * I + (lane & 15);
         const double* yb = sY + (lane >> 4) * NRP + 16 * J + (lane & 15);
-        for (int k0 = 0; k0 < rows; k0 += 8) {
-          acc[lt][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[k0 * NRP], yb[k0 * NRP], acc[lt][0], 0, 0, 0);
-          acc[lt][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[(k0 + 4) * NRP], yb[(k0 + 4) * NRP], acc[lt][1], 0, 0, 0);
+        uint64_t m = __ballot(((actl >> I) & 1u) && (((actl >> J) & 1u) || J == NT - 1));
+        while (m) {
+          const int g = __builtin_ctzll(m);
+          m &= m - 1;
+          const double a = ya[4 * g * NRP], bv = yb[4 * g * NRP];
+          if (g & 1) acc[lt][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc[lt][1], 0, 0, 0);
+          else acc[lt][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc[lt][0], 0, 0, 0);
         }
       }
     }
@@ -718,6 +736,7 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
   const int nch0 = (L + dm.LPC - 1) / dm.LPC, nch = nch0 < dm.NPART ? nch0 : dm.NPART;  // partials used
   const double lam = S->lam;
   double* rhs = sS + np * np;
+  double* rinv = rhs + np;  // reciprocal pivots of the factor
   // S = H_pp + lam diag + 1e-6 I - sum_c G_c (upper triangle, mirrored).  A thread takes 4
   // consecutive columns b0..b0+3 of a row a (b0 from the row's diagonal 16 x 16 tile, which
   // k_ba_lin writes in full) and loads the 4-wide slices of every partial before summing, so
@@ -776,7 +795,9 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
   bool fail = false;
   for (int k = 0; k < np; k += kChol) {
     const int pw = min(kChol, np - k);
-    double Lb[kChol][kChol];
+    // pivots as reciprocals (one division per column; the entries below it are products), so
+    // the panel's dependent chain holds one sqrt and one division per column
+    double Lb[kChol][kChol], rp[kChol];
 #pragma unroll
     for (int a2 = 0; a2 < kChol; ++a2) {
       if (a2 < pw) {
@@ -786,6 +807,7 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
           if (c < a2) d -= Lb[a2][c] * Lb[a2][c];
         if (!(d > 0.0)) fail = true;
         Lb[a2][a2] = sqrt(d);
+        rp[a2] = 1.0 / Lb[a2][a2];
 #pragma unroll
         for (int b2 = 0; b2 < kChol; ++b2) {
           if (b2 > a2 && b2 < pw) {
@@ -793,7 +815,7 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
 #pragma unroll
             for (int c = 0; c < kChol; ++c)
               if (c < a2) v2 -= Lb[b2][c] * Lb[a2][c];
-            Lb[b2][a2] = v2 / Lb[a2][a2];
+            Lb[b2][a2] = v2 * rp[a2];
           }
         }
       }
@@ -808,7 +830,7 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
 #pragma unroll
           for (int c = 0; c < kChol; ++c)
             if (c < a2) v2 -= x[c] * Lb[a2][c];
-          x[a2] = v2 / Lb[a2][a2];
+          x[a2] = v2 * rp[a2];
           sS[i * np + k + a2] = x[a2];
         }
       }
@@ -826,12 +848,15 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
         sS[i * np + j] = v2;
       }
     }
-    if (tid == 0)  // the diagonal block's factor (no thread reads these rows in this phase)
+    if (tid == 0) {  // the diagonal block's factor (no thread reads these rows in this phase)
 #pragma unroll
-      for (int a2 = 0; a2 < kChol; ++a2)
+      for (int a2 = 0; a2 < kChol; ++a2) {
 #pragma unroll
         for (int b2 = 0; b2 < kChol; ++b2)
           if (a2 < pw && b2 >= a2 && b2 < pw) sS[(k + b2) * np + k + a2] = Lb[b2][a2];
+        if (a2 < pw) rinv[k + a2] = rp[a2];
+      }
+    }
     __syncthreads();
   }
   if (fail) {
@@ -852,14 +877,14 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
     const int r0 = lane, r1 = lane + 64;
     double x0 = r0 < np ? rhs[r0] : 0.0, x1 = r1 < np ? rhs[r1] : 0.0;
     for (int j = 0; j < np; ++j) {
-      const double yj = bcast(j < 64 ? x0 : x1, j & 63) / sS[j * np + j];
+      const double yj = bcast(j < 64 ? x0 : x1, j & 63) * rinv[j];
       if (r0 == j) x0 = yj;
       if (r1 == j) x1 = yj;
       if (r0 > j && r0 < np) x0 -= sS[r0 * np + j] * yj;
       if (r1 > j && r1 < np) x1 -= sS[r1 * np + j] * yj;
     }
     for (int j = np - 1; j >= 0; --j) {
-      const double xj = bcast(j < 64 ? x0 : x1, j & 63) / sS[j * np + j];
+      const double xj = bcast(j < 64 ? x0 : x1, j & 63) * rinv[j];
       if (r0 == j) x0 = xj;
       if (r1 == j) x1 = xj;
       if (r0 < j) x0 -= sS[j * np + r0] * xj;

@@ -63,7 +63,6 @@ struct fvo_ctx {
   uint8_t* blur = nullptr;    // [B][total_px] debug only (orb_blur_debug), allocated on first use
   int orb_last_batch = 0;     // images of the last ORB call
   uint8_t* score = nullptr;   // [B][total_px]
-  int32_t* rowcnt = nullptr;  // [B][total_rows]
   int32_t* rowoff = nullptr;  // [B][total_rows]
   uint32_t* cand = nullptr;   // [B][cand_total] packed (score<<24 | y<<12 | x)
   uint64_t* hel = nullptr;    // [B][cand_total] (harris float bits << 32 | packed)
@@ -94,9 +93,7 @@ struct fvo_ctx {
   int32_t* pnp_good = nullptr;    // [B][max_iters] inlier counts
   void* pnp_state = nullptr;      // [B] PnpState
   int32_t pnp_max_iters = 0;
-  uint64_t* keepbits = nullptr;   // [B][total_rows][keep_words] FAST+NMS keep bits
-  uint8_t* fast_rec = nullptr;    // [B][tiles][2*32 + 1024] per FAST tile: row keep prefixes + kept scores
-  int keep_words = 0;
+  uint8_t* fast_rec = nullptr;    // [B][tiles][kTRec] per FAST tile: row keep words + prefixes + kept scores
   // local BA workspace (per window w < max_batch; strides in ba_* counts)
   void* ba_ws = nullptr;          // one allocation, carved per window (ba.hip)
   int64_t ba_win_bytes = 0;

@@ -126,12 +126,14 @@ __constant__ int c_cdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2
 // an LDS list so cornerScore<16> runs on dense lanes (textured frames make ~80 % of waves
 // contain a corner, so per-pixel scoring ran the score code on nearly every wave); then the
 // strict 3x3 NMS + border filter of the tile is evaluated from the LDS score tile.  Output:
-// one keep bit per pixel (a 64-bit word per tile row), per-row keep counts, and the scores of
-// the kept pixels only -- per tile a record of the rows' keep prefixes (32 u16) followed by
-// the kept scores in row-major order -- so no full-level score map crosses HBM (the score map
-// itself is produced only on request, by the SCOREMAP instance, for the debug hook).
+// per tile one record, written as contiguous runs: the rows' keep bits (a 64-bit word per tile
+// row), the rows' keep prefixes (32 u16) and the kept pixels' scores in row-major order -- no
+// full-level score map and no scattered per-row keep words or counters cross HBM (the row
+// counts are popcounts of the records' words, taken by k_row_scan; the score map itself is
+// produced only on request, by the SCOREMAP instance, for the debug hook).
 constexpr int kTW = 64, kTH = 32;
-constexpr int kTRec = 2 * kTH + kTH * kTW / 2;  // tile record: u16 row prefixes + <= 1024 kept scores
+constexpr int kRecKeep = 0, kRecPre = 8 * kTH, kRecSc = kRecPre + 2 * kTH;  // byte offsets in a record
+constexpr int kTRec = kRecSc + kTH * kTW / 2;  // + <= 1024 kept scores
 
 constexpr int kFW = kTW + 2, kFH = kTH + 2;     // FAST region (NMS halo)
 constexpr int kIW = kTW + 8, kIH = kTH + 8;     // image patch (FAST radius 3 + halo)
@@ -146,9 +148,8 @@ __device__ __forceinline__ int tile_level(const OrbDev& G, int t) {
 
 template <bool SCOREMAP>
 __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t* __restrict__ pyr,
-                                                  uint8_t* __restrict__ score, uint64_t* __restrict__ keep,
-                                                  int32_t* __restrict__ rowcnt, uint8_t* __restrict__ trec,
-                                                  int64_t total, int thr, int edge, int kw, int ntiles) {
+                                                  uint8_t* __restrict__ score, uint8_t* __restrict__ trec,
+                                                  int64_t total, int thr, int edge, int ntiles) {
   __shared__ __attribute__((aligned(16))) uint8_t s_img[kIH][kIW];
   __shared__ __attribute__((aligned(16))) uint8_t s_sc[kFH][kFW];
   __shared__ uint16_t s_list[kFH * kFW];
@@ -293,14 +294,7 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
       continue;
     }
     const unsigned long long m = __ballot(k);
-    if (c == 0) {
-      s_m[rr] = m;
-      if (y < h) {
-        const int grow = G.row0[l] + y;
-        keep[((int64_t)b * G.total_rows + grow) * kw + tx] = m;
-        if (m) atomicAdd(&rowcnt[(int64_t)b * G.total_rows + grow], __popcll(m));
-      }
-    }
+    if (c == 0) s_m[rr] = m;  // rows past the level's end keep nothing
   }
   if (SCOREMAP) return;
   __syncthreads();
@@ -317,27 +311,30 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   }
   __syncthreads();
   uint8_t* rec = trec + ((int64_t)b * ntiles + t) * kTRec;
-  if (threadIdx.x < kTH) reinterpret_cast<uint16_t*>(rec)[threadIdx.x] = (uint16_t)s_rp[threadIdx.x];
+  if (threadIdx.x < kTH) reinterpret_cast<unsigned long long*>(rec + kRecKeep)[threadIdx.x] = s_m[threadIdx.x];
+  else if (threadIdx.x < 2 * kTH)
+    reinterpret_cast<uint16_t*>(rec + kRecPre)[threadIdx.x - kTH] = (uint16_t)s_rp[threadIdx.x - kTH];
   for (int rr = threadIdx.x >> 6; rr < kTH; rr += 4) {
     const unsigned long long m = s_m[rr];
-    if ((m >> c) & 1ull) rec[2 * kTH + s_rp[rr] + __popcll(m & ((1ull << c) - 1ull))] = s_sc[rr + 1][c + 1];
+    if ((m >> c) & 1ull) rec[kRecSc + s_rp[rr] + __popcll(m & ((1ull << c) - 1ull))] = s_sc[rr + 1][c + 1];
   }
 }
 
 // ordered (row-major) compaction of the kept pixels: one wave per row; the scores come from
 // the tile records k_fast_nms wrote
 __global__ __launch_bounds__(64) void k_keep_compact(const OrbDev G, const uint8_t* __restrict__ trec,
-                                                     const uint64_t* __restrict__ keep,
                                                      const int32_t* __restrict__ rowoff, uint32_t* __restrict__ cand,
-                                                     int64_t cand_total, int edge, int kw, int ntiles) {
+                                                     int64_t cand_total, int edge, int ntiles) {
   const int r = blockIdx.x, b = blockIdx.y;
   const int l = level_of_row(G, r);
   const int y = r - G.row0[l];
   const int h = G.h[l];
   if (y < edge || y >= h - edge) return;
   const int lane = threadIdx.x, ntx = G.ntx[l];
-  const uint64_t* kr = keep + ((int64_t)b * G.total_rows + r) * kw;
-  const unsigned long long word = lane < ntx ? kr[lane] : 0ull;
+  // this row's records: tile (y / kTH, lane) of the level; the row's keep word and prefix in it
+  const uint8_t* myrec = trec + ((int64_t)b * ntiles + G.tile0[l] + (y / kTH) * ntx + min(lane, ntx - 1)) * kTRec;
+  const unsigned long long word =
+      lane < ntx ? reinterpret_cast<const unsigned long long*>(myrec + kRecKeep)[y % kTH] : 0ull;
   const int cnt = __popcll(word);
   int inc = cnt;
 #pragma unroll
@@ -346,9 +343,7 @@ __global__ __launch_bounds__(64) void k_keep_compact(const OrbDev G, const uint8
     if (lane >= o) inc += v;
   }
   const int pre_lane = inc - cnt;
-  // this row's records: tile (y / kTH, lane) of the level; the row's prefix inside it
-  const uint8_t* myrec = trec + ((int64_t)b * ntiles + G.tile0[l] + (y / kTH) * ntx + min(lane, ntx - 1)) * kTRec;
-  const int rpre = word ? reinterpret_cast<const uint16_t*>(myrec)[y % kTH] : 0;
+  const int rpre = word ? reinterpret_cast<const uint16_t*>(myrec + kRecPre)[y % kTH] : 0;
   const int base = rowoff[(int64_t)b * G.total_rows + r];
   uint32_t* out = cand + b * cand_total + G.cand_off[l];
   for (int j = 0; j < ntx; ++j) {
@@ -360,16 +355,25 @@ __global__ __launch_bounds__(64) void k_keep_compact(const OrbDev G, const uint8
       const int x = 64 * j + lane;
       const int rank = __popcll(wj & ((1ull << lane) - 1ull));
       const uint8_t* rec = trec + ((int64_t)b * ntiles + G.tile0[l] + (y / kTH) * ntx + j) * kTRec;
-      out[base + pj + rank] = ((uint32_t)rec[2 * kTH + rj + rank] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+      out[base + pj + rank] = ((uint32_t)rec[kRecSc + rj + rank] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
     }
   }
 }
 
-__global__ void k_row_scan(const OrbDev G, const int32_t* __restrict__ rowcnt, int32_t* __restrict__ rowoff,
-                           int32_t* __restrict__ ncand, int total_rows, int nlevels) {
+// per level: each row's keep count (popcounts of its keep words in the level's tile records),
+// exclusive scan -> row offsets, total -> ncand
+__global__ void k_row_scan(const OrbDev G, const uint8_t* __restrict__ trec, int32_t* __restrict__ rowoff,
+                           int32_t* __restrict__ ncand, int total_rows, int nlevels, int ntiles) {
   int l = blockIdx.x, b = blockIdx.y;
   int r0 = G.row0[l], h = G.h[l];
-  const int32_t* rc = rowcnt + (int64_t)b * total_rows + r0;
+  const int ntx = G.ntx[l];
+  const uint8_t* lrec = trec + ((int64_t)b * ntiles + G.tile0[l]) * kTRec;
+  auto rc = [&](int y) {
+    const uint8_t* rr = lrec + (int64_t)(y / kTH) * ntx * kTRec + kRecKeep + 8 * (y % kTH);
+    int n = 0;
+    for (int j = 0; j < ntx; ++j) n += __popcll(*reinterpret_cast<const unsigned long long*>(rr + (int64_t)j * kTRec));
+    return n;
+  };
   int32_t* ro = rowoff + (int64_t)b * total_rows + r0;
   __shared__ int s_w[16];
   __shared__ int s_carry;
@@ -377,7 +381,7 @@ __global__ void k_row_scan(const OrbDev G, const int32_t* __restrict__ rowcnt, i
   __syncthreads();
   for (int base = 0; base < h; base += blockDim.x) {
     int i = base + threadIdx.x;
-    int v = i < h ? rc[i] : 0;
+    int v = i < h ? rc(i) : 0;
     int inc = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1054,16 +1058,14 @@ int orb_init(fvo_ctx* ctx) {
   for (int l = 0; l < c.nlevels; ++l) maxcand = std::max<int64_t>(maxcand, g.cand_off[l + 1] - g.cand_off[l]);
   ctx->scratch_per = 2 * maxcand;
   // (the full FAST score map, ctx->score, is allocated on first debug request)
-  if ((rc = fvo_alloc(ctx, &ctx->pyr, B * g.total_px)) || (rc = fvo_alloc(ctx, &ctx->rowcnt, B * g.total_rows)) ||
+  if ((rc = fvo_alloc(ctx, &ctx->pyr, B * g.total_px)) ||
       (rc = fvo_alloc(ctx, &ctx->rowoff, B * g.total_rows)) || (rc = fvo_alloc(ctx, &ctx->cand, B * g.cand_total)) ||
       (rc = fvo_alloc(ctx, &ctx->hel, B * g.cand_total)) || (rc = fvo_alloc(ctx, &ctx->ncand, B * c.nlevels)) ||
       (rc = fvo_alloc(ctx, &ctx->nsel1, B * c.nlevels)) || (rc = fvo_alloc(ctx, &ctx->nsel2, B * c.nlevels)) ||
       (rc = fvo_alloc(ctx, &ctx->koff, B * (c.nlevels + 1))) ||
       (rc = fvo_alloc(ctx, &ctx->scratch, B * c.nlevels * ctx->scratch_per)))
     return rc;
-  ctx->keep_words = (g.w[0] + kTW - 1) / kTW;
-  if (ctx->keep_words > 64) return fvo_fail(ctx, "ORB: image wider than 4096 px");
-  if ((rc = fvo_alloc(ctx, &ctx->keepbits, B * g.total_rows * ctx->keep_words))) return rc;
+  if ((g.w[0] + kTW - 1) / kTW > 64) return fvo_fail(ctx, "ORB: image wider than 4096 px");  // k_keep_compact: a lane per tile
   if ((rc = fvo_alloc(ctx, &ctx->fast_rec, B * make_dev(g).tile0[g.nlevels] * kTRec))) return rc;
   return 0;
 }
@@ -1125,15 +1127,12 @@ int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride
     FVO_TIMED(ctx, KN_ORB_RESIZE, s, hipLaunchKernelGGL(k_resize, dim3((g.w[l] + 255) / 256, (g.h[l] + kResRows - 1) / kResRows, batch), dim3(256), 0, s, G, ctx->pyr, total, l,
                        ctx->rt.xofs + ctx->rt.xoff[l], ctx->rt.xc1 + ctx->rt.xoff[l], ctx->rt.yofs + ctx->rt.yoff[l],
                        ctx->rt.yc1 + ctx->rt.yoff[l]));
-  FVO_HIP(ctx, hipMemsetAsync(ctx->rowcnt, 0, sizeof(int32_t) * (size_t)batch * g.total_rows, s));
   FVO_TIMED(ctx, KN_ORB_FAST, s, hipLaunchKernelGGL(k_fast_nms<false>, dim3(ntiles, batch), dim3(256), 0, s, G, ctx->pyr,
-                     nullptr, ctx->keepbits, ctx->rowcnt, ctx->fast_rec, total, thr, c.edge_threshold,
-                     ctx->keep_words, ntiles));
-  FVO_TIMED(ctx, KN_ORB_ROW_SCAN, s, hipLaunchKernelGGL(k_row_scan, dim3(L, batch), dim3(256), 0, s, G, ctx->rowcnt, ctx->rowoff, ctx->ncand, g.total_rows,
-                     L));
+                     nullptr, ctx->fast_rec, total, thr, c.edge_threshold, ntiles));
+  FVO_TIMED(ctx, KN_ORB_ROW_SCAN, s, hipLaunchKernelGGL(k_row_scan, dim3(L, batch), dim3(256), 0, s, G, ctx->fast_rec, ctx->rowoff, ctx->ncand, g.total_rows,
+                     L, ntiles));
   FVO_TIMED(ctx, KN_ORB_COMPACT, s, hipLaunchKernelGGL(k_keep_compact, dim3(g.total_rows, batch), dim3(64), 0, s, G, ctx->fast_rec,
-                     ctx->keepbits, ctx->rowoff, ctx->cand, g.cand_total, c.edge_threshold, ctx->keep_words,
-                     ntiles));
+                     ctx->rowoff, ctx->cand, g.cand_total, c.edge_threshold, ntiles));
   FVO_TIMED(ctx, KN_ORB_SELECT1, s, hipLaunchKernelGGL(k_select<ElemFast>, dim3(L, batch), dim3(kSelThreads), 0, s, G, ctx->cand, ctx->ncand, ctx->nsel1,
                      ctx->scratch, ctx->scratch_per, g.cand_total, L, 2));
   FVO_TIMED(ctx, KN_ORB_HARRIS, s, hipLaunchKernelGGL(k_harris, dim3(32, L, batch), dim3(256), 0, s, G, ctx->pyr, ctx->cand, ctx->nsel1, ctx->hel, total,
@@ -1181,8 +1180,7 @@ int orb_score_debug(fvo_ctx* ctx) {
     const OrbDev G = make_dev(g);
     const int ntiles = G.tile0[g.nlevels];
     hipLaunchKernelGGL(k_fast_nms<true>, dim3(ntiles, ctx->orb_last_batch), dim3(256), 0, 0, G, ctx->pyr, ctx->score,
-                       nullptr, nullptr, nullptr, g.total_px, ctx->cfg.fast_threshold, ctx->cfg.edge_threshold,
-                       ctx->keep_words, ntiles);
+                       nullptr, g.total_px, ctx->cfg.fast_threshold, ctx->cfg.edge_threshold, ntiles);
     FVO_LAUNCH_CHECK(ctx);
   }
   FVO_HIP(ctx, hipDeviceSynchronize());
