@@ -28,6 +28,7 @@
 // poses moved by 1.3e-4 against the fp64 oracle (measured), outside north_star's 1e-4.
 // All reductions have a fixed order, so results are run-to-run deterministic.
 #include <cfloat>
+#include <type_traits>
 
 #include "fvo_internal.h"
 
@@ -45,16 +46,24 @@ struct BaCam {
 
 constexpr int kKMax = 21;
 constexpr int kBlock = 256;
-// k_ba_lin: blocks per window; block p reduces the landmark chunks p, p + kLinParts, ... into
-// one partial Schur product (MFMA accumulators kept across its chunks), so k_ba_solve sums
-// kLinParts partials instead of one per chunk.  Fixed chunk order: deterministic.
+// k_ba_lin: blocks per window NPART = (chunk capacity) / kLinChunksPerPart, clamped to [1,
+// kLinParts] (FVO_BA_PARTS overrides); block p reduces the landmark chunks p, p + NPART, ...
+// into one partial Schur product (MFMA accumulators kept across its chunks), so k_ba_solve
+// sums NPART partials instead of one per chunk.  Fixed chunk order: deterministic.  The
+// count matters in the overlapped pipeline: each k_ba_lin block holds a whole CU (its LDS
+// slice), so more, shorter blocks evict the concurrent front stage from more CUs per LM
+// iteration, fewer leave the BA latency-bound.  Measured (bench.py, overlapped): 600p / 64
+// windows / 64 chunks: 16 parts 4770 frames/s, 8: 4787, 4: 4848, 2: 4556, 1: 4054; 1080p /
+// 32 windows / 256 chunks: 16 parts 1219, 8: 1120, 4: 1125.
 #ifndef FVO_BA_PARTS
-#define FVO_BA_PARTS 16
+#define FVO_BA_PARTS 0
 #endif
 #ifndef FVO_BA_LPC64
 #define FVO_BA_LPC64 64
 #endif
-constexpr int kLinParts = FVO_BA_PARTS;
+constexpr int kLinParts = 16, kLinChunksPerPart = 16;
+// k_ba_lin runs a group of kLinBlock / LPC lanes per landmark inside one wave: LPC >= 16
+static_assert(FVO_BA_LPC64 >= 32 && FVO_BA_LPC64 <= 64, "LPC64 in [32, 64]");
 // k_ba_lin runs 16 waves per block: its LDS slice (up to 150 KB) allows one block per CU, so
 // the block's own waves are all the latency hiding the CU gets
 constexpr int kLinWaves = 16, kLinBlock = 64 * kLinWaves;
@@ -218,13 +227,20 @@ __device__ __forceinline__ void exp_so3(const double* w, double* R) {
   for (int i = 0; i < 9; ++i) R[i] = ((i % 4 == 0) ? 1.0 : 0.0) + s * K[i] + c1 * K2[i];
 }
 
+// 1 / sqrt(d): the hardware estimate refined by one Newton step (relative error ~1e-15)
+__device__ __forceinline__ double rsq_r(double d) {
+  const double r = __builtin_amdgcn_rsq(d);
+  return r * fma(-0.5 * d * r, r, 1.5);
+}
+
 // observation weight 1 / sigma2[octave]; 0 once the observation was rejected (oct = -1)
 __device__ __forceinline__ double obs_is2(const BaIn& in, const BaObs& o) {
   return o.oct < 0 ? 0.0 : in.isig2[o.oct];
 }
 
-// residual, robust weight (x information) and cost of one observation; Jacobians if J
-template <bool J>
+// residual, robust weight (x information) and cost of one observation; Jacobians if J (the
+// pose Jacobian Jp only if JP)
+template <bool J, bool JP = true>
 __device__ __forceinline__ void ba_eval(const double* T, const double* X, const BaObs& o, const BaCam& c,
                                         double is2, double* r, double& w, double& rho, double (*Jp)[6],
                                         double (*Jl)[3]) {
@@ -249,7 +265,8 @@ __device__ __forceinline__ void ba_eval(const double* T, const double* X, const 
   // d(Xc)/d(w, v) = [-[Xc]x | I]
   const double sk[3][6] = {{0.0, z, -y, 1.0, 0.0, 0.0}, {-z, 0.0, x, 0.0, 1.0, 0.0}, {y, -x, 0.0, 0.0, 0.0, 1.0}};
   for (int k = 0; k < 3; ++k) {
-    for (int j = 0; j < 6; ++j) Jp[k][j] = Jc[k][0] * sk[0][j] + Jc[k][1] * sk[1][j] + Jc[k][2] * sk[2][j];
+    if (JP)
+      for (int j = 0; j < 6; ++j) Jp[k][j] = Jc[k][0] * sk[0][j] + Jc[k][1] * sk[1][j] + Jc[k][2] * sk[2][j];
     for (int j = 0; j < 3; ++j) Jl[k][j] = Jc[k][0] * T[j] + Jc[k][1] * T[3 + j] + Jc[k][2] * T[6 + j];
   }
 }
@@ -584,13 +601,11 @@ __device__ __forceinline__ void lin_tile(int k, int ntu, int NT, int& I, int& J)
 }
 
 __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm, BaCam cam) {
-  extern __shared__ double sY[];  // [3 LPC][NR + 2], then per-observation terms, then L factors
+  extern __shared__ double sY[];  // [3 LPC][NR + 2]
   const BaWin v = view(ws, dm, blockIdx.x);
   const BaState* S = v.st;
   if (!S->active) return;
   const int L = S->L, part = blockIdx.y, LPC = dm.LPC;
-  double* sHg = sY + 3 * LPC * (dm.NR + 2);  // [LPC * K][9]
-  double* sLf = sHg + 9 * LPC * dm.K;        // [LPC][6]
   if (part * LPC >= L) return;  // no chunk for this partial (k_ba_solve sums only the used ones)
   const int n = S->n;
   const int np = 6 * (n - 1);
@@ -602,92 +617,86 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
   int ntiles = 0;
   for (int i = 0; i < ntu; ++i) ntiles += (ntu - i) + (ntu < NT ? 1 : 0);
   typedef double d4 __attribute__((ext_vector_type(4)));
-  d4 acc[kLinMaxTiles][2];
+  d4 acc[kLinMaxTiles];
 #pragma unroll
-  for (int lt = 0; lt < kLinMaxTiles; ++lt) acc[lt][0] = acc[lt][1] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int lt = 0; lt < kLinMaxTiles; ++lt) acc[lt] = d4{0.0, 0.0, 0.0, 0.0};
   // s_act[g]: bit I set when rows 4g .. 4g+3 of the chunk's Yt hold a non-zero entry in the
   // columns of tile I (a landmark's rows are non-zero only in the pose columns of the frames
   // observing it, a few of the window's K-1 frames); a 4-row MFMA step of tile (I, J) whose rows
   // are zero in tile I's or J's columns adds exactly zero and is skipped
   __shared__ uint32_t s_act[64];
+  // a group of GL = kLinBlock / LPC lanes per landmark of the chunk (GL >= K: lane j of the
+  // group takes the landmark's j-th observation -- at most one per frame)
+  const int GL = kLinBlock / LPC, t = threadIdx.x / GL, j = threadIdx.x % GL;
   for (int c = part; c * LPC < L; c += dm.NPART) {
-    for (int i = threadIdx.x; i < rows * NRP; i += kLinBlock) sY[i] = 0.0;
+    {
+      typedef double d2 __attribute__((ext_vector_type(2)));
+      d2* z2 = reinterpret_cast<d2*>(sY);
+      for (int i = threadIdx.x; i < rows * NRP / 2; i += kLinBlock) z2[i] = d2{0.0, 0.0};
+    }
     if (threadIdx.x < 64) s_act[threadIdx.x] = 0u;
     __syncthreads();
-    // the chunk's observations are contiguous (landmark-major): [ob0, ob1)
-    const int lc0 = c * LPC, lc1 = min(L, lc0 + LPC);
-    const int ob0 = v.lstart[lc0], nob = v.lstart[lc1] - ob0;
-    // (a) per observation: its landmark-block terms w Jl^T Jl (upper 6) and w Jl^T r (3)
-    for (int i = threadIdx.x; i < nob; i += kLinBlock) {
-      const BaObs o = v.obs[ob0 + i];
-      double r[3], w, rho, Jp[3][6], Jl[3][3];
-      ba_eval<true>(S->T[o.frame], X + 3 * o.lm, o, cam, obs_is2(in, o), r, w, rho, Jp, Jl);
-      double* hg = sHg + 9 * i;
-      int q = 0;
-      for (int a = 0; a < 3; ++a) {
-        for (int b = a; b < 3; ++b) hg[q++] = w * (Jl[0][a] * Jl[0][b] + Jl[1][a] * Jl[1][b] + Jl[2][a] * Jl[2][b]);
-        hg[6 + a] = w * (Jl[0][a] * r[0] + Jl[1][a] * r[1] + Jl[2][a] * r[2]);
-      }
-    }
-    __syncthreads();
-    // (b) per landmark: the terms summed in observation order, damped Cholesky, z = L^-1 g
-    const int t = threadIdx.x, l = lc0 + t;
-    if (t < LPC && l < L) {
+    const int lc0 = c * LPC, l = lc0 + t;
+    if (l < L) {
+      // (a) lane j: observation j's landmark-block terms w Jl^T Jl (upper 6) and w Jl^T r (3);
+      // (b) their sum over the group (xor butterfly: every lane ends with the same sums), the
+      // damped 3x3 Cholesky (redundantly per lane) and z = L^-1 g; (c) lane j: the rows
+      // 6 (f-1) .. 6 (f-1) + 5 of W L^-T for its observation (solve L y = W_p)
       const int o0 = v.lstart[l], o1 = v.lstart[l + 1];
-      double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-      for (int oi = o0; oi < o1; ++oi) {
-        const double* hg = sHg + 9 * (oi - ob0);
-        for (int q = 0; q < 6; ++q) H[q] += hg[q];
-        for (int a = 0; a < 3; ++a) g[a] += hg[6 + a];
+      const bool has = j < o1 - o0;
+      double hg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      BaObs o{};
+      if (has) {
+        o = v.obs[o0 + j];
+        double r[3], w, rho, Jl[3][3];
+        ba_eval<true, false>(S->T[o.frame], X + 3 * o.lm, o, cam, obs_is2(in, o), r, w, rho, nullptr, Jl);
+        int q = 0;
+        for (int a = 0; a < 3; ++a) {
+          for (int b = a; b < 3; ++b) hg[q++] = w * (Jl[0][a] * Jl[0][b] + Jl[1][a] * Jl[1][b] + Jl[2][a] * Jl[2][b]);
+          hg[6 + a] = w * (Jl[0][a] * r[0] + Jl[1][a] * r[1] + Jl[2][a] * r[2]);
+        }
       }
-      // damped Cholesky of [H0 H1 H2; . H3 H4; . . H5]
+      for (int m = GL >> 1; m >= 1; m >>= 1)
+#pragma unroll
+        for (int q = 0; q < 9; ++q) hg[q] += __shfl_xor(hg[q], m, 64);
+      const double* H = hg;
       const double a00 = H[0] + lam * H[0] + 1e-6, a11 = H[3] + lam * H[3] + 1e-6, a22 = H[5] + lam * H[5] + 1e-6;
-      const double l00 = sqrt(a00);
-      const double l10 = H[1] / l00, l20 = H[2] / l00;
-      const double l11 = sqrt(a11 - l10 * l10);
-      const double l21 = (H[4] - l20 * l10) / l11;
-      const double l22 = sqrt(a22 - l20 * l20 - l21 * l21);
-      double* Lf = v.Lf + 6 * l;
-      Lf[0] = l00; Lf[1] = l10; Lf[2] = l11; Lf[3] = l20; Lf[4] = l21; Lf[5] = l22;
-      double* sl = sLf + 6 * t;
-      sl[0] = l00; sl[1] = l10; sl[2] = l11; sl[3] = l20; sl[4] = l21; sl[5] = l22;
-      v.gl[3 * l] = g[0]; v.gl[3 * l + 1] = g[1]; v.gl[3 * l + 2] = g[2];
+      const double i00 = rsq_r(a00), l00 = a00 * i00;
+      const double l10 = H[1] * i00, l20 = H[2] * i00;
+      const double d11 = a11 - l10 * l10, i11 = rsq_r(d11), l11 = d11 * i11;
+      const double l21 = (H[4] - l20 * l10) * i11;
+      const double d22 = a22 - l20 * l20 - l21 * l21, i22 = rsq_r(d22), l22 = d22 * i22;
       double* Y0 = sY + 3 * t * NRP;
-      const double z0 = g[0] / l00, z1 = (g[1] - l10 * z0) / l11, z2 = (g[2] - l20 * z0 - l21 * z1) / l22;
-      Y0[NR - 1] = z0;
-      Y0[NRP + NR - 1] = z1;
-      Y0[2 * NRP + NR - 1] = z2;
-    }
-    __syncthreads();
-    // (c) per observation: rows 6 (f-1) .. 6 (f-1) + 5 of W L^-T (solve L y = W_p)
-    for (int i = threadIdx.x; i < nob; i += kLinBlock) {
-      const BaObs o = v.obs[ob0 + i];
-      const int f = o.frame;
-      if (f == 0) continue;
-      const int tl = o.lm - lc0;
-      {
-        const uint32_t bits = (1u << (6 * (f - 1) / 16)) | (1u << ((6 * (f - 1) + 5) / 16));
-        atomicOr(&s_act[3 * tl / 4], bits);
-        if ((3 * tl + 2) / 4 != 3 * tl / 4) atomicOr(&s_act[(3 * tl + 2) / 4], bits);
+      if (j == 0) {
+        double* Lf = v.Lf + 6 * l;
+        Lf[0] = l00; Lf[1] = l10; Lf[2] = l11; Lf[3] = l20; Lf[4] = l21; Lf[5] = l22;
+        v.gl[3 * l] = H[6]; v.gl[3 * l + 1] = H[7]; v.gl[3 * l + 2] = H[8];
+        const double z0 = H[6] * i00, z1 = (H[7] - l10 * z0) * i11, z2 = (H[8] - l20 * z0 - l21 * z1) * i22;
+        Y0[NR - 1] = z0;
+        Y0[NRP + NR - 1] = z1;
+        Y0[2 * NRP + NR - 1] = z2;
       }
-      const double* sl = sLf + 6 * tl;
-      const double l00 = sl[0], l10 = sl[1], l11 = sl[2], l20 = sl[3], l21 = sl[4], l22 = sl[5];
-      const double* Wo = v.W + (int64_t)(ob0 + i) * 18;
-      double* Y0 = sY + 3 * tl * NRP;
-      for (int p = 0; p < 6; ++p) {
-        const double y0 = Wo[3 * p] / l00;
-        const double y1 = (Wo[3 * p + 1] - l10 * y0) / l11;
-        const double y2 = (Wo[3 * p + 2] - l20 * y0 - l21 * y1) / l22;
-        const int col = 6 * (f - 1) + p;
-        Y0[col] = y0;
-        Y0[NRP + col] = y1;
-        Y0[2 * NRP + col] = y2;
+      const int f = o.frame;
+      if (has && f > 0) {
+        const double* Wo = v.W + (int64_t)(o0 + j) * 18;
+        for (int pp = 0; pp < 6; ++pp) {
+          const double y0 = Wo[3 * pp] * i00;
+          const double y1 = (Wo[3 * pp + 1] - l10 * y0) * i11;
+          const double y2 = (Wo[3 * pp + 2] - l20 * y0 - l21 * y1) * i22;
+          const int col = 6 * (f - 1) + pp;
+          Y0[col] = y0;
+          Y0[NRP + col] = y1;
+          Y0[2 * NRP + col] = y2;
+        }
+        const uint32_t bits = (1u << (6 * (f - 1) / 16)) | (1u << ((6 * (f - 1) + 5) / 16));
+        atomicOr(&s_act[3 * t / 4], bits);
+        if ((3 * t + 2) / 4 != 3 * t / 4) atomicOr(&s_act[(3 * t + 2) / 4], bits);
       }
     }
     __syncthreads();
     // G += Yt^T Yt on MFMA: A[i][k] = Yt[k][16I + i], B[k][j] = Yt[k][16J + j], lane holds k = lane >> 4;
     // the active 4-row steps of the tile (every row's z column is live: J = NT-1 always
-    // counts), ascending, alternately into two accumulators by step parity (fixed order)
+    // counts), ascending into one accumulator per tile (fixed order)
     const uint32_t actl = lane < rows / 4 ? s_act[lane] : 0u;
 #pragma unroll
     for (int lt = 0; lt < kLinMaxTiles; ++lt) {
@@ -702,8 +711,7 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
           const int g = __builtin_ctzll(m);
           m &= m - 1;
           const double a = ya[4 * g * NRP], bv = yb[4 * g * NRP];
-          if (g & 1) acc[lt][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc[lt][1], 0, 0, 0);
-          else acc[lt][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc[lt][0], 0, 0, 0);
+          acc[lt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc[lt], 0, 0, 0);
         }
       }
     }
@@ -718,7 +726,7 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
       int I, J;
       lin_tile(k, ntu, NT, I, J);
       for (int i = 0; i < 4; ++i)
-        Gc[(16 * I + (lane >> 4) + 4 * i) * NR + 16 * J + (lane & 15)] = acc[lt][0][i] + acc[lt][1][i];
+        Gc[(16 * I + (lane >> 4) + 4 * i) * NR + 16 * J + (lane & 15)] = acc[lt][i];
     }
   }
 }
@@ -731,6 +739,10 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
   BaState* S = v.st;
   if (!S->active) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#ifdef FVO_BA_STAMPS
+  long long stamp[6];
+  stamp[0] = clock64();
+#endif
   const int n = S->n, L = S->L, NR = dm.NR;
   const int np = 6 * (n - 1);
   const int nch0 = (L + dm.LPC - 1) / dm.LPC, nch = nch0 < dm.NPART ? nch0 : dm.NPART;  // partials used
@@ -783,6 +795,9 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
     rhs[a] = -S->Hpp[a / 6 + 1][21 + a % 6] + gs;
   }
   __syncthreads();
+#ifdef FVO_BA_STAMPS
+  stamp[1] = clock64();
+#endif
   const int ta = tid / kSGB, tb = tid % kSGB;
   // Right-looking Cholesky by panels of kChol columns, two barriers per panel: (A) every
   // thread factors the panel's diagonal block itself (identical arithmetic everywhere, so
@@ -795,8 +810,9 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
   bool fail = false;
   for (int k = 0; k < np; k += kChol) {
     const int pw = min(kChol, np - k);
-    // pivots as reciprocals (one division per column; the entries below it are products), so
-    // the panel's dependent chain holds one sqrt and one division per column
+    // pivots as reciprocal square roots (rsq_r, one hardware estimate + one Newton step), so
+    // the entries below the diagonal are products and the panel's dependent chain holds no
+    // IEEE sqrt / division sequence
     double Lb[kChol][kChol], rp[kChol];
 #pragma unroll
     for (int a2 = 0; a2 < kChol; ++a2) {
@@ -806,8 +822,8 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
         for (int c = 0; c < kChol; ++c)
           if (c < a2) d -= Lb[a2][c] * Lb[a2][c];
         if (!(d > 0.0)) fail = true;
-        Lb[a2][a2] = sqrt(d);
-        rp[a2] = 1.0 / Lb[a2][a2];
+        rp[a2] = rsq_r(d);
+        Lb[a2][a2] = d * rp[a2];
 #pragma unroll
         for (int b2 = 0; b2 < kChol; ++b2) {
           if (b2 > a2 && b2 < pw) {
@@ -859,6 +875,9 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
     }
     __syncthreads();
   }
+#ifdef FVO_BA_STAMPS
+  stamp[2] = clock64();
+#endif
   if (fail) {
     if (tid == 0) S->fail = 1;
     return;
@@ -874,26 +893,51 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
       const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
       return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
     };
+    // The factor's entries a step needs (column j of L for the forward pass, row j for the
+    // backward one) and the pivot's reciprocal are loaded one step ahead, so LDS latency stays
+    // off the chain (readlane -> multiply -> FMA); rows >= np carry garbage that is never read.
     const int r0 = lane, r1 = lane + 64;
+    const int c0 = min(r0, np - 1), c1 = min(r1, np - 1);
     double x0 = r0 < np ? rhs[r0] : 0.0, x1 = r1 < np ? rhs[r1] : 0.0;
-    for (int j = 0; j < np; ++j) {
-      const double yj = bcast(j < 64 ? x0 : x1, j & 63) * rinv[j];
-      if (r0 == j) x0 = yj;
-      if (r1 == j) x1 = yj;
-      if (r0 > j && r0 < np) x0 -= sS[r0 * np + j] * yj;
-      if (r1 > j && r1 < np) x1 -= sS[r1 * np + j] * yj;
+    {
+      double a0 = sS[c0 * np], a1 = sS[c1 * np], rv = rinv[0];
+      auto fwd = [&](int j, auto hi_t) {
+        constexpr bool HI = decltype(hi_t)::value;
+        const int jn = min(j + 1, np - 1);
+        const double na0 = sS[c0 * np + jn], na1 = sS[c1 * np + jn], nrv = rinv[jn];
+        const double yj = bcast(HI ? x1 : x0, j & 63) * rv;
+        x0 = r0 == j ? yj : (r0 > j ? x0 - a0 * yj : x0);
+        x1 = r1 == j ? yj : (r1 > j ? x1 - a1 * yj : x1);
+        a0 = na0; a1 = na1; rv = nrv;
+      };
+      const int jm = min(np, 64);
+      for (int j = 0; j < jm; ++j) fwd(j, std::false_type{});
+      for (int j = 64; j < np; ++j) fwd(j, std::true_type{});
     }
-    for (int j = np - 1; j >= 0; --j) {
-      const double xj = bcast(j < 64 ? x0 : x1, j & 63) * rinv[j];
-      if (r0 == j) x0 = xj;
-      if (r1 == j) x1 = xj;
-      if (r0 < j) x0 -= sS[j * np + r0] * xj;
-      if (r1 < j) x1 -= sS[j * np + r1] * xj;
+    {
+      double b0 = sS[(np - 1) * np + c0], b1 = sS[(np - 1) * np + c1], rv = rinv[np - 1];
+      auto bwd = [&](int j, auto hi_t) {
+        constexpr bool HI = decltype(hi_t)::value;
+        const int jn = max(j - 1, 0);
+        const double nb0 = sS[jn * np + c0], nb1 = sS[jn * np + c1], nrv = rinv[jn];
+        const double xj = bcast(HI ? x1 : x0, j & 63) * rv;
+        x0 = r0 == j ? xj : (r0 < j ? x0 - b0 * xj : x0);
+        x1 = r1 == j ? xj : (r1 < j ? x1 - b1 * xj : x1);
+        b0 = nb0; b1 = nb1; rv = nrv;
+      };
+      for (int j = np - 1; j >= 64; --j) bwd(j, std::true_type{});
+      for (int j = min(np, 64) - 1; j >= 0; --j) bwd(j, std::false_type{});
     }
     if (r0 < np) rhs[r0] = x0;
     if (r1 < np) rhs[r1] = x1;
   }
   __syncthreads();
+#ifdef FVO_BA_STAMPS
+  stamp[3] = clock64();
+  if (blockIdx.x == 0 && tid == 0)
+    printf("solve stamps np=%d: assemble %lld chol %lld trsv %lld\n", np, stamp[1] - stamp[0], stamp[2] - stamp[1],
+           stamp[3] - stamp[2]);
+#endif
   for (int a = tid; a < 6 * n; a += kSolveBlock) S->dp[a] = a < 6 ? 0.0 : rhs[a - 6];
   if (tid < n) {
     const int f = tid;
@@ -1047,7 +1091,9 @@ BaDims make_dims(const fvo_ctx* ctx) {
   // observation terms); measured: halving LPC (two blocks per CU) is slower at both shapes
   d.LPC = d.NR == 64 ? FVO_BA_LPC64 : FVO_BA_LPC64 / 2;
   d.NCH = (d.Lmax + d.LPC - 1) / d.LPC;
-  d.NPART = d.NCH < kLinParts ? d.NCH : kLinParts;
+  d.NPART = FVO_BA_PARTS > 0 ? FVO_BA_PARTS : d.NCH / kLinChunksPerPart;
+  d.NPART = d.NPART < 1 ? 1 : d.NPART > kLinParts ? kLinParts : d.NPART;
+  if (d.NPART > d.NCH) d.NPART = d.NCH;
   d.NCU = (d.Lmax + kBlock - 1) / kBlock;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
@@ -1078,7 +1124,7 @@ size_t build_shm(const BaDims& d) {
   const size_t maps = (size_t)2 * (d.K - 1) * d.cap + d.cap;
   return (d.cap < 0xFFFF && maps <= 156 * 1024) ? maps : (size_t)d.cap;  // + ~4 KB static <= 160 KiB
 }
-size_t lin_shm(const BaDims& d) { return (size_t)8 * (3 * d.LPC * (d.NR + 2) + 9 * d.LPC * d.K + 6 * d.LPC); }
+size_t lin_shm(const BaDims& d) { return (size_t)8 * 3 * d.LPC * (d.NR + 2); }
 size_t solve_shm(int K) {
   const int np = 6 * (K - 1);
   return (size_t)8 * (np * np + 2 * np);  // S, rhs, pivot roots
