@@ -58,15 +58,19 @@ constexpr int kBlock = 256;
 #ifndef FVO_BA_PARTS
 #define FVO_BA_PARTS 0
 #endif
+#ifndef FVO_BA_LW
+#define FVO_BA_LW 16
+#endif
 #ifndef FVO_BA_LPC64
 #define FVO_BA_LPC64 64
 #endif
 constexpr int kLinParts = 16, kLinChunksPerPart = 16;
 // k_ba_lin runs a group of kLinBlock / LPC lanes per landmark inside one wave: LPC >= 16
-static_assert(FVO_BA_LPC64 >= 32 && FVO_BA_LPC64 <= 64, "LPC64 in [32, 64]");
+static_assert(64 * FVO_BA_LW / (FVO_BA_LPC64 / 2) <= 64 && 64 * FVO_BA_LW / FVO_BA_LPC64 >= 16,
+              "a landmark's lane group fits one wave and holds K observations");
 // k_ba_lin runs 16 waves per block: its LDS slice (up to 150 KB) allows one block per CU, so
 // the block's own waves are all the latency hiding the CU gets
-constexpr int kLinWaves = 16, kLinBlock = 64 * kLinWaves;
+constexpr int kLinWaves = FVO_BA_LW, kLinBlock = 64 * kLinWaves;
 constexpr int kLinMaxTiles = (36 + kLinWaves - 1) / kLinWaves;  // 16x16 tiles per wave: 36 upper tiles at NR = 128
 constexpr double kD2Mono = 5.991, kD2Stereo = 7.815, kMinZ = 0.01, kLam0 = 1e-3;
 
