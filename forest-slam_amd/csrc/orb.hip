@@ -77,27 +77,47 @@ __global__ void k_copy_level0_v(const uint4* __restrict__ img, int64_t stride16,
   }
 }
 
-// INTER_LINEAR_EXACT level l from level l-1; a block covers 256 columns x kResRows rows (the
-// column tables are read once per thread).  The border cases are folded into the weights
-// (a clamped source index with weights 256 / 0 gives exactly the border formulas: s << 8 for
-// a column, (h + 128) >> 8 = (256 h + 32768) >> 16 for a row), so every load is unconditional
-// and the kResRows rows' loads are all in flight at once.
-constexpr int kResRows = 4;
+// INTER_LINEAR_EXACT level l from level l-1; a thread covers kResCols consecutive columns x
+// kResRows rows (the column tables are read once per thread).  The border cases are folded
+// into the weights (a clamped source index with weights 256 / 0 gives exactly the border
+// formulas: s << 8 for a column, (h + 128) >> 8 = (256 h + 32768) >> 16 for a row), so every
+// load is unconditional and the rows' loads are all in flight at once.  Interior threads read
+// the source bytes of their 4 columns as one 8-byte window per source row (three aligned
+// dwords, v_alignbyte) instead of 16 byte loads; a window never reaches past level l-1's
+// successor in the same image, so the aligned over-read stays inside the pyramid buffer.
+constexpr int kResRows = 4, kResCols = 4;
 __global__ void k_resize(const OrbDev G, uint8_t* __restrict__ pyr, int64_t total, int l, const int32_t* __restrict__ xofs,
                          const int32_t* __restrict__ xc1, const int32_t* __restrict__ yofs,
                          const int32_t* __restrict__ yc1) {
   const XcdBlock xb = xcd_block();  // blocks sharing source rows on one XCD
-  const int x = xb.x * blockDim.x + threadIdx.x;
+  const int x0 = (xb.x * blockDim.x + threadIdx.x) * kResCols;
   const int b = xb.z;
   const int w = G.w[l], h = G.h[l];
-  if (x >= w) return;
+  if (x0 >= w) return;
   const int sw = G.w[l - 1], sh = G.h[l - 1];
   const uint8_t* src = pyr + b * total + G.off[l - 1];
   uint8_t* dst = pyr + b * total + G.off[l];
-  const int ox = xofs[x];
-  const int oxa = ox >= 0 ? ox : (ox == -1 ? 0 : sw - 1), oxb = ox >= 0 ? ox + 1 : oxa;
-  const uint32_t cx1 = ox >= 0 ? (uint32_t)xc1[x] : 0u, cx0 = 256u - cx1;
-  uint32_t v[kResRows];
+  int oxa[kResCols], oxb[kResCols];
+  uint32_t cx0[kResCols], cx1[kResCols];
+#pragma unroll
+  for (int i = 0; i < kResCols; ++i) {
+    const int ox = xofs[min(x0 + i, w - 1)];
+    oxa[i] = ox >= 0 ? ox : (ox == -1 ? 0 : sw - 1);
+    oxb[i] = ox >= 0 ? ox + 1 : oxa[i];
+    cx1[i] = ox >= 0 ? (uint32_t)xc1[min(x0 + i, w - 1)] : 0u;
+    cx0[i] = 256u - cx1[i];
+  }
+  // interior: every column regular (ox >= 0) and the 4 columns' sources within 8 bytes
+  const bool win8 = x0 + kResCols <= w && xofs[x0] >= 0 && xofs[x0 + kResCols - 1] >= 0 &&
+                    oxb[kResCols - 1] - oxa[0] <= 7;
+  auto window = [&](const uint8_t* row) -> uint64_t {
+    const uintptr_t pa = reinterpret_cast<uintptr_t>(row + oxa[0]);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(pa & ~(uintptr_t)3);
+    const uint32_t sft = (uint32_t)(pa & 3);
+    const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+    return ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sft) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sft);
+  };
+  uint32_t v[kResRows][kResCols];
 #pragma unroll
   for (int k = 0; k < kResRows; ++k) {
     const int y = min(xb.y * kResRows + k, h - 1);
@@ -106,13 +126,29 @@ __global__ void k_resize(const OrbDev G, uint8_t* __restrict__ pyr, int64_t tota
     const uint32_t cy1 = oy >= 0 ? (uint32_t)yc1[y] : 0u, cy0 = 256u - cy1;
     const uint8_t* sa = src + (int64_t)ra * sw;
     const uint8_t* sb = src + (int64_t)rb * sw;
-    const uint32_t ha = cx0 * sa[oxa] + cx1 * sa[oxb], hb = cx0 * sb[oxa] + cx1 * sb[oxb];
-    v[k] = (ha * cy0 + hb * cy1 + 32768u) >> 16;
+    if (win8) {
+      const uint64_t wa = window(sa), wb = window(sb);
+#pragma unroll
+      for (int i = 0; i < kResCols; ++i) {
+        const int da = 8 * (oxa[i] - oxa[0]), db = 8 * (oxb[i] - oxa[0]);
+        const uint32_t ha = cx0[i] * (uint32_t)((wa >> da) & 255u) + cx1[i] * (uint32_t)((wa >> db) & 255u);
+        const uint32_t hb = cx0[i] * (uint32_t)((wb >> da) & 255u) + cx1[i] * (uint32_t)((wb >> db) & 255u);
+        v[k][i] = (ha * cy0 + hb * cy1 + 32768u) >> 16;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kResCols; ++i) {
+        const uint32_t ha = cx0[i] * sa[oxa[i]] + cx1[i] * sa[oxb[i]], hb = cx0[i] * sb[oxa[i]] + cx1[i] * sb[oxb[i]];
+        v[k][i] = (ha * cy0 + hb * cy1 + 32768u) >> 16;
+      }
+    }
   }
 #pragma unroll
   for (int k = 0; k < kResRows; ++k) {
     const int y = xb.y * kResRows + k;
-    if (y < h) dst[(int64_t)y * w + x] = (uint8_t)(v[k] > 255u ? 255u : v[k]);
+#pragma unroll
+    for (int i = 0; i < kResCols; ++i)
+      if (y < h && x0 + i < w) dst[(int64_t)y * w + x0 + i] = (uint8_t)(v[k][i] > 255u ? 255u : v[k][i]);
   }
 }
 
@@ -1124,7 +1160,7 @@ int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride
                                                       images, image_stride, pitch, ctx->pyr, total, W, H));
   }
   for (int l = 1; l < L; ++l)
-    FVO_TIMED(ctx, KN_ORB_RESIZE, s, hipLaunchKernelGGL(k_resize, dim3((g.w[l] + 255) / 256, (g.h[l] + kResRows - 1) / kResRows, batch), dim3(256), 0, s, G, ctx->pyr, total, l,
+    FVO_TIMED(ctx, KN_ORB_RESIZE, s, hipLaunchKernelGGL(k_resize, dim3((g.w[l] + 256 * kResCols - 1) / (256 * kResCols), (g.h[l] + kResRows - 1) / kResRows, batch), dim3(256), 0, s, G, ctx->pyr, total, l,
                        ctx->rt.xofs + ctx->rt.xoff[l], ctx->rt.xc1 + ctx->rt.xoff[l], ctx->rt.yofs + ctx->rt.yoff[l],
                        ctx->rt.yc1 + ctx->rt.yoff[l]));
   FVO_TIMED(ctx, KN_ORB_FAST, s, hipLaunchKernelGGL(k_fast_nms<false>, dim3(ntiles, batch), dim3(256), 0, s, G, ctx->pyr,
