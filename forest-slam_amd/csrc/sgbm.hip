@@ -502,6 +502,7 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
   constexpr int XS = 2 * D;  // u32 words per column of a 4-row group
   constexpr int RK = sg_ring_keys(D), RS = sg_ring_raw(D);
   __shared__ uint32_t s_key[4][RK];  // right-view keys of the live x2 window (ring, by x2)
+  __shared__ __attribute__((aligned(16))) uint16_t s_S[4][D];  // one column's S of each row (WTA neighbours)
   __shared__ int16_t s_raw[4][RS];   // raw disparities awaiting their check (ring, by x1)
   const int lane = threadIdx.x, q = lane & 15, r = lane >> 4;
   // consecutive row groups on one XCD: a group's first row reads the previous group's last
@@ -697,22 +698,15 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
     kmin = dmin<kRHalfMirror>(kmin);
     kmin = dmin<kRMirror>(kmin);
     const int d = (int)(kmin & 127u);
-    uint32_t nb = 0;
-    {
-      const int im = d - 1 - q * DQ, ip = d + 1 - q * DQ;
-      uint32_t wm = 0, wp = 0;
+    // S[d-1] << 16 | S[d+1] (only read when 0 < d < D-1): the row's S words through a one-column
+    // LDS slot (a wave's LDS accesses execute in order: no barrier, and the next column's store
+    // comes after these loads)
+    uint32_t* sw = reinterpret_cast<uint32_t*>(&s_S[r][q * DQ]);
 #pragma unroll
-      for (int kk = 0; kk < PQ; ++kk) {
-        wm = (im >> 1) == kk ? Sw[kk] : wm;
-        wp = (ip >> 1) == kk ? Sw[kk] : wp;
-      }
-      if (im >= 0 && im < DQ) nb |= ((im & 1) ? (wm >> 16) : (wm & 0xFFFFu)) << 16;
-      if (ip >= 0 && ip < DQ) nb |= (ip & 1) ? (wp >> 16) : (wp & 0xFFFFu);
-    }
-    nb = dor<kQX1>(nb);
-    nb = dor<kQX2>(nb);
-    nb = dor<kRHalfMirror>(nb);
-    nb = dor<kRMirror>(nb);
+    for (int kk = 0; kk < PQ; ++kk) sw[kk] = Sw[kk];
+    asm volatile("" ::: "memory");  // u32 stores, u16 loads: keep the compiler from reordering them
+    const uint32_t nb = ((uint32_t)s_S[r][max(d - 1, 0)] << 16) | s_S[r][min(d + 1, D - 1)];
+    asm volatile("" ::: "memory");
     wk = q == i ? kmin : wk;
     wn = q == i ? nb : wn;
   };
