@@ -100,6 +100,14 @@ __device__ __forceinline__ uint32_t dshift(uint32_t v, uint32_t old) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, 0xF, 0xF, false);
 }
 
+// the same with `edge` = the wanted value on the row's edge lane and 0 on the others: the shift
+// reads 0 where it has no source (the old value), OR-ed with `edge` -- one v_or_b32_dpp instead
+// of a move of the sentinel plus a DPP move
+template <int CTRL>
+__device__ __forceinline__ uint32_t dshift_or(uint32_t v, uint32_t edge) {
+  return edge | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+
 template <int NV4>
 __device__ __forceinline__ void load_run(const uint16_t* base, uint32_t* out) {
   const uint4* p4 = reinterpret_cast<const uint4*>(base);
@@ -430,9 +438,9 @@ __host__ __device__ constexpr int sg_ring_raw(int D) { return sg_pow2(D + 16); }
 template <int PQ>
 __device__ __forceinline__ uint32_t step16(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
                                            uint32_t P2) {
-  // a row's lanes 0 / 15 have no left / right neighbour: the shift leaves the sentinel there
-  const uint32_t lo0 = dshift<kRShr1>(st[PQ - 1], kSent << 16);
-  const uint32_t hiN = dshift<kRShl1>(st[0], kSent);
+  // a row's lanes 0 / 15 have no left / right neighbour: the sentinel there
+  const uint32_t lo0 = dshift_or<kRShr1>(st[PQ - 1], q == 0 ? kSent << 16 : 0u);
+  const uint32_t hiN = dshift_or<kRShl1>(st[0], q == 15 ? kSent : 0u);
   const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
   u16x2 mn = splat(0xFFFF);
   uint32_t oldk = 0;
@@ -459,10 +467,10 @@ __device__ __forceinline__ void vadd(uint32_t* a, const uint32_t* b) {
 // exactly (modular).  16 lanes per row as step16; m = min Vp (stored by the cost pass).
 template <int PQ>
 __device__ __forceinline__ void derive16(const uint32_t* vp, const uint32_t* v, uint32_t* c, uint32_t m, u16x2 P1,
-                                         uint32_t P2) {
-  // a row's lanes 0 / 15 have no left / right neighbour: the shift leaves the sentinel there
-  const uint32_t lo0 = dshift<kRShr1>(vp[PQ - 1], kSent << 16);
-  const uint32_t hiN = dshift<kRShl1>(vp[0], kSent);
+                                         uint32_t P2, int q) {
+  // a row's lanes 0 / 15 have no left / right neighbour: the sentinel there
+  const uint32_t lo0 = dshift_or<kRShr1>(vp[PQ - 1], q == 0 ? kSent << 16 : 0u);
+  const uint32_t hiN = dshift_or<kRShl1>(vp[0], q == 15 ? kSent : 0u);
   const u16x2 mp2 = splat(m + P2), mpv = splat(m);
 #pragma unroll
   for (int k = 0; k < PQ; ++k) {
@@ -615,7 +623,7 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
     for (int j = 0; j < SEG; ++j) {
       const int x = x0 + j;
       uint32_t c[PQ];
-      derive16<PQ>(pb[j % PD], vb[j % PD], c, mb[j % PD], P1, p.P2);
+      derive16<PQ>(pb[j % PD], vb[j % PD], c, mb[j % PD], P1, p.P2, q);
       if (FIRST) {
 #pragma unroll
         for (int k = 0; k < PQ; ++k) c[k] = x < 0 ? 0u : c[k];
@@ -729,8 +737,8 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
       for (int t = 0; t < SEG; ++t) {
         const int a = SEG - 1 - t, c = t;  // L column, R column
         if (t < SEG / 2) {
-          derive16<PQ>(Pn[a], Vn[a], Cs[a], Mn[a], P1, p.P2);
-          derive16<PQ>(Pn[c], Vn[c], Cs[c], Mn[c], P1, p.P2);
+          derive16<PQ>(Pn[a], Vn[a], Cs[a], Mn[a], P1, p.P2, q);
+          derive16<PQ>(Pn[c], Vn[c], Cs[c], Mn[c], P1, p.P2, q);
         }
         lmin = step16<PQ>(lst, Cs[a], q, P1, lmin, p.P2);
         minR = step16<PQ>(Rst, Cs[c], q, P1, minR, p.P2);
@@ -764,7 +772,7 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
       uint32_t lmin = zero ? 0u : ckn[PQ];
 #pragma unroll
       for (int i = SEG - 1; i >= 0; --i) {
-        derive16<PQ>(Pn[i], Vn[i], Cs[i], Mn[i], P1, p.P2);
+        derive16<PQ>(Pn[i], Vn[i], Cs[i], Mn[i], P1, p.P2, q);
         if (i <= ihi_of(sg)) lmin = step16<PQ>(lst, Cs[i], q, P1, lmin, p.P2);
 #pragma unroll
         for (int kk = 0; kk < PQ; ++kk) Ls[i][kk] = as_u(as_v(lst[kk]) + as_v(Vn[i][kk]));
