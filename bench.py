@@ -381,8 +381,15 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # FVO_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU
+        # (RCCL needs one GPU per rank); the driver's runs use nccl = RCCL
+        backend = os.environ.get("FVO_DIST_BACKEND", "nccl")
+        local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
