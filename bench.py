@@ -270,8 +270,13 @@ def main_frames(args):
     tdist = None
     if world > 1:
         import torch.distributed as tdist
+        backend = os.environ.get("FVO_DIST_BACKEND", "nccl")  # gloo: rehearsal, several ranks per GPU
+        local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
