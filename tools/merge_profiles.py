@@ -36,9 +36,17 @@ def main(src, dst):
             w.writeheader()
             w.writerows(rows + kept)
         print(f"{name}: {len(rows)} rows of {sorted(shapes)} + {len(kept)} kept")
+    # the bench line that ran under the trace pass; one file per shape (a 1080p run must not
+    # overwrite the 600p one): bench_under_trace.json for the headline shape, else _1080p etc.
     b = os.path.join(src, "bench_under_trace.json")
     if os.path.exists(b):
-        shutil.copy(b, os.path.join(dst, "bench_under_trace.json"))
+        shapes = set()
+        with open(os.path.join(src, "kernel_stats.csv"), newline="") as f:
+            shapes = {r["shape"] for r in csv.DictReader(f)}
+        name = "bench_under_trace.json"
+        if any(sh.startswith("1920x1080") for sh in shapes):
+            name = "bench_under_trace_1080p.json"
+        shutil.copy(b, os.path.join(dst, name))
 
 
 if __name__ == "__main__":
