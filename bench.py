@@ -22,6 +22,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -256,85 +258,155 @@ def pmc_valu(shape: str):
                         for r in rows if r["kernel"].startswith(hot)}}
 
 
-def main_frames(args):
-    """--shard frames: one sequence of steps x B frame pairs split over the ranks by contiguous
-    frame-pair shards (dist.frame_shard, K-1 halo for the local BA), SURVEY §8e's strong-scaling
-    path.  Each rank renders its shard plus the halo before it, runs its
-    shard in `steps` steps of ceil(B / world) frames, then the relative poses are all-gathered
-    and chained left to right (dist.gather_relative_poses + eval.chain) -- inside the timed
-    region (W untimed passes over the shard first).  value = the sequence's frames / the
-    max-over-ranks time."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    tdist = None
-    if world > 1:
-        import torch.distributed as tdist
-        backend = os.environ.get("FVO_DIST_BACKEND", "nccl")  # gloo: rehearsal, several ranks per GPU
-        local = local % torch.cuda.device_count()
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+def _free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """``--gpus N`` (N > 1) run directly, with no torch.distributed launcher around it: start N
+    worker ranks as ``python -m torch.distributed.run --nproc-per-node N ... bench.py <same
+    args>`` and return their exit status.  This process never touches the GPU (no HIP call
+    before or after), so the workers own the devices; rank 0 prints the JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+class Ranks:
+    """This process's place in the run: world size / rank / local rank from the launcher's
+    environment, the process group (backend nccl = RCCL by default; FVO_DIST_BACKEND=gloo
+    rehearses several ranks on one GPU), the device.  Refuses a run whose rank count differs
+    from --gpus, so a line's n_gpus is always the world size the process group reports."""
+
+    def __init__(self, args, cpu: bool = False):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {self.world} rank(s)")
+        self.dist, self.backend = None, None
+        if cpu:
+            self.dev = torch.device("cpu")
         else:
-            tdist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            self.dev = torch.device("cuda", local)
+        self.local = local
+        if self.world > 1:
+            import torch.distributed as tdist
+            self.dist = tdist
+            backend = os.environ.get("FVO_DIST_BACKEND", "gloo" if cpu else "nccl")
+            if backend == "nccl":
+                tdist.init_process_group("nccl", device_id=self.dev)
+            else:
+                tdist.init_process_group(backend)
+            self.backend = tdist.get_backend()
+        self.world_size_seen = self.dist.get_world_size() if self.dist else 1
+        if self.world_size_seen != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {self.world_size_seen} rank(s)")
+        # distinct (host, device) pairs over the ranks: = n_gpus on a real node, fewer in a
+        # rehearsal that puts several ranks on one card
+        if self.dist:
+            ids = [None] * self.world
+            self.dist.all_gather_object(ids, (socket.gethostname(), str(self.dev)))
+            self.devices = len(set(ids))
+        else:
+            self.devices = 1
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max_elapsed(self, elapsed: float) -> float:
+        if not self.dist:
+            return elapsed
+        t = torch.tensor([elapsed], dtype=torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def fields(self) -> dict:
+        return {"world_size_seen": self.world_size_seen, "backend": self.backend or "none (1 rank)",
+                "devices": self.devices}
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def main_dry_run(args):
+    """--dry-run: the launcher and process-group path without a GPU (CPU test of --gpus N):
+    gloo ranks on the CPU, a 1 ms host "step" + one all-reduce per step, the same barrier /
+    max-over-ranks timing and the same rank / world fields in the JSON line; value is null."""
+    rk = Ranks(args, cpu=True)
+    rk.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+        if rk.dist:
+            x = torch.ones(1)
+            rk.dist.all_reduce(x)
+    rk.barrier()
+    elapsed = rk.max_elapsed(time.perf_counter() - t0)
+    if rk.rank == 0:
+        out = {"metric": "stereo frames/sec (extract+match+local-BA) at 600p, 1/8 MI355X; ATE RMSE", "value": None,
+               "unit": "frames/s", "n_gpus": rk.world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 3), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": None, "data": "dry run: no GPU, no VO work",
+               "config": {"workload": "dry run (launcher / process-group check)", "parallelism": f"x{rk.world}"}}
+        out.update(rk.fields())
+        print(json.dumps(out), flush=True)
+    rk.close()
+
+
+def main_frames(args):
+    """--shard frames: ONE sequence of steps x B frame pairs split over the ranks by contiguous
+    frame-pair shards (SURVEY §8e's strong-scaling path).  Each rank renders only the images its
+    shard reads (its pairs, the BA halo of K-1 pairs before them and the image before that);
+    the timed region is one whole ``dist.run_sequence_sharded`` call -- the schedule the
+    bit-identity test covers: prime, the halo pairs, the shard in steps of ceil(B / world)
+    frames, the all-gather of the relative poses and the left-to-right chain -- after W untimed
+    passes.  value = the sequence's frames / the max-over-ranks time; the halo's share of a
+    rank's pairs is reported beside it."""
+    rk = Ranks(args)
+    dev = rk.dev
     import forest_slam_amd.build as fbuild
     from forest_slam_amd import dist as fdist
-    from forest_slam_amd import eval as ev
     from forest_slam_amd import synth, vo
     if not os.path.exists(fbuild.OUT):
         raise SystemExit("libfvo.so missing: run __graft_entry__.build() first")
     W, H, K = args.width, args.height, args.ba_window
+    world, rank = rk.world, rk.rank
     b = -(-args.batch // world)  # frames per rank per step
     n_pairs = args.steps * args.batch
-    s, e = fdist.frame_shard(n_pairs, rank, world)
     halo = K - 1 if K else 0
-    first = max(1, s - halo)  # pairs run before the timed shard: the BA halo
-    # the rank's frames: images first-1 .. e-1 of the one sequence (seed 0, same scene on every rank)
+    first, e = fdist.frame_shard(n_pairs, rank, world, halo=halo)  # pairs first .. e-1 (halo included)
+    owned = e - fdist.frame_shard(n_pairs, rank, world)[0]
+    # the rank's images first-1 .. e-1 of the one sequence (seed 0, same scene on every rank)
     seq = synth.StereoSequence(seed=0, n_frames=n_pairs + 1, W=W, H=H, device=dev)
-    L_all, R_all = seq.frames(range(first - 1, e))
+    L_loc, R_loc = seq.frames(range(first - 1, e))
     torch.cuda.synchronize()
     ba_caps = {k: v for k, v in (("ba_max_landmarks", args.ba_max_landmarks), ("ba_max_obs", args.ba_max_obs)) if v}
     fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=b, nfeatures=args.nfeatures, device=dev,
                            ba_window=K, overlap_sgbm=bool(args.overlap_sgbm), **ba_caps)
+    group = None
 
     def run():
-        fe.prime(L_all[0], R_all[0])
-        # the pairs before the shard (local indices 1 .. s-first): BA halo and warm-up
-        for a in range(1, s - first + 1, b):
-            fe.step(L_all[a:min(a + b, s - first + 1)], R_all[a:min(a + b, s - first + 1)])
-        torch.cuda.synchronize()
-        if tdist is not None:
-            tdist.barrier()
+        rk.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        Ts, sts = [], []
-        for a in range(s - first + 1, e - first + 1, b):
-            z = min(a + b, e - first + 1)
-            T, st = fe.step(L_all[a:z], R_all[a:z])
-            Ts.append(T.clone())
-            sts.append(st.clone())
-        T_loc = torch.cat(Ts) if Ts else torch.zeros((0, 4, 4), dtype=torch.float64, device=dev)
-        st_loc = torch.cat(sts) if sts else torch.zeros((0,), dtype=torch.int32, device=dev)
-        if tdist is not None:
-            T_all, S_all = fdist.gather_relative_poses(T_loc, st_loc, n_pairs)
-        else:
-            T_all, S_all = T_loc.cpu().numpy(), st_loc.cpu().numpy()
-        cum = ev.chain(T_all, S_all != -1)
+        rows, _, _ = fdist.run_sequence_sharded(lambda: fe, L_loc, R_loc, use_ba=bool(K), group=group,
+                                                first_image=first - 1, n_pairs=n_pairs)
         torch.cuda.synchronize()
-        if tdist is not None:
-            tdist.barrier()
-        return time.perf_counter() - t0, cum
+        rk.barrier()
+        return time.perf_counter() - t0, rows
 
-    for _ in range(max(args.warmup, 1)):  # whole untimed passes (rank 0's shard starts the sequence)
+    for _ in range(max(args.warmup, 1)):  # whole untimed passes
         run()
-    elapsed, cum = run()
-    if tdist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, rows = run()
+    elapsed = rk.max_elapsed(elapsed)
     if rank == 0:
         out = {
             "metric": "stereo frames/sec (extract+match+local-BA) at 600p, 1/8 MI355X; ATE RMSE",
@@ -350,11 +422,13 @@ def main_frames(args):
                                    + (f", local BA K={K} ({halo}-pair halo per shard)" if K else ""),
                        "frames_per_step": args.batch, "frames_per_step_per_gpu": b, "width": W, "height": H,
                        "nfeatures": args.nfeatures, "parallelism": f"frame-shard x{world}"},
-            "chained_poses": int(len(cum)),
+            "timed": "one dist.run_sequence_sharded call: prime + halo pairs + shard + all-gather + chain",
+            "halo_pairs_rank0": int((e - first) - owned), "pairs_rank0": int(e - first),
+            "chained_poses": int(len(rows)),
         }
+        out.update(rk.fields())
         print(json.dumps(out), flush=True)
-    if tdist is not None:
-        tdist.destroy_process_group()
+    rk.close()
 
 
 def main():
@@ -376,28 +450,20 @@ def main():
     ap.add_argument("--shard", choices=("sequences", "frames"), default="sequences",
                     help="sequences: one sequence per GPU, B frames per GPU per step (weak scaling, the default); "
                          "frames: ONE sequence of steps x B frames split by frame pairs over the GPUs (strong scaling)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / process-group check without a GPU (gloo ranks on the CPU, no VO work)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)  # N ranks, one per GPU; this process never touches the GPU
+    if args.dry_run:
+        return main_dry_run(args)
     if args.shard == "frames":
         return main_frames(args)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        # FVO_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU
-        # (RCCL needs one GPU per rank); the driver's runs use nccl = RCCL
-        backend = os.environ.get("FVO_DIST_BACKEND", "nccl")
-        local = local % torch.cuda.device_count()
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    rk = Ranks(args)
+    world, rank, dev = rk.world, rk.rank, rk.dev
 
     import forest_slam_amd.build as fbuild
     from forest_slam_amd import eval as ev
@@ -420,10 +486,11 @@ def main():
     fwd = (L_all[1:].contiguous(), R_all[1:].contiguous())
     bwd = (L_all[:B].flip(0).contiguous(), R_all[:B].flip(0).contiguous())
     from forest_slam_amd import dist as fdist
-    # front-end step + (world > 1, local BA) the RCCL map exchange and the multi-sequence map
-    # built from it (dist.GlobalMap: every rank's window landmarks in its sequence's frame)
-    lm_cap = int(fe.ctx.cfg.ba_max_landmarks)
-    rank_step = fdist.SequenceRank(fe, map_capacity=(args.warmup + args.steps + 4) * world * lm_cap)
+    # front-end step + (world > 1) the RCCL map exchange of the step's poses and every frame's
+    # points3D and the multi-sequence map built from it on the device (dist.GlobalMap), on a
+    # side stream behind the step
+    steps_total = max(args.warmup, 1) + 2 + args.steps
+    rank_step = fdist.SequenceRank(fe, map_capacity=steps_total * world * B * fe.cap)
     nstep = [0]
 
     def eager_step():
@@ -456,29 +523,26 @@ def main():
     # stream overlapped its launches share the GPU with the main stream's kernels, so the
     # in-order launch time of the breakdown pass is reported beside it
     fe.ctx.timing_enable([dom])
-    if dist is not None:
-        dist.barrier()
+    rk.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    rk.barrier()
     elapsed = time.perf_counter() - t0
     dom_t = fe.ctx.timing_read()
     fe.ctx.timing_enable([])
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = rk.max_elapsed(elapsed)
 
     global_map = None
     if rank_step.gmap is not None:
         gm = rank_step.gmap.flush()
-        global_map = {"points": len(gm), "sequences": world, "steps_placed": len(rank_step.gmap.counts),
-                      "what": "every rank's last-BA-window landmarks per step, all-gathered over RCCL and placed "
-                              "with each sequence's chained poses (dist.GlobalMap)"}
+        torch.cuda.synchronize()
+        global_map = {"points": len(gm), "sequences": world, "steps_placed": rank_step.gmap.steps,
+                      "what": "every posed frame's points3D of every rank, all-gathered over RCCL each step and "
+                              "placed on the device with each sequence's chained poses (dist.GlobalMap: "
+                              "fvo_chain_poses + fvo_map_transform)"}
     frames = world * B * args.steps
     value = frames / elapsed
     dom_ms, dom_launches = dom_t.get(dom, (0.0, 0))
@@ -576,10 +640,10 @@ def main():
             "stages_ms_per_step": stage_ms,
             "workspace_gb": round(fe.ctx.workspace_bytes / 1e9, 2),
         }
+        out.update(rk.fields())
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    rk.close()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -31,7 +31,7 @@ class FvoConfig(ctypes.Structure):
             "ba_max_obs", "sgbm_max_batch")]
 
 
-ABI_VERSION = 4  # FVO_ABI_VERSION of include/fvo.h
+ABI_VERSION = 5  # FVO_ABI_VERSION of include/fvo.h
 STAGE_ORB, STAGE_BF, STAGE_SGBM, STAGE_POSE, STAGE_BA, STAGE_MONO = 1, 2, 4, 8, 16, 32
 
 # name -> (restype, argtypes); mirrors include/fvo.h
@@ -65,6 +65,7 @@ SIGNATURES = {
                                         ctypes.c_double, ctypes.c_double, _P, _P, _P, _P, _P]),
     "fvo_undistort_gray": (ctypes.c_int, [_P, _P, _I, _L, _I, _P, _P, _P, _L, _I, _P]),
     "fvo_map_transform": (ctypes.c_int, [_P, _P, _I, _P, _I, _L, _P, _P, _L, _P, _P, _P]),
+    "fvo_chain_poses": (ctypes.c_int, [_P, _P, _P, _P, _I, _I, _P, _P, _P, _P]),
     "fvo_voxel_workspace_bytes": (ctypes.c_int64, [_L]),
     "fvo_voxel_down_sample": (ctypes.c_int, [_P, _P, _L, ctypes.c_double, _P, _L, _P, _P, _P, _P]),
     "fvo_motion_blur": (ctypes.c_int, [_P, _P, _I, _L, _I, _I, ctypes.c_double, _P, _P, _I, _P, _P, _L, _I, _P]),
@@ -382,6 +383,31 @@ class Context:
                                              _ptr(map_xyz32) if map_xyz32 is not None else None,
                                              _stream(self.device)))
         return map_count
+
+    def chain_poses(self, T, status, cum_state, n_points=None, out=None):
+        """Advance the pose chains of S sequences over one batch of n frames each on the device
+        (stereo_slam.py:292-306; fvo_chain_poses).  T f64 [S,n,4,4], status i32 [S,n], n_points
+        i32 [S,n] or None, cum_state f64 [S,4,4] (advanced in place).  Returns (cum f64
+        [S,n,4,4] = each frame's cumulative pose, n_points_out i32 [S,n] = n_points of the
+        posed frames (status >= 0), 0 elsewhere; None without n_points)."""
+        if T.dim() != 4 or T.shape[2:] != (4, 4) or T.dtype != torch.float64 or not T.is_contiguous():
+            raise TypeError("T must be contiguous float64 [S, n, 4, 4]")
+        S, n = T.shape[0], T.shape[1]
+        if status.dtype != torch.int32 or status.shape != (S, n) or not status.is_contiguous():
+            raise TypeError("status must be contiguous int32 [S, n]")
+        if cum_state.dtype != torch.float64 or cum_state.shape != (S, 4, 4) or not cum_state.is_contiguous():
+            raise TypeError("cum_state must be contiguous float64 [S, 4, 4]")
+        if n_points is not None and (n_points.dtype != torch.int32 or n_points.shape != (S, n)
+                                     or not n_points.is_contiguous()):
+            raise TypeError("n_points must be contiguous int32 [S, n]")
+        if out is None:
+            cum = torch.empty_like(T)
+            npo = torch.empty_like(n_points) if n_points is not None else None
+        else:
+            cum, npo = out
+        self._check(self.L.fvo_chain_poses(self.h, _ptr(T), _ptr(status), _ptr(n_points), S, n, _ptr(cum_state),
+                                           _ptr(cum), _ptr(npo), _stream(self.device)))
+        return cum, npo
 
     def voxel_down_sample(self, points, voxel_size, workspace=None):
         """Open3D voxel_down_sample (mono_slam.py:155): points f64 [N,3] (device) ->

@@ -30,7 +30,7 @@
 #include <cfloat>
 #include <type_traits>
 
-#include "fvo_internal.h"
+#include "fvo_device.h"
 
 namespace {
 
@@ -47,7 +47,7 @@ struct BaCam {
 constexpr int kKMax = 21;
 constexpr int kBlock = 256;
 // k_ba_lin: blocks per window NPART = (chunk capacity) / kLinChunksPerPart, clamped to [1,
-// kLinParts] (FVO_BA_PARTS overrides); block p reduces the landmark chunks p, p + NPART, ...
+// kLinParts]; block p reduces the landmark chunks p, p + NPART, ...
 // into one partial Schur product (MFMA accumulators kept across its chunks), so k_ba_solve
 // sums NPART partials instead of one per chunk.  Fixed chunk order: deterministic.  The
 // count matters in the overlapped pipeline: each k_ba_lin block holds a whole CU (its LDS
@@ -55,22 +55,16 @@ constexpr int kBlock = 256;
 // iteration, fewer leave the BA latency-bound.  Measured (bench.py, overlapped): 600p / 64
 // windows / 64 chunks: 16 parts 4770 frames/s, 8: 4787, 4: 4848, 2: 4556, 1: 4054; 1080p /
 // 32 windows / 256 chunks: 16 parts 1219, 8: 1120, 4: 1125.
-#ifndef FVO_BA_PARTS
-#define FVO_BA_PARTS 0
-#endif
-#ifndef FVO_BA_LW
-#define FVO_BA_LW 16
-#endif
-#ifndef FVO_BA_LPC64
-#define FVO_BA_LPC64 64
-#endif
 constexpr int kLinParts = 16, kLinChunksPerPart = 16;
+// landmarks per k_ba_lin chunk at NR = 64 (half at NR = 128); measured: 32 / 16 per chunk
+// (4610 / 4404 frames/s) and two 8-wave blocks per CU (4796) lose to one 16-wave block with 64
+constexpr int kLinLPC64 = 64, kLinWavesDefault = 16;
 // k_ba_lin runs a group of kLinBlock / LPC lanes per landmark inside one wave: LPC >= 16
-static_assert(64 * FVO_BA_LW / (FVO_BA_LPC64 / 2) <= 64 && 64 * FVO_BA_LW / FVO_BA_LPC64 >= 16,
+static_assert(64 * kLinWavesDefault / (kLinLPC64 / 2) <= 64 && 64 * kLinWavesDefault / kLinLPC64 >= 16,
               "a landmark's lane group fits one wave and holds K observations");
 // k_ba_lin runs 16 waves per block: its LDS slice (up to 150 KB) allows one block per CU, so
 // the block's own waves are all the latency hiding the CU gets
-constexpr int kLinWaves = FVO_BA_LW, kLinBlock = 64 * kLinWaves;
+constexpr int kLinWaves = kLinWavesDefault, kLinBlock = 64 * kLinWaves;
 constexpr int kLinMaxTiles = (36 + kLinWaves - 1) / kLinWaves;  // 16x16 tiles per wave: 36 upper tiles at NR = 128
 constexpr double kD2Mono = 5.991, kD2Stereo = 7.815, kMinZ = 0.01, kLam0 = 1e-3;
 
@@ -743,10 +737,6 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
   BaState* S = v.st;
   if (!S->active) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-#ifdef FVO_BA_STAMPS
-  long long stamp[6];
-  stamp[0] = clock64();
-#endif
   const int n = S->n, L = S->L, NR = dm.NR;
   const int np = 6 * (n - 1);
   const int nch0 = (L + dm.LPC - 1) / dm.LPC, nch = nch0 < dm.NPART ? nch0 : dm.NPART;  // partials used
@@ -799,9 +789,6 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
     rhs[a] = -S->Hpp[a / 6 + 1][21 + a % 6] + gs;
   }
   __syncthreads();
-#ifdef FVO_BA_STAMPS
-  stamp[1] = clock64();
-#endif
   const int ta = tid / kSGB, tb = tid % kSGB;
   // Right-looking Cholesky by panels of kChol columns, two barriers per panel: (A) every
   // thread factors the panel's diagonal block itself (identical arithmetic everywhere, so
@@ -879,9 +866,6 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
     }
     __syncthreads();
   }
-#ifdef FVO_BA_STAMPS
-  stamp[2] = clock64();
-#endif
   if (fail) {
     if (tid == 0) S->fail = 1;
     return;
@@ -936,12 +920,6 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
     if (r1 < np) rhs[r1] = x1;
   }
   __syncthreads();
-#ifdef FVO_BA_STAMPS
-  stamp[3] = clock64();
-  if (blockIdx.x == 0 && tid == 0)
-    printf("solve stamps np=%d: assemble %lld chol %lld trsv %lld\n", np, stamp[1] - stamp[0], stamp[2] - stamp[1],
-           stamp[3] - stamp[2]);
-#endif
   for (int a = tid; a < 6 * n; a += kSolveBlock) S->dp[a] = a < 6 ? 0.0 : rhs[a - 6];
   if (tid < n) {
     const int f = tid;
@@ -1093,9 +1071,9 @@ BaDims make_dims(const fvo_ctx* ctx) {
   d.NR = 6 * (d.K - 1) < 63 ? 64 : 128;
   // landmarks per k_ba_lin chunk: LDS slice 3 LPC x (NR + 2) doubles <= 99 KB (+ the chunk's
   // observation terms); measured: halving LPC (two blocks per CU) is slower at both shapes
-  d.LPC = d.NR == 64 ? FVO_BA_LPC64 : FVO_BA_LPC64 / 2;
+  d.LPC = d.NR == 64 ? kLinLPC64 : kLinLPC64 / 2;
   d.NCH = (d.Lmax + d.LPC - 1) / d.LPC;
-  d.NPART = FVO_BA_PARTS > 0 ? FVO_BA_PARTS : d.NCH / kLinChunksPerPart;
+  d.NPART = d.NCH / kLinChunksPerPart;
   d.NPART = d.NPART < 1 ? 1 : d.NPART > kLinParts ? kLinParts : d.NPART;
   if (d.NPART > d.NCH) d.NPART = d.NCH;
   d.NCU = (d.Lmax + kBlock - 1) / kBlock;
@@ -1220,10 +1198,7 @@ int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* mat
   // The windows are independent: the batch is split in two halves whose LM sequences run on
   // two streams, so one half's latency-bound kernels (build, the per-window solve on one
   // block each) overlap the other half's whole-GPU kernels instead of leaving most CUs idle.
-#ifndef FVO_BA_SPLIT
-#define FVO_BA_SPLIT 1
-#endif
-  const int nh = (FVO_BA_SPLIT && nwin >= 8) ? (nwin + 1) / 2 : nwin;
+  const int nh = nwin >= 8 ? (nwin + 1) / 2 : nwin;
   const bool two = nh < nwin;
   if (two) {
     FVO_HIP(ctx, hipEventRecord(ctx->ba_fork, s));

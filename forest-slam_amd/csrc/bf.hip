@@ -8,7 +8,7 @@
 //   first index wins ties exactly like batchDistance(K=1).  Both directions in one
 //   launch (blockIdx.z).
 // k_bf_finish: mutual-nearest check + ordered compaction (ascending queryIdx).
-#include "fvo_internal.h"
+#include "fvo_device.h"
 
 namespace {
 

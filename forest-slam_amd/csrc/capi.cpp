@@ -318,6 +318,16 @@ int fvo_map_transform(fvo_ctx* c, const float* points, int32_t point_stride, con
                            (hipStream_t)stream);
 }
 
+int fvo_chain_poses(fvo_ctx* c, const double* T, const int32_t* status, const int32_t* n_points, int32_t n_seq,
+                    int32_t n, double* cum_state, double* cum_out, int32_t* n_points_out, fvo_stream stream) {
+  if (!c) return -1;
+  if (n_seq < 0 || n < 0) return fvo_fail(c, "n_seq and n must be >= 0");
+  if (n_seq == 0 || n == 0) return 0;
+  if (!T || !status || !cum_state || !cum_out) return fvo_fail(c, "null pointer argument");
+  if ((n_points == nullptr) != (n_points_out == nullptr)) return fvo_fail(c, "n_points and n_points_out: both or neither");
+  return chain_poses_run(c, T, status, n_points, n_seq, n, cum_state, cum_out, n_points_out, (hipStream_t)stream);
+}
+
 int64_t fvo_voxel_workspace_bytes(int64_t n_points) {
   if (n_points < 1 || n_points > INT32_MAX) return -1;
   return voxel_workspace_bytes(n_points);

@@ -18,7 +18,7 @@
 // Specification, operation by operation: oracle/essential_ref.cpp.  fp64, -ffp-contract=off.
 #include <cfloat>
 
-#include "fvo_internal.h"
+#include "fvo_device.h"
 #include "ransac.h"
 
 namespace {

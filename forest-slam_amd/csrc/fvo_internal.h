@@ -164,6 +164,8 @@ int motion_blur_run(fvo_ctx* ctx, const uint8_t* img, int batch, int64_t sstride
                     int64_t dstride, int dpitch, hipStream_t s);
 int map_transform_run(fvo_ctx* ctx, const float* pts, int stride, const int32_t* npts, int batch, int64_t cap,
                       const double* T, int32_t* count, int64_t map_cap, double* out64, float* out32, hipStream_t s);
+int chain_poses_run(fvo_ctx* ctx, const double* T, const int32_t* status, const int32_t* npts, int n_seq, int n,
+                    double* cum, double* cum_out, int32_t* npts_out, hipStream_t s);
 int64_t voxel_workspace_bytes(int64_t n);
 int voxel_run(fvo_ctx* ctx, const double* pts, int64_t n, double voxel, void* ws, size_t ws_bytes, double* out,
               int32_t* n_out, int32_t* status, hipStream_t s);
@@ -194,30 +196,4 @@ int fvo_alloc(fvo_ctx* ctx, T** p, size_t n) {
   if (e != hipSuccess) return fvo_fail(ctx, std::string("hipMalloc failed: ") + hipGetErrorString(e));
   ctx->ws_bytes += (int64_t)bytes;
   return 0;
-}
-
-// ---------------------------------------------------------------- device helpers
-__device__ __forceinline__ int wave_lane() { return (int)(threadIdx.x & 63); }
-
-// XCD-aware block order.  Dispatch sends linear block L to XCD L mod 8, so neighbouring
-// blocks (which read overlapping image rows / patches) would land in 8 different L2s; the
-// logical index returned here hands each XCD one contiguous eighth of the grid instead.
-struct XcdBlock {
-  int x, y, z;
-};
-__device__ __forceinline__ XcdBlock xcd_block() {
-  const int gx = gridDim.x, gy = gridDim.y;
-  const int N = gx * gy * gridDim.z;
-  const int L = (blockIdx.z * gy + blockIdx.y) * gx + blockIdx.x;
-  const int per = N >> 3;
-  const int lg = L < (per << 3) ? (L & 7) * per + (L >> 3) : L;
-  const int t = lg / gx;
-  return XcdBlock{lg - t * gx, t % gy, t / gy};
-}
-
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
 }

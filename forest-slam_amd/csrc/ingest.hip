@@ -7,7 +7,7 @@
 // (INTER_LINEAR, BORDER_CONSTANT 0) and the 14-bit BGR2GRAY, one 32-bit store.
 // HBM traffic per pixel: the 3 source bytes (the 2x2 gathers of neighbouring outputs hit
 // the same lines in L1/L2) + 1 output byte.  Specification: oracle/ingest_ref.cpp.
-#include "fvo_internal.h"
+#include "fvo_device.h"
 
 namespace {
 

@@ -10,6 +10,8 @@
 //   k_map_xform   thread per point: x' = ((T00 x + T01 y) + T02 z) + T03 in fp64 (no contraction;
 //                 numpy's dgemm order is unpinned), appended at the map's running count as
 //                 f64 xyz and/or the PointCloud2 float32 xyz record; HBM-bound (12 B in, 24+12 out).
+//   k_chain       the pose chain stereo_slam.py:306 on the device (fvo_chain_poses): the map's
+//                 placing poses without a host round trip.
 //   voxel_down_sample (Open3D PointCloud::VoxelDownSample): min bound by block partials, voxel
 //                 keys floor((p - (min - v/2)) / v) packed 3x21 bits, stable radix sort of
 //                 (key, index) (hipcub), segment heads + exclusive scan, then one thread per
@@ -19,7 +21,7 @@
 // Specification: oracle/map_ref.cpp.
 #include <hipcub/hipcub.hpp>
 
-#include "fvo_internal.h"
+#include "fvo_device.h"
 
 namespace {
 
@@ -31,10 +33,18 @@ __global__ __launch_bounds__(256) void k_map_xform(const float* __restrict__ pts
   const int b = blockIdx.y;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t n = min((int64_t)npts[b], cap);
+  if ((int64_t)blockIdx.x * 256 >= n) return;  // uniform: no point of set b in this block
+  // the set's offset in the map: one wave sums the counts of the sets before it
+  __shared__ int64_t s_base;
+  if (threadIdx.x < 64) {
+    int64_t part = 0;
+    for (int j = threadIdx.x; j < b; j += 64) part += min((int64_t)npts[j], cap);
+    part = wave_sum(part);
+    if (threadIdx.x == 0) s_base = count[0] + part;
+  }
+  __syncthreads();
   if (i >= n) return;
-  int64_t base = count[0];
-  for (int j = 0; j < b; ++j) base += min((int64_t)npts[j], cap);
-  const int64_t o = base + i;
+  const int64_t o = s_base + i;
   if (o >= map_cap) return;
   const float* p = pts + ((int64_t)b * cap + i) * stride;
   const double x = p[0], y = p[1], z = p[2];
@@ -59,6 +69,35 @@ __global__ void k_map_count(const int32_t* __restrict__ npts, int batch, int64_t
   int64_t t = count[0];
   for (int j = 0; j < batch; ++j) t += min((int64_t)npts[j], cap);
   count[0] = (int32_t)min(t, (int64_t)INT32_MAX);
+}
+
+// Pose chains (fvo_chain_poses): 16 lanes per sequence, lane (i, j) holds cum[i][j]; per frame
+// in order, c'_ij = ((c_i0 t_0j + c_i1 t_1j) + c_i2 t_2j) + c_i3 t_3j with the row of cum from the
+// sequence's lanes (stereo_slam.py:306, np.dot(cumulative, T)), applied when the frame is posed
+// (status >= 0: the reference chained it, :292).  Four sequences per wave; the serial chain is
+// ~n dependent 4-term dot products, a few microseconds per batch.
+__global__ __launch_bounds__(64) void k_chain(const double* __restrict__ T, const int32_t* __restrict__ status,
+                                              const int32_t* __restrict__ npts, int n_seq, int n,
+                                              double* __restrict__ cum, double* __restrict__ cum_out,
+                                              int32_t* __restrict__ npts_out) {
+  const int lane = threadIdx.x, sq = blockIdx.x * 4 + (lane >> 4), e = lane & 15, i = e >> 2, j = e & 3;
+  const bool live = sq < n_seq;
+  const int sqc = live ? sq : n_seq - 1;  // lanes past the last sequence mirror it and store nothing
+  const int row = (lane & ~15) + 4 * i;
+  double c = cum[(int64_t)sqc * 16 + e];
+  for (int f = 0; f < n; ++f) {
+    const int64_t k = (int64_t)sqc * n + f;
+    const int st = status[k];
+    const double* M = T + k * 16;
+    const double t0 = M[j], t1 = M[4 + j], t2 = M[8 + j], t3 = M[12 + j];
+    const double c0 = __shfl(c, row, 64), c1 = __shfl(c, row + 1, 64), c2 = __shfl(c, row + 2, 64),
+                 c3 = __shfl(c, row + 3, 64);
+    const double nc = ((c0 * t0 + c1 * t1) + c2 * t2) + c3 * t3;
+    if (st >= 0) c = nc;
+    if (live) cum_out[k * 16 + e] = c;
+    if (live && npts_out && e == 0) npts_out[k] = st >= 0 ? npts[k] : 0;
+  }
+  if (live) cum[(int64_t)sq * 16 + e] = c;
 }
 
 constexpr int kVxBlocks = 256;
@@ -204,6 +243,14 @@ int map_transform_run(fvo_ctx* ctx, const float* pts, int stride, const int32_t*
   });
   FVO_LAUNCH_CHECK(ctx);
   hipLaunchKernelGGL(k_map_count, dim3(1), dim3(64), 0, s, npts, batch, cap, count);
+  FVO_LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+int chain_poses_run(fvo_ctx* ctx, const double* T, const int32_t* status, const int32_t* npts, int n_seq, int n,
+                    double* cum, double* cum_out, int32_t* npts_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_chain, dim3((n_seq + 3) / 4), dim3(64), 0, s, T, status, npts, n_seq, n, cum, cum_out,
+                     npts_out);
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }

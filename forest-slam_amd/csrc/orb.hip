@@ -20,7 +20,7 @@
 #include <cmath>
 #include <cstring>
 
-#include "fvo_internal.h"
+#include "fvo_device.h"
 #include "orb_pattern.inc"
 
 namespace {
@@ -1216,7 +1216,8 @@ int orb_score_debug(fvo_ctx* ctx) {
     const OrbDev G = make_dev(g);
     const int ntiles = G.tile0[g.nlevels];
     hipLaunchKernelGGL(k_fast_nms<true>, dim3(ntiles, ctx->orb_last_batch), dim3(256), 0, 0, G, ctx->pyr, ctx->score,
-                       nullptr, g.total_px, ctx->cfg.fast_threshold, ctx->cfg.edge_threshold, ntiles);
+                       nullptr, g.total_px, std::min(std::max(ctx->cfg.fast_threshold, 0), 255),
+                       ctx->cfg.edge_threshold, ntiles);  // the threshold orb_run uses
     FVO_LAUNCH_CHECK(ctx);
   }
   FVO_HIP(ctx, hipDeviceSynchronize());

@@ -20,7 +20,7 @@
 #include <cstdlib>
 #include <type_traits>
 
-#include "fvo_internal.h"
+#include "fvo_device.h"
 #include "ransac.h"
 
 namespace {

@@ -33,7 +33,7 @@
 #include <cstdlib>
 #include <type_traits>
 
-#include "fvo_internal.h"
+#include "fvo_device.h"
 
 namespace {
 
@@ -206,11 +206,8 @@ __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q
 // row's image bytes are loaded right after the current row is staged and taken before the
 // row's C / V stores (vmcnt retires in order: a wait for them behind the stores would also
 // wait for the stores).  Integer arithmetic as oracle/sgbm_ref.cpp (order-independent sums).
-#ifndef FVO_SG_CW
-#define FVO_SG_CW 1
-#endif
 template <int D, int CB, int G>
-__global__ __launch_bounds__(G * CB, FVO_SG_CW) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
+__global__ __launch_bounds__(G * CB, 1) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
                                                     int64_t stride, int pitch, SgParams p, uint16_t* __restrict__ Vvol,
                                                     uint16_t* __restrict__ Mvol) {
   constexpr int DQ = D / G, PQ = DQ / 2, NV2 = DQ / 4;
@@ -494,18 +491,12 @@ __device__ __forceinline__ void derive16(const uint32_t* vp, const uint32_t* v, 
 // by an LDS atomicMin -- the serial rule "replace iff disp2cost > cost" of sgbm_ref.cpp (the
 // smallest cost wins, among equal costs the largest x1, the first one the scan visits).  The
 // pseudo left-right check then runs on the LDS row and writes the row-major raw disparity.
-#ifndef FVO_SG_EXP
-#define FVO_SG_EXP 0  // timing-only experiments: 1 = sweep 1 alone, 2 = sweep 2 alone
-#endif
-#ifndef FVO_SG_PD
-#define FVO_SG_PD 4
-#endif
 template <int D>
 __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t* __restrict__ Vvol,
                                                                  const uint16_t* __restrict__ Mvol, SgParams p,
                                                                  uint32_t* __restrict__ ckpt, int nck,
                                                                  int16_t* __restrict__ raw) {
-  constexpr int DQ = D / 16, PQ = DQ / 2, SEG = 8, PF = 8, PD = FVO_SG_PD;
+  constexpr int DQ = D / 16, PQ = DQ / 2, SEG = 8, PF = 8, PD = 4;  // PD: prefetch distance (measured 2/4/8)
   constexpr int CKW = PQ + 1 <= 4 ? 4 : 8;
   constexpr int XS = 2 * D;  // u32 words per column of a 4-row group
   constexpr int RK = sg_ring_keys(D), RS = sg_ring_raw(D);
@@ -643,15 +634,9 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
 #pragma unroll
     for (int kk = 0; kk < CKW; kk += 4) *reinterpret_cast<uint4*>(cp + kk) = make_uint4(v[kk], v[kk + 1], v[kk + 2], v[kk + 3]);
   };
-#if FVO_SG_EXP != 2
   block1(xs, std::true_type{});
 #pragma unroll 1
   for (int x0 = xs + SEG; x0 < W1; x0 += SEG) block1(x0, std::false_type{});
-#endif
-#if FVO_SG_EXP == 1
-  if (minPrev == 0x12345678u) raw[0] = 1;
-  return;
-#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the checkpoints, re-read below by the lanes that stored them
 
   // ---- sweep 2: segments s of reflected columns x' = SEG*s + i (x1 = W1-1-x'), right to left
@@ -924,6 +909,10 @@ int sgbm_init(fvo_ctx* ctx) {
   // must not wrap -- OpenCV's 16-bit CostType carries the same assumption
   if (49 * (2 * p.ftzero + 63) + p.P2 + p.P1 > 0xFFFF)
     return fvo_fail(ctx, "SGBM: P1/P2/preFilterCap too large for 16-bit path costs");
+  // the row pass sums S = L + R + V in u16 lanes and its WTA keys on S: each path is at most
+  // C + P2, so 3 (C + P2) must not wrap either
+  if (3 * (49 * (2 * p.ftzero + 63) + p.P2) > 0xFFFF)
+    return fvo_fail(ctx, "SGBM: P2/preFilterCap too large for the 16-bit aggregated cost");
   const int64_t B = c.sgbm_max_batch > 0 ? std::min(c.sgbm_max_batch, c.max_batch) : c.max_batch;
   const int64_t plane = (int64_t)p.width1 * p.D;
   int rc;

@@ -13,9 +13,9 @@
   ``frame_shard`` / ``gather_relative_poses``; ``run_sequence_sharded`` is the whole
   single-sequence run (bench.py --shard frames).
 * ``SequenceRank`` — one rank's step of the multi-sequence run (bench.py, tests): the
-  front-end step, the latest BA window's landmarks (``fvo_ba_landmarks``), the map
-  exchange (``exchange_window_map``) and the multi-sequence map built from it
-  (``GlobalMap``).
+  front-end step, then on a side stream the map exchange of the step's poses and every
+  frame's points3D (``exchange_frame_map``) and the multi-sequence map built from it on the
+  device (``GlobalMap``: ``fvo_chain_poses`` + ``fvo_map_transform``).
 * Keyframe exchange for the multi-sequence map: ``allgather_keyframes`` (poses + landmark
   positions, tens of KB: latency-bound, one collective per window step).
 
@@ -73,29 +73,40 @@ def gather_relative_poses(T_local: torch.Tensor, status_local: torch.Tensor, n_p
 
 
 def run_sequence_sharded(make_frontend, L_all: torch.Tensor, R_all: torch.Tensor, stamps=None, use_ba: bool = True,
-                         group=None):
+                         group=None, first_image: int = 0, n_pairs: int | None = None):
     """One sequence split over the ranks by frame pairs (the strong-scaling
-    path): rank r runs the pairs frame_shard(n-1, r, world) on its own front end
+    path): rank r runs the pairs frame_shard(n_pairs, r, world) on its own front end
     (``make_frontend()``), starting K-1 pairs early when local BA is on (``frame_shard(...,
     halo=K-1)``, so every owned pair's BA window spans the same K frames as on one GPU) and
     dropping those warm-up results; the relative poses and statuses are all-gathered
     (``gather_relative_poses``) and every rank composes the chain left to right in float64
     (stereo_slam.py:306, ``eval.chain``).  Returns what ``vo.run_sequence`` returns on one
-    GPU for the whole sequence: (TUM rows, relative T, statuses) -- bit-identical to it."""
+    GPU for the whole sequence: (TUM rows, relative T, statuses) -- bit-identical to it.
+
+    ``L_all[i - first_image]`` is image i: a rank may hold only the images its shard reads
+    (images s-1 .. e-1 of its halo'd shard), with ``n_pairs`` the whole sequence's pair count
+    (default: every image is held, n_pairs = len(L_all) - 1)."""
     from . import eval as ev
     from .vo import _check_overflow
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    n_pairs = L_all.shape[0] - 1
+    if n_pairs is None:
+        if first_image:
+            raise ValueError("n_pairs is required when L_all starts past image 0")
+        n_pairs = L_all.shape[0] - 1
     fe = make_frontend()
     halo = fe.ba_window - 1 if (fe.ba_window and use_ba) else 0
     s, e = frame_shard(n_pairs, rank, world, halo=halo)
+    if e > s and (s - 1 < first_image or e - 1 - first_image >= L_all.shape[0]):
+        raise ValueError(f"rank {rank} needs images {s - 1}..{e - 1}, holds {first_image}.."
+                         f"{first_image + L_all.shape[0] - 1}")
     drop = warmup_pairs(n_pairs, rank, world, halo)
     Ts, sts = [], []
     if e > s:
-        fe.prime(L_all[s - 1], R_all[s - 1])
+        o = first_image
+        fe.prime(L_all[s - 1 - o], R_all[s - 1 - o])
         for a in range(s, e, fe.B):
             b = min(a + fe.B, e)
-            T, st = fe.step(L_all[a:b], R_all[a:b])
+            T, st = fe.step(L_all[a - o:b - o], R_all[a - o:b - o])
             Ts.append((T if use_ba else fe.T[:b - a]).clone())
             sts.append(st.clone())
     dev = L_all.device
@@ -110,133 +121,114 @@ def run_sequence_sharded(make_frontend, L_all: torch.Tensor, R_all: torch.Tensor
     return ev.tum_rows(np.asarray(stamps)[1:][valid], cum), T, S
 
 
-def exchange_window_map(T_step: torch.Tensor, st_step: torch.Tensor, lm_xyz: torch.Tensor, lm_count: torch.Tensor,
-                        group=None):
+def exchange_frame_map(T_step: torch.Tensor, st_step: torch.Tensor, P3: torch.Tensor, n_points: torch.Tensor,
+                       group=None):
     """The per-step map exchange of the multi-sequence run: every rank's
-    BA-refined relative poses of the step (f64 [B,4,4]) with their statuses (i32 [B]) and its
-    latest window's landmarks (f64 [Lmax,3] + i32 [1] count, fixed size) are all-gathered over
-    RCCL.  Fixed shapes and device-side counts: no host synchronisation, the collectives queue
-    behind the step's kernels.  Returns (T [world,B,4,4], st [world,B], xyz [world,Lmax,3],
-    counts [world,1]) on the inputs' device.  Under the gloo backend (CPU tests, or GPU ranks
-    sharing one card) the tensors go through host copies."""
+    relative poses of the step (f64 [B,4,4], BA-refined with local BA), their statuses (i32 [B])
+    and every frame's points3D (the back-projected, depth-filtered points PnP consumed: f32
+    [B,cap,3] + i32 [B] counts, stereo_slam.py:274-289) are all-gathered (RCCL over xGMI).
+    Fixed shapes and device-side counts: no host synchronisation, the collectives queue on the
+    current stream.  Returns (T [world,B,4,4], st [world,B], P3 [world,B,cap,3], n [world,B])
+    on the inputs' device.  Under the gloo backend (CPU tests, or GPU ranks sharing one card)
+    the tensors go through host copies."""
     world = dist.get_world_size(group)
     host = dist.get_backend(group) == "gloo" and T_step.is_cuda
     dev = T_step.device
-    ins = [t.contiguous().cpu() if host else t.contiguous() for t in (T_step, st_step, lm_xyz, lm_count)]
+    ins = [t.contiguous().cpu() if host else t.contiguous() for t in (T_step, st_step, P3, n_points)]
     outs = []
     for t in ins:
-        o = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(o, t, group=group)
-        outs.append(torch.stack(o).to(dev) if host else torch.stack(o))
+        o = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather(list(o.unbind(0)), t, group=group)
+        outs.append(o.to(dev) if host else o)
     return tuple(outs)
 
 
-class MapChain:
-    """Host side of ``GlobalMap``: per rank the chain of the gathered relative poses, composed
-    left to right in float64 exactly as ``eval.chain`` (frames with status -1 or keypoint
-    overflow keep the previous pose, stereo_slam.py:292,306), and the pose that places a
-    step's landmarks.  A step's last BA window ends at frame e and starts at
-    s = max(0, e-K+1) (frame 0 = the primed pair); its landmarks are in camera-s
-    coordinates, and the reference maps points of camera f-1 with the chain through frame f
-    (pair f's points are back-projected from the previous image and transformed by the
-    cumulative pose that already includes T_f, stereo_slam.py:306-310), so they are placed
-    with the chain through s+1."""
-
-    def __init__(self, world: int, window: int):
-        self.world, self.K = int(world), int(window)
-        self.cums = [[np.eye(4)] for _ in range(self.world)]  # cums[r][f]: rank r's chain through frame f
-
-    def advance(self, T: np.ndarray, S: np.ndarray) -> np.ndarray:
-        """T f64 [world,n,4,4], S i32 [world,n] of one step -> landmark poses f64 [world,4,4]."""
-        from .vo import STATUS_KP_OVERFLOW
-        land = []
-        for r in range(self.world):
-            ch = self.cums[r]
-            for i in range(T.shape[1]):
-                ok = S[r, i] != -1 and S[r, i] != STATUS_KP_OVERFLOW
-                ch.append(np.dot(ch[-1], T[r, i]) if ok else ch[-1].copy())
-            e = len(ch) - 1
-            s = max(0, e - self.K + 1)
-            land.append(ch[min(s + 1, e)])
-        return np.stack(land)
-
-
 class GlobalMap:
-    """The multi-sequence map product built from ``exchange_window_map``'s
-    output: every rank's latest-window landmarks placed in its sequence's map frame
-    (``MapChain``) and appended to one ``mapping.PointMap`` -- the reference's
-    ``all_points_3D`` (stereo_slam.py:306-318) for all ranks' sequences at once, one
-    fvo_map_transform launch per step with the ranks' sets in rank order.
+    """The multi-sequence map product built from ``exchange_frame_map``'s
+    output, entirely on the device: per sequence the chain of its relative poses
+    (``fvo_chain_poses``: cum = cum @ T for every posed frame, stereo_slam.py:292-306) and every
+    posed frame's points3D transformed by its cumulative pose and appended to one
+    ``mapping.PointMap`` (``fvo_map_transform``) -- the reference's ``all_points_3D``
+    (stereo_slam.py:308-318) for all ranks' sequences at once, frame-major within a rank and
+    the ranks in rank order per step.  No host synchronisation: ``place`` only queues kernels
+    on the current stream."""
 
-    The gathered poses reach the host through pinned buffers copied asynchronously; a step
-    is placed ``lag`` steps later (its copy has long finished), so building the map never
-    stalls the rank's stream.  ``flush`` places what is still queued."""
-
-    def __init__(self, world: int, window: int, capacity: int, device, ctx=None, lag: int = 1):
+    def __init__(self, world: int, capacity: int, device, ctx=None):
         from .mapping import PointMap
-        self.lag = int(lag)
-        self.chain = MapChain(world, window)
+        self.world = int(world)
         self.map = PointMap(capacity, device, ctx)
-        self.counts = []  # per placed step: i32 [world] device landmark counts (test / report)
-        self.queue = []
+        self.ctx = self.map.ctx
+        self.cum = torch.eye(4, dtype=torch.float64, device=self.map.dev).repeat(self.world, 1, 1).contiguous()
+        self.steps = 0
 
-    def push(self, gathered, n: int):
-        Tg, Sg, Xg, Cg = gathered
-        hT = torch.empty(Tg[:, :n].shape, dtype=torch.float64, pin_memory=True)
-        hS = torch.empty(Sg[:, :n].shape, dtype=torch.int32, pin_memory=True)
-        hT.copy_(Tg[:, :n], non_blocking=True)
-        hS.copy_(Sg[:, :n], non_blocking=True)
-        X32 = Xg.to(torch.float32)  # PointCloud2 / fvo_map_transform take float32 xyz
-        cnt = Cg.reshape(-1).to(torch.int32).clone()
-        ev = torch.cuda.current_stream(Tg.device).record_event() if Tg.is_cuda else None
-        self.queue.append((ev, hT, hS, X32, cnt, int(n)))
-        while len(self.queue) > self.lag:
-            self._place(self.queue.pop(0))
+    def place(self, gathered):
+        Tg, Sg, Pg, Ng = gathered
+        S, n = Tg.shape[0], Tg.shape[1]
+        cum, n_eff = self.ctx.chain_poses(Tg.contiguous(), Sg.contiguous(), self.cum, n_points=Ng.contiguous())
+        self.map.add_frames(Pg.reshape(S * n, Pg.shape[2], Pg.shape[3]), n_eff.reshape(-1), cum.reshape(S * n, 4, 4))
+        self.steps += 1
 
     def flush(self):
-        while self.queue:
-            self._place(self.queue.pop(0))
+        """The map (pending kernels are on the stream ``place`` ran on: synchronise it before
+        reading on the host)."""
         return self.map
-
-    def _place(self, item):
-        ev, hT, hS, X32, cnt, n = item
-        if ev is not None:
-            ev.synchronize()
-        land = self.chain.advance(hT.numpy(), hS.numpy())
-        self.map.add_frames(X32, cnt, land)
-        self.counts.append(cnt)
 
 
 class SequenceRank:
     """One rank of the sequence-per-GPU run: ``step`` = the front end's step over the rank's
-    next frames, then the exchange of the refined poses and of the latest BA window's
-    landmarks with every other rank (``exchange_window_map``; skipped for world size 1 or
-    without local BA) and, with ``map_capacity`` > 0, their placement in the multi-sequence
-    map (``GlobalMap``; ``self.gmap``).  Returns (T, status, gathered) with gathered = None or
-    the (T, st, xyz, counts) all-gather result."""
+    next frames, then, when the exchange is on (a process group of more than one rank, or
+    ``exchange=True``), the exchange of the step's relative poses, statuses and points3D with
+    every rank (``exchange_frame_map``) and, with ``map_capacity`` > 0, their placement in the
+    multi-sequence map (``GlobalMap``; ``self.gmap``).
 
-    def __init__(self, frontend, group=None, map_capacity: int = 0):
+    The exchange and the map run on their own stream behind the step's kernels: the host does
+    not wait for them (nor for the step), and the next step's back stage only waits for the
+    copy of this step's poses and points into the send buffers.  Returns (T, status, gathered)
+    with gathered = None or the (T, st, P3, n) all-gather result, valid on ``self.stream``
+    (synchronise it, or the device, before reading it on the host)."""
+
+    def __init__(self, frontend, group=None, map_capacity: int = 0, exchange: bool | None = None):
         self.fe = frontend
         self.group = group
-        self.exchange = (dist.is_available() and dist.is_initialized() and frontend.ba_window > 0
-                         and dist.get_world_size(group) > 1)
+        if exchange is None:
+            exchange = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.exchange = bool(exchange)
         self.gmap = None
+        self.copied = None
         if self.exchange:
-            dev = frontend.dev
-            self.lm_out = (torch.empty((int(frontend.ctx.cfg.ba_max_landmarks), 3), dtype=torch.float64, device=dev),
-                           torch.empty((1,), dtype=torch.int32, device=dev))
+            dev, B, cap = frontend.dev, frontend.B, frontend.cap
+            self.world = dist.get_world_size(group)
+            self.stream = torch.cuda.Stream(dev)
+            e = lambda shape, dt: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
+            self.sT, self.sS = e((B, 4, 4), torch.float64), e((B,), torch.int32)
+            self.sP, self.sN = e((B, cap, 3), torch.float32), e((B,), torch.int32)
             if map_capacity > 0:
-                self.gmap = GlobalMap(dist.get_world_size(group), frontend.ba_window, map_capacity, dev,
-                                      ctx=frontend.ctx)
+                self.gmap = GlobalMap(self.world, map_capacity, dev, ctx=frontend.ctx)
 
     def step(self, L: torch.Tensor, R: torch.Tensor):
-        T, st = self.fe.step(L, R)
-        gathered = None
-        if self.exchange:
-            xyz, cnt = self.fe.ctx.ba_landmarks(L.shape[0] - 1, out=self.lm_out)
-            gathered = exchange_window_map(T, st, xyz, cnt, self.group)
+        fe = self.fe
+        dev = fe.dev
+        main = torch.cuda.current_stream(dev)
+        if self.copied is not None:  # the previous step's send copies read T / P3 before they are rewritten
+            main.wait_event(self.copied)
+        T, st = fe.step(L, R)
+        if not self.exchange:
+            return T, st, None
+        n = L.shape[0]
+        self.stream.wait_stream(main)
+        with torch.cuda.stream(self.stream):
+            # fixed-size send buffers: frames past n are padding (status -2: not posed, 0 points)
+            self.sT[:n].copy_(T)
+            self.sS[:n].copy_(st)
+            self.sP[:n].copy_(fe.P3[:n])
+            self.sN[:n].copy_(fe.npts[:n])
+            if n < fe.B:
+                self.sS[n:].fill_(-2)
+                self.sN[n:].zero_()
+            self.copied = self.stream.record_event()
+            gathered = exchange_frame_map(self.sT, self.sS, self.sP, self.sN, self.group)
             if self.gmap is not None:
-                self.gmap.push(gathered, L.shape[0])
+                self.gmap.place(gathered)
         return T, st, gathered
 
 

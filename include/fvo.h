@@ -28,6 +28,8 @@
  *   fvo_motion_blur         <- apply_random_motion_blur(img, blur_percentage, kernel_size, angle=0)
  *                              (cv2.getRotationMatrix2D + warpAffine + filter2D + np.where)
  *                              forest_slam_ros/src/stereo_slam.py:142-178, :194, :206
+ *   fvo_chain_poses         <- cumulative_est_tf_mat = np.dot(cumulative_est_tf_mat, T) per posed frame
+ *                              (the len(points3D) >= 6 guard), stereo_slam.py:292, :306 — on the device
  *   fvo_map_transform       <- (cum @ hstack(points3D, 1).T)[:3].T appended to the map + PointCloud2
  *                              float32 packing: stereo_slam.py:308-318; mono_slam.py:148; gt_mapping.py
  *   fvo_voxel_down_sample   <- open3d PointCloud.voxel_down_sample(voxel_size=0.5)
@@ -55,7 +57,7 @@
 extern "C" {
 #endif
 
-#define FVO_ABI_VERSION 4
+#define FVO_ABI_VERSION 5
 
 typedef struct fvo_ctx fvo_ctx;
 typedef void* fvo_stream; /* hipStream_t */
@@ -270,6 +272,21 @@ int fvo_map_transform(fvo_ctx* ctx, const float* points, int32_t point_stride, c
  * voxel index (x, then y, then z — Open3D's hash-map order is unspecified), *n_out (device).
  * workspace: device scratch of fvo_voxel_workspace_bytes(n_points) bytes (caller-owned).
  * status (device, may be NULL): 0 ok, 1 = a voxel index outside [0, 2^21) (result invalid). */
+/* Pose chains of n_seq sequences advanced over one batch of n frames each (any stage; no
+ * workspace) — stereo_slam.py:292-306 on the device, for the map of every posed frame:
+ * for s < n_seq, i < n in order, a frame is posed when status[s*n + i] >= 0 (pose valid, or
+ * RANSAC failure with its identity T; -1 = the len(points3D) >= 6 skip, other negatives =
+ * padding / overflow: not posed).  A posed frame advances cum[s] = cum[s] @ T[s*n + i] (fp64,
+ * C_ij = ((c_i0 t_0j + c_i1 t_1j) + c_i2 t_2j) + c_i3 t_3j, no contraction — NumPy's BLAS order
+ * is unpinned, <= 1 ulp).  Outputs: cum_out[s*n + i] = cum[s] after frame i, n_points_out[s*n + i]
+ * = n_points[s*n + i] for posed frames, 0 otherwise (so fvo_map_transform(points, n_points_out,
+ * cum_out) appends exactly the posed frames' points3D, stereo_slam.py:308-314).
+ * cum_state: [n_seq][16] fp64 row-major, read and advanced in place (identity at a sequence's
+ * start).  T, cum_out: [n_seq*n][16] fp64; status, n_points, n_points_out: [n_seq*n] int32.
+ * n_points may be NULL (n_points_out then NULL too). */
+int fvo_chain_poses(fvo_ctx* ctx, const double* T, const int32_t* status, const int32_t* n_points, int32_t n_seq,
+                    int32_t n, double* cum_state, double* cum_out, int32_t* n_points_out, fvo_stream stream);
+
 int64_t fvo_voxel_workspace_bytes(int64_t n_points);
 int fvo_voxel_down_sample(fvo_ctx* ctx, const double* points, int64_t n_points, double voxel_size, void* workspace,
                           int64_t workspace_bytes, double* out, int32_t* n_out, int32_t* status, fvo_stream stream);

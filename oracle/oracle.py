@@ -21,7 +21,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "liboracle.so")
+# FVO_ORACLE_LIB: the sanitizer build (oracle/Makefile.asan, tools/sanitize.sh)
+_LIB = os.environ.get("FVO_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 _lib = None
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)

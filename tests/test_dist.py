@@ -31,12 +31,12 @@ def _worker(rank, world, port, n_pairs, out):
     s, e = fd.frame_shard(n_pairs, rank, world)
     T, S = fd.gather_relative_poses(torch.from_numpy(allT[s - 1:e - 1]), torch.from_numpy(allS[s - 1:e - 1]), n_pairs)
     poses, lms = fd.allgather_keyframes(torch.full((10, 7), float(rank)), torch.ones((rank + 2, 3)) * rank)
-    Tw, Sw, Xw, Cw = fd.exchange_window_map(torch.full((4, 4, 4), float(rank), dtype=torch.float64),
-                                            torch.full((4,), rank - 1, dtype=torch.int32),
-                                            torch.full((16, 3), 10.0 + rank, dtype=torch.float64),
-                                        torch.tensor([rank + 5], dtype=torch.int32))
+    Tw, Sw, Pw, Nw = fd.exchange_frame_map(torch.full((4, 4, 4), float(rank), dtype=torch.float64),
+                                           torch.full((4,), rank - 1, dtype=torch.int32),
+                                           torch.full((4, 16, 3), 10.0 + rank, dtype=torch.float32),
+                                           torch.tensor([rank + 5, 1, 2, 3], dtype=torch.int32))
     out[rank] = (T, S, [p[0, 0].item() for p in poses], [l.shape[0] for l in lms],
-                 (Tw[:, 0, 0, 0].tolist(), Xw[:, 0, 0].tolist(), Cw[:, 0].tolist(), Sw[:, 3].tolist()))
+                 (Tw[:, 0, 0, 0].tolist(), Pw[:, 0, 0, 0].tolist(), Nw[:, 0].tolist(), Sw[:, 3].tolist()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -69,35 +69,3 @@ def test_gather_poses_two_ranks_gloo():
         assert kf == [0.0, 1.0] and nl == [2, 3]
         # chaining the gathered poses equals the single-process chain exactly
         assert np.array_equal(ev.chain(T, S != -1), ev.chain(allT, S != -1))
-
-
-def test_map_chain_places_landmarks_with_the_reference_chain():
-    """dist.MapChain (GlobalMap's host side): per rank the gathered relative poses chained as
-    eval.chain does (status -1 / overflow frames keep the pose), and each step's landmarks
-    placed with the chain through s+1, s = the first frame of the step's last BA window."""
-    from forest_slam_amd import dist as fd
-    from forest_slam_amd import eval as ev
-    rng = np.random.default_rng(5)
-    world, K, B, steps = 3, 4, 3, 4
-    T = np.tile(np.eye(4), (world, B * steps, 1, 1))
-    T[..., :3, 3] = rng.normal(0, 0.3, (world, B * steps, 3))
-    S = np.ones((world, B * steps), np.int32)
-    S[1, 4] = -1
-    S[2, 7] = -3
-    mc = fd.MapChain(world, K)
-    got = [mc.advance(T[:, k * B:(k + 1) * B], S[:, k * B:(k + 1) * B]) for k in range(steps)]
-    for r in range(world):
-        valid = (S[r] != -1) & (S[r] != -3)
-        cum = ev.chain(T[r], valid)  # TUM chain: the poses of the valid frames
-        full = [np.eye(4)]
-        j = 0
-        for f in range(B * steps):
-            if valid[f]:
-                full.append(cum[j])
-                j += 1
-            else:
-                full.append(full[-1])
-        for k in range(steps):
-            e = (k + 1) * B
-            s = max(0, e - K + 1)
-            assert np.array_equal(got[k][r], full[s + 1]), (r, k)

@@ -1,5 +1,6 @@
 """Front-end behaviour on the GPU: keypoint-capacity overflow reporting, frame-pair sharding
-with local BA (K-1 halo), and the multi-rank step (two ranks sharing one card, gloo)."""
+with local BA (K-1 halo), and the multi-rank step (two ranks sharing one card over gloo; one
+rank over RCCL for the no-host-sync check)."""
 import os
 import socket
 
@@ -95,17 +96,18 @@ def _rank_worker(rank, world, port, out):
     fe = _fe(seq, 3, ba_window=3)
     sr = fd.SequenceRank(fe, map_capacity=40000)
     assert sr.exchange and sr.gmap is not None
-    local = fd.GlobalMap(1, 3, 40000, "cuda:0", ctx=fe.ctx)  # this rank's own map, built without the exchange
+    local = fd.GlobalMap(1, 40000, "cuda:0", ctx=fe.ctx)  # this rank's own map, built without the exchange
     fe.prime(L[0], R[0])
     res = []
     for s in (1, 4):
-        T, st, (Tg, Sg, Xg, Cg) = sr.step(L[s:s + 3], R[s:s + 3])
-        xyz, cnt = fe.ctx.ba_landmarks(2)
-        local.push((T[None], st[None], xyz[None], cnt[None]), 3)
+        T, st, (Tg, Sg, Pg, Ng) = sr.step(L[s:s + 3], R[s:s + 3])
         torch.cuda.synchronize()
-        c = int(cnt.item())
-        res.append(dict(T=T.cpu().numpy(), st=st.cpu().numpy(), xyz=xyz[:c].cpu().numpy(), Tg=Tg.cpu().numpy(),
-                        Sg=Sg.cpu().numpy(), Xg=Xg.cpu().numpy(), Cg=Cg.cpu().numpy()))
+        mine = (T.clone()[None], st.clone()[None], fe.P3[:3].clone()[None], fe.npts[:3].clone()[None])
+        local.place(mine)
+        torch.cuda.synchronize()
+        res.append(dict(T=mine[0][0].cpu().numpy(), st=mine[1][0].cpu().numpy(), P=mine[2][0].cpu().numpy(),
+                        N=mine[3][0].cpu().numpy(), Tg=Tg.cpu().numpy(), Sg=Sg.cpu().numpy(), Pg=Pg.cpu().numpy(),
+                        Ng=Ng.cpu().numpy()))
     g, lo = sr.gmap.flush(), local.flush()
     torch.cuda.synchronize()
     out[rank] = dict(steps=res, gmap=g.cloud64(), gmap32=g.cloud32(), local=lo.cloud64(), local32=lo.cloud32())
@@ -113,13 +115,33 @@ def _rank_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_two_ranks_exchange_window_maps():
-    """the bench's multi-rank step (dist.SequenceRank:
-    front-end step -> fvo_ba_landmarks -> exchange_window_map -> GlobalMap) with two ranks on
-    the box's one GPU (gloo exchanging host copies).  Each rank's gathered poses / statuses /
-    landmarks equal what the other rank computed; both ranks hold byte-identical global maps,
-    equal to the union (step by step, in rank order) of the maps each rank builds from its
-    own poses and landmarks alone (stereo_slam.py:306-318 per sequence)."""
+def _map_ref(steps):
+    """One rank's map restated on the host: every posed frame's (status >= 0) points3D
+    transformed by its cumulative pose (stereo_slam.py:292-314), in fvo_chain_poses' /
+    fvo_map_transform's summation order (no contraction)."""
+    c = np.eye(4)
+    segs = []
+    for stp in steps:
+        for f in range(len(stp["st"])):
+            if stp["st"][f] < 0:
+                continue
+            t = stp["T"][f]
+            c = np.array([[((c[i, 0] * t[0, j] + c[i, 1] * t[1, j]) + c[i, 2] * t[2, j]) + c[i, 3] * t[3, j]
+                           for j in range(4)] for i in range(4)])
+            P = stp["P"][f][:stp["N"][f]].astype(np.float64)
+            x, y, z = P[:, 0], P[:, 1], P[:, 2]
+            segs.append(np.stack([((c[k, 0] * x + c[k, 1] * y) + c[k, 2] * z) + c[k, 3] for k in range(3)], axis=1))
+    return segs
+
+
+def test_two_ranks_exchange_frame_maps():
+    """the bench's multi-rank step (dist.SequenceRank: front-end step ->
+    exchange_frame_map of the step's poses, statuses and points3D -> GlobalMap on the device)
+    with two ranks on the box's one GPU (gloo exchanging host copies).  Each rank's gathered
+    poses / statuses / points equal what the other rank computed; both ranks hold byte-identical
+    global maps, equal to the union (step by step, in rank order) of the maps each rank builds
+    from its own step data alone, and holding EVERY posed frame's points3D placed with the
+    chained poses (stereo_slam.py:306-318, restated on the host)."""
     import torch.multiprocessing as mp
     mgr = mp.Manager()
     out = mgr.dict()
@@ -130,21 +152,62 @@ def test_two_ranks_exchange_window_maps():
             for o in range(2):
                 mine = out[o]["steps"][step]
                 assert np.array_equal(g["Tg"][o], mine["T"]) and np.array_equal(g["Sg"][o], mine["st"])
-                c = int(g["Cg"][o][0])
-                assert c == len(mine["xyz"]) and c > 0
-                assert np.array_equal(g["Xg"][o][:c], mine["xyz"])
+                assert np.array_equal(g["Ng"][o], mine["N"]) and (mine["N"] > 0).any()
+                for f in range(len(mine["N"])):
+                    assert np.array_equal(g["Pg"][o][f][:mine["N"][f]], mine["P"][f][:mine["N"][f]])
     assert np.array_equal(out[0]["gmap"], out[1]["gmap"]) and np.array_equal(out[0]["gmap32"], out[1]["gmap32"])
     # union of the local maps: step-major, rank-minor segments
     segs, segs32, pos = [], [], [0, 0]
     for step in range(2):
         for r in range(2):
-            c = len(out[r]["steps"][step]["xyz"])
+            st = out[r]["steps"][step]
+            c = int(st["N"][st["st"] >= 0].sum())
             segs.append(out[r]["local"][pos[r]:pos[r] + c])
             segs32.append(out[r]["local32"][pos[r]:pos[r] + c])
             pos[r] += c
     assert pos == [len(out[0]["local"]), len(out[1]["local"])]
     assert np.array_equal(out[0]["gmap"], np.concatenate(segs))
     assert np.array_equal(out[0]["gmap32"], np.concatenate(segs32))
+    # every posed frame of every rank, placed by the reference chain
+    for r in range(2):
+        ref = np.concatenate(_map_ref(out[r]["steps"]))
+        assert np.array_equal(out[r]["local"], ref)
+
+
+def test_sequence_rank_step_does_not_wait_for_the_gpu():
+    """SequenceRank.step with the map exchange on (RCCL, a one-rank group on
+    the box's GPU) queues the front-end step, the all-gather and the device-side map placement
+    and returns without host synchronisation: with ~0.5 s of spinning queued on the caller's
+    stream ahead of it, step() returns well before the spin ends; the map then holds every
+    posed frame's points3D (stereo_slam.py:306-318)."""
+    import time
+
+    import torch.distributed as dist
+    from forest_slam_amd import dist as fd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        seq, L, R = _frames(41, 7, start=30)
+        fe = _fe(seq, 3, ba_window=3, overlap_sgbm=True)
+        sr = fd.SequenceRank(fe, map_capacity=40000, exchange=True)
+        fe.prime(L[0], R[0])
+        T, st, _ = sr.step(L[1:4], R[1:4])  # warm-up: the communicator is created on first use
+        torch.cuda.synchronize()
+        steps = [dict(T=T.cpu().numpy().copy(), st=st.cpu().numpy().copy(), P=fe.P3[:3].cpu().numpy().copy(),
+                      N=fe.npts[:3].cpu().numpy().copy())]
+        torch.cuda._sleep(1_000_000_000)  # ~0.5 s of spinning on the caller's stream
+        t0 = time.perf_counter()
+        T, st, _ = sr.step(L[4:7], R[4:7])
+        dt = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        spun = time.perf_counter() - t0
+        assert spun > 0.2 and dt < 0.5 * spun, (dt, spun)
+        steps.append(dict(T=T.cpu().numpy(), st=st.cpu().numpy(), P=fe.P3[:3].cpu().numpy(),
+                          N=fe.npts[:3].cpu().numpy()))
+        assert np.array_equal(sr.gmap.flush().cloud64(), np.concatenate(_map_ref(steps)))
+    finally:
+        dist.destroy_process_group()
 
 
 def test_frontend_step_captured_in_hip_graph_replays_bit_identically():

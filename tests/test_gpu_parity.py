@@ -307,8 +307,13 @@ def test_orb_rejects_edge_threshold_below_half_patch():
 def test_sgbm_rejects_path_costs_that_wrap_u16():
     """The path step folds min(a + P1, b + P1) into min(a, b) + P1, exact only while the largest
     path value (49 x the largest BT pixel cost + P2) plus P1 stays below 2^16: a context whose
-    P1 / P2 / preFilterCap break that is refused at creation (csrc/sgbm.hip sgbm_init)."""
+    P1 / P2 / preFilterCap break that is refused at creation (csrc/sgbm.hip sgbm_init).  So is
+    one whose aggregated cost S = L + R + V (the WTA key, at most 3 x (49 x 93 + P2)) could
+    wrap, e.g. P2 = 20000."""
     from forest_slam_amd import _lib
     with pytest.raises(RuntimeError, match="fvo_create"):
         _lib.Context(320, 200, P2=62000, stages=_lib.STAGE_SGBM)  # 49 (2*15 + 63) + 62000 + 392 > 65535
+    with pytest.raises(RuntimeError, match="fvo_create"):
+        _lib.Context(320, 200, P2=20000, stages=_lib.STAGE_SGBM)  # 3 (49 (2*15 + 63) + 20000) > 65535
     _lib.Context(320, 200, P2=1568, stages=_lib.STAGE_SGBM).close()
+    _lib.Context(320, 200, P2=17000, stages=_lib.STAGE_SGBM).close()  # 3 (4557 + 17000) = 64671

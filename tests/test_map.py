@@ -153,3 +153,54 @@ def test_gpu_point_map_overflow_is_reported():
     with pytest.raises(RuntimeError, match="overflow"):
         pm.add_frames(P, torch.tensor([80], dtype=torch.int32, device="cuda"), T, check=True)
     assert pm.overflowed()
+
+
+def _chain_ref(T, S, N, cum0):
+    """stereo_slam.py:292-306 restated per sequence: cum = cum @ T for posed frames
+    (status >= 0), summed over k ascending without contraction (fvo_chain_poses' order)."""
+    cum = cum0.copy()
+    out = np.zeros_like(T)
+    nout = np.zeros_like(N)
+    for s in range(T.shape[0]):
+        c = cum[s]
+        for f in range(T.shape[1]):
+            if S[s, f] >= 0:
+                t = T[s, f]
+                c = np.array([[((c[i, 0] * t[0, j] + c[i, 1] * t[1, j]) + c[i, 2] * t[2, j]) + c[i, 3] * t[3, j]
+                               for j in range(4)] for i in range(4)])
+                nout[s, f] = N[s, f]
+            out[s, f] = c
+        cum[s] = c
+    return out, nout, cum
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_chain_poses_matches_reference_chain():
+    """fvo_chain_poses (the multi-sequence map's placing poses on the device): per sequence
+    cum = cum @ T for every posed frame (status >= 0; -1 = the < 6 points skip, -2 padding, -3
+    overflow leave it unchanged), carried across calls; equal to the ascending-k restatement bit
+    for bit and to eval.chain's np.dot chain within 1e-12; points of unposed frames zeroed."""
+    from forest_slam_amd import _lib
+    from forest_slam_amd import eval as ev
+    rng = np.random.default_rng(9)
+    S_, n = 5, 7
+    T = np.stack([[_pose(100 * s + f) for f in range(2 * n)] for s in range(S_)])
+    T[..., :3, 3] *= 0.01
+    St = rng.choice([1, 1, 1, 0, -1, -2, -3], size=(S_, 2 * n)).astype(np.int32)
+    N = rng.integers(0, 900, size=(S_, 2 * n)).astype(np.int32)
+    ctx = _lib.Context(64, 64, max_batch=1, stages=_lib.STAGE_BF, kp_capacity=64, device="cuda:0")
+    cum = torch.eye(4, dtype=torch.float64, device="cuda:0").repeat(S_, 1, 1).contiguous()
+    ref_cum = np.tile(np.eye(4), (S_, 1, 1))
+    for h in range(2):  # two calls: the chain carries over
+        sl = slice(h * n, (h + 1) * n)
+        dT = torch.from_numpy(np.ascontiguousarray(T[:, sl])).cuda()
+        got, gn = ctx.chain_poses(dT, torch.from_numpy(np.ascontiguousarray(St[:, sl])).cuda(), cum,
+                                  n_points=torch.from_numpy(np.ascontiguousarray(N[:, sl])).cuda())
+        want, wn, ref_cum = _chain_ref(T[:, sl], St[:, sl], N[:, sl], ref_cum)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy(), want) and np.array_equal(gn.cpu().numpy(), wn)
+    assert np.array_equal(cum.cpu().numpy(), ref_cum)
+    for s in range(S_):
+        posed = St[s] >= 0
+        assert np.allclose(ev.chain(T[s], posed)[-1], ref_cum[s], rtol=0, atol=1e-12)
