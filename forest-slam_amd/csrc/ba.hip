@@ -21,7 +21,7 @@
 //                its last column W H_ll^-1 g — the dense J^T J block contraction
 //   k_ba_solve   (window): S = H_pp + lam diag + 1e-6 I - sum_chunks G, Cholesky (fp64, LDS),
 //                pose step, tentative poses
-//   k_ba_upd     (window, 256 landmarks): back-substitution X' = X + H_ll^-1 (-g - W^T dp),
+//   k_ba_upd     (window, 8-16 landmarks): back-substitution X' = X + H_ll^-1 (-g - W^T dp),
 //                cost partials at the tentative point
 //   k_ba_accept  (window): LM accept / reject, lambda update
 // fp64 everywhere (the GEMM too): S = H_pp - G cancels, and with fp32 operands the refined
@@ -66,6 +66,7 @@ static_assert(64 * kLinWavesDefault / (kLinLPC64 / 2) <= 64 && 64 * kLinWavesDef
 // the block's own waves are all the latency hiding the CU gets
 constexpr int kLinWaves = kLinWavesDefault, kLinBlock = 64 * kLinWaves;
 constexpr int kLinMaxTiles = (36 + kLinWaves - 1) / kLinWaves;  // 16x16 tiles per wave: 36 upper tiles at NR = 128
+static_assert(10 <= kLinWaves, "NR = 64 (10 upper tiles): one tile per wave");
 constexpr double kD2Mono = 5.991, kD2Stereo = 7.815, kMinZ = 0.01, kLam0 = 1e-3;
 
 struct BaState {
@@ -77,13 +78,13 @@ struct BaState {
 };
 
 struct BaDims {
-  int Lmax, Omax, K, cap, NR, LPC, NCH, NCU, NPART;
-  int64_t oSt, oX0, oX1, oL, oG, oLs, oObs, oFl, oW, oGp, oCp, oNext, oHdr, win;
+  int Lmax, Omax, K, cap, NR, LPC, NCH, NCU, NPART, LPU, NCUP;
+  int64_t oSt, oX0, oX1, oL, oG, oLs, oObs, oFl, oGp, oCp, oNext, oHdr, win;
 };
 
 struct BaWin {
   BaState* st;
-  double *X0, *X1, *Lf, *gl, *W, *Gp, *cp;
+  double *X0, *X1, *Lf, *gl, *Gp, *cp;
   int *lstart, *flist, *next, *hdr;
   BaObs* obs;
 };
@@ -99,7 +100,6 @@ __device__ __forceinline__ BaWin view(void* base, const BaDims& d, int w) {
   v.lstart = (int*)(p + d.oLs);
   v.obs = (BaObs*)(p + d.oObs);
   v.flist = (int*)(p + d.oFl);
-  v.W = (double*)(p + d.oW);
   v.Gp = (double*)(p + d.oGp);
   v.cp = (double*)(p + d.oCp);
   v.next = (int*)(p + d.oNext);
@@ -238,7 +238,7 @@ __device__ __forceinline__ double obs_is2(const BaIn& in, const BaObs& o) {
 
 // residual, robust weight (x information) and cost of one observation; Jacobians if J (the
 // pose Jacobian Jp only if JP)
-template <bool J, bool JP = true>
+template <bool J, bool JP = true, bool JL = true>
 __device__ __forceinline__ void ba_eval(const double* T, const double* X, const BaObs& o, const BaCam& c,
                                         double is2, double* r, double& w, double& rho, double (*Jp)[6],
                                         double (*Jl)[3]) {
@@ -265,7 +265,59 @@ __device__ __forceinline__ void ba_eval(const double* T, const double* X, const 
   for (int k = 0; k < 3; ++k) {
     if (JP)
       for (int j = 0; j < 6; ++j) Jp[k][j] = Jc[k][0] * sk[0][j] + Jc[k][1] * sk[1][j] + Jc[k][2] * sk[2][j];
+    if (JL)
+      for (int j = 0; j < 3; ++j) Jl[k][j] = Jc[k][0] * T[j] + Jc[k][1] * T[3 + j] + Jc[k][2] * T[6 + j];
+  }
+}
+
+// Residual, weight, cost, J_l and what the pose / landmark coupling block W = J_p^T w J_l
+// (6 x 3) of one observation is made of, without forming J_p: with J_c the projection
+// Jacobian and J_p = J_c [-[X_c]x | I], W = w [-[X_c]x | I]^T M with M = J_c^T J_l, so a row
+// of W (ba_wrow) is w times a row of M (translation) or a skew combination of M's rows
+// (rotation).  M and X_c take fewer live registers than J_p or W; k_ba_lin and k_ba_upd form
+// W's rows with the same arithmetic.
+struct BaCoupling {
+  double M[3][3];  // J_c^T J_l
+  double xc[3];    // the point in the camera frame
+  double w;
+};
+__device__ __forceinline__ void ba_eval_lw(const double* T, const double* X, const BaObs& o, const BaCam& c,
+                                           double is2, double* r, double& rho, double (*Jl)[3], BaCoupling& cp) {
+  const double x = T[0] * X[0] + T[1] * X[1] + T[2] * X[2] + T[9];
+  const double y = T[3] * X[0] + T[4] * X[1] + T[5] * X[2] + T[10];
+  const double z = T[6] * X[0] + T[7] * X[1] + T[8] * X[2] + T[11];
+  const bool ok = z > kMinZ;
+  const double iz = 1.0 / (ok ? z : 1.0);
+  const bool st = !isnan(o.ur);
+  r[0] = c.fx * x * iz + c.cx - (double)o.u;
+  r[1] = c.fy * y * iz + c.cy - (double)o.v;
+  r[2] = st ? c.fx * (x - c.b) * iz + c.cx - (double)o.ur : 0.0;
+  const double s = (r[0] * r[0] + r[1] * r[1] + r[2] * r[2]) * is2;
+  const double d2 = st ? kD2Stereo : kD2Mono;
+  const bool inl = s <= d2;
+  rho = ok ? (inl ? s : 2.0 * sqrt(d2 * s) - d2) : 0.0;
+  cp.w = ok ? (inl ? 1.0 : sqrt(d2 / fmax(s, 1e-300))) * is2 : 0.0;
+  const double Jc[3][3] = {{c.fx * iz, 0.0, -c.fx * x * iz * iz},
+                           {0.0, c.fy * iz, -c.fy * y * iz * iz},
+                           {st ? c.fx * iz : 0.0, 0.0, st ? -c.fx * (x - c.b) * iz * iz : 0.0}};
+  for (int k = 0; k < 3; ++k)
     for (int j = 0; j < 3; ++j) Jl[k][j] = Jc[k][0] * T[j] + Jc[k][1] * T[3 + j] + Jc[k][2] * T[6 + j];
+  for (int q = 0; q < 3; ++q)
+    for (int k = 0; k < 3; ++k) cp.M[q][k] = Jc[0][q] * Jl[0][k] + Jc[1][q] * Jl[1][k] + Jc[2][q] * Jl[2][k];
+  cp.xc[0] = x;
+  cp.xc[1] = y;
+  cp.xc[2] = z;
+}
+
+// row a of W: rows of [-[X_c]x]^T are a = 0: (0, -z, y), 1: (z, 0, -x), 2: (-y, x, 0)
+__device__ __forceinline__ void ba_wrow(const BaCoupling& cp, int a, double* wr) {
+  const double x = cp.xc[0], y = cp.xc[1], z = cp.xc[2];
+  for (int k = 0; k < 3; ++k) {
+    const double m = a == 0 ? y * cp.M[2][k] - z * cp.M[1][k]
+                   : a == 1 ? z * cp.M[0][k] - x * cp.M[2][k]
+                   : a == 2 ? x * cp.M[1][k] - y * cp.M[0][k]
+                            : cp.M[a - 3][k];
+    wr[k] = cp.w * m;
   }
 }
 
@@ -544,7 +596,8 @@ __global__ void k_ba_setcost(void* ws, BaDims dm, int first) {
   if (first) S->cost0 = 0.5 * c;
 }
 
-// pose blocks of one frame + W of its observations
+// pose blocks of one frame (H_pp, g_p); the coupling blocks W are recomputed where they are
+// used (k_ba_lin, k_ba_upd) instead of crossing HBM
 __global__ __launch_bounds__(kBlock) void k_ba_pp(BaIn in, void* ws, BaDims dm, BaCam cam) {
   const BaWin v = view(ws, dm, blockIdx.x);
   BaState* S = v.st;
@@ -558,17 +611,13 @@ __global__ __launch_bounds__(kBlock) void k_ba_pp(BaIn in, void* ws, BaDims dm, 
   for (int ii = b0 + threadIdx.x; ii < b1; ii += kBlock) {
     const int oi = v.flist[ii];
     const BaObs o = v.obs[oi];
-    double r[3], w, rho, Jp[3][6], Jl[3][3];
-    ba_eval<true>(T, X + 3 * o.lm, o, cam, obs_is2(in, o), r, w, rho, Jp, Jl);
+    double r[3], w, rho, Jp[3][6];
+    ba_eval<true, true, false>(T, X + 3 * o.lm, o, cam, obs_is2(in, o), r, w, rho, Jp, nullptr);
     int q = 0;
     for (int a = 0; a < 6; ++a) {
       for (int bb = a; bb < 6; ++bb) h[q++] += w * (Jp[0][a] * Jp[0][bb] + Jp[1][a] * Jp[1][bb] + Jp[2][a] * Jp[2][bb]);
       h[21 + a] += w * (Jp[0][a] * r[0] + Jp[1][a] * r[1] + Jp[2][a] * r[2]);
     }
-    double* Wo = v.W + (int64_t)oi * 18;
-    for (int a = 0; a < 6; ++a)
-      for (int bb = 0; bb < 3; ++bb)
-        Wo[3 * a + bb] = w * (Jp[0][a] * Jl[0][bb] + Jp[1][a] * Jl[1][bb] + Jp[2][a] * Jl[2][bb]);
   }
   // the 27 block sums at once (same order as block_sum: wave sums, then the waves in order)
   __shared__ double s_part[kBlock / 64][27];
@@ -598,8 +647,22 @@ __device__ __forceinline__ void lin_tile(int k, int ntu, int NT, int& I, int& J)
   I = J = -1;
 }
 
+// Per chunk of LPC landmarks: (1) a group of GL = kLinBlock / LPC lanes per landmark, lane j =
+// the landmark's j-th observation (at most one per frame): residual, weight, J_p and J_l from
+// the poses staged in LDS, W = J_p^T w J_l in registers (never stored), w J_l^T J_l and
+// w J_l^T r summed over the group (xor butterfly), the damped 3x3 Cholesky (redundantly per
+// lane), z = L^-1 g and the rows Y = W L^-T; the group writes its landmark's three rows of Yt
+// whole (zeros in the columns of frames it is not seen in), so the buffer needs no clearing
+// pass, and one word of which 16-column tiles those rows touch.  (2) G += Yt^T Yt on MFMA.
+// The next chunk's landmark starts / observation / position are loaded during this chunk
+// (starts before its arithmetic, the observation record before its MFMA phase), so its
+// arithmetic starts from registers.
+// MAXT: 16x16 tiles per wave (1 at NR = 64: 10 tiles over 16 waves; 3 at NR = 128: 36 tiles)
+template <int MAXT>
 __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm, BaCam cam) {
   extern __shared__ double sY[];  // [3 LPC][NR + 2]
+  __shared__ double sT[kKMax][12];  // the window's current poses
+  __shared__ uint32_t s_tm[64];     // per landmark of the chunk: bit I = its rows reach tile I's columns
   const BaWin v = view(ws, dm, blockIdx.x);
   const BaState* S = v.st;
   if (!S->active) return;
@@ -614,135 +677,226 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
   const int NT = NR / 16, ntu = (np + 15) / 16;  // tiles covering the pose rows
   int ntiles = 0;
   for (int i = 0; i < ntu; ++i) ntiles += (ntu - i) + (ntu < NT ? 1 : 0);
+  for (int i = threadIdx.x; i < n * 12; i += kLinBlock) sT[i / 12][i % 12] = S->T[i / 12][i % 12];
   typedef double d4 __attribute__((ext_vector_type(4)));
-  d4 acc[kLinMaxTiles];
+  d4 acc[MAXT];
 #pragma unroll
-  for (int lt = 0; lt < kLinMaxTiles; ++lt) acc[lt] = d4{0.0, 0.0, 0.0, 0.0};
-  // s_act[g]: bit I set when rows 4g .. 4g+3 of the chunk's Yt hold a non-zero entry in the
-  // columns of tile I (a landmark's rows are non-zero only in the pose columns of the frames
-  // observing it, a few of the window's K-1 frames); a 4-row MFMA step of tile (I, J) whose rows
-  // are zero in tile I's or J's columns adds exactly zero and is skipped
-  __shared__ uint32_t s_act[64];
-  // a group of GL = kLinBlock / LPC lanes per landmark of the chunk (GL >= K: lane j of the
-  // group takes the landmark's j-th observation -- at most one per frame)
+  for (int lt = 0; lt < MAXT; ++lt) acc[lt] = d4{0.0, 0.0, 0.0, 0.0};
+  // this wave's tiles (fixed for the kernel)
+  int tI[MAXT], tJ[MAXT];
+#pragma unroll
+  for (int lt = 0; lt < MAXT; ++lt) {
+    const int k = kLinWaves * lt + wid;
+    tI[lt] = tJ[lt] = -1;
+    if (k < ntiles) lin_tile(k, ntu, NT, tI[lt], tJ[lt]);
+  }
   const int GL = kLinBlock / LPC, t = threadIdx.x / GL, j = threadIdx.x % GL;
-  for (int c = part; c * LPC < L; c += dm.NPART) {
-    {
-      typedef double d2 __attribute__((ext_vector_type(2)));
-      d2* z2 = reinterpret_cast<d2*>(sY);
-      for (int i = threadIdx.x; i < rows * NRP / 2; i += kLinBlock) z2[i] = d2{0.0, 0.0};
+  // one chunk ahead: the landmark's observation range, its observation j, its position
+  int ns0 = 0, ns1 = 0;
+  BaObs onext{};
+  double xn[3] = {0.0, 0.0, 0.0};
+  auto fetch_start = [&](int c) {
+    const int l = c * LPC + t;
+    ns0 = ns1 = 0;
+    if (c * LPC < L && l < L) {
+      ns0 = v.lstart[l];
+      ns1 = v.lstart[l + 1];
+      xn[0] = X[3 * l];
+      xn[1] = X[3 * l + 1];
+      xn[2] = X[3 * l + 2];
     }
-    if (threadIdx.x < 64) s_act[threadIdx.x] = 0u;
-    __syncthreads();
+  };
+  auto fetch_obs = [&]() {
+    if (j < ns1 - ns0) onext = v.obs[ns0 + j];
+  };
+  fetch_start(part);
+  fetch_obs();
+  __syncthreads();  // sT
+  for (int c = part; c * LPC < L; c += dm.NPART) {
+    const BaObs o = onext;
+    const int cnt = ns1 - ns0;
+    const double xl[3] = {xn[0], xn[1], xn[2]};
     const int lc0 = c * LPC, l = lc0 + t;
-    if (l < L) {
-      // (a) lane j: observation j's landmark-block terms w Jl^T Jl (upper 6) and w Jl^T r (3);
-      // (b) their sum over the group (xor butterfly: every lane ends with the same sums), the
-      // damped 3x3 Cholesky (redundantly per lane) and z = L^-1 g; (c) lane j: the rows
-      // 6 (f-1) .. 6 (f-1) + 5 of W L^-T for its observation (solve L y = W_p)
-      const int o0 = v.lstart[l], o1 = v.lstart[l + 1];
-      const bool has = j < o1 - o0;
-      double hg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-      BaObs o{};
-      if (has) {
-        o = v.obs[o0 + j];
-        double r[3], w, rho, Jl[3][3];
-        ba_eval<true, false>(S->T[o.frame], X + 3 * o.lm, o, cam, obs_is2(in, o), r, w, rho, nullptr, Jl);
-        int q = 0;
-        for (int a = 0; a < 3; ++a) {
-          for (int b = a; b < 3; ++b) hg[q++] = w * (Jl[0][a] * Jl[0][b] + Jl[1][a] * Jl[1][b] + Jl[2][a] * Jl[2][b]);
-          hg[6 + a] = w * (Jl[0][a] * r[0] + Jl[1][a] * r[1] + Jl[2][a] * r[2]);
-        }
+    const bool live = l < L, has = live && j < cnt;
+    // (a) lane j: observation j's landmark-block terms w Jl^T Jl (upper 6) and w Jl^T r (3), and
+    // its coupling block W; (b) their sum over the group (every lane ends with the same sums),
+    // the damped 3x3 Cholesky and z = L^-1 g; (c) lane j: rows 6 (f-1) .. 6 (f-1) + 5 of W L^-T
+    double hg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    BaCoupling cpl{};
+    const int f = has ? (int)o.frame : 0;
+    if (has) {
+      double r[3], rho, Jl[3][3];
+      ba_eval_lw(sT[f], xl, o, cam, obs_is2(in, o), r, rho, Jl, cpl);
+      const double w = cpl.w;
+      int q = 0;
+      for (int a2 = 0; a2 < 3; ++a2) {
+        for (int b2 = a2; b2 < 3; ++b2) hg[q++] = w * (Jl[0][a2] * Jl[0][b2] + Jl[1][a2] * Jl[1][b2] + Jl[2][a2] * Jl[2][b2]);
+        hg[6 + a2] = w * (Jl[0][a2] * r[0] + Jl[1][a2] * r[1] + Jl[2][a2] * r[2]);
       }
-      for (int m = GL >> 1; m >= 1; m >>= 1)
+    }
+    uint32_t fm = has && f > 0 ? 1u << f : 0u;  // frames with pose columns that see the landmark
+    for (int m = GL >> 1; m >= 1; m >>= 1) {
 #pragma unroll
-        for (int q = 0; q < 9; ++q) hg[q] += __shfl_xor(hg[q], m, 64);
-      const double* H = hg;
-      const double a00 = H[0] + lam * H[0] + 1e-6, a11 = H[3] + lam * H[3] + 1e-6, a22 = H[5] + lam * H[5] + 1e-6;
-      const double i00 = rsq_r(a00), l00 = a00 * i00;
-      const double l10 = H[1] * i00, l20 = H[2] * i00;
-      const double d11 = a11 - l10 * l10, i11 = rsq_r(d11), l11 = d11 * i11;
-      const double l21 = (H[4] - l20 * l10) * i11;
-      const double d22 = a22 - l20 * l20 - l21 * l21, i22 = rsq_r(d22), l22 = d22 * i22;
-      double* Y0 = sY + 3 * t * NRP;
-      if (j == 0) {
+      for (int q = 0; q < 9; ++q) hg[q] += __shfl_xor(hg[q], m, 64);
+      fm |= (uint32_t)__shfl_xor((int)fm, m, 64);
+    }
+    const double* H = hg;
+    const double a00 = H[0] + lam * H[0] + 1e-6, a11 = H[3] + lam * H[3] + 1e-6, a22 = H[5] + lam * H[5] + 1e-6;
+    const double i00 = rsq_r(a00), l00 = a00 * i00;
+    const double l10 = H[1] * i00, l20 = H[2] * i00;
+    const double d11 = a11 - l10 * l10, i11 = rsq_r(d11), l11 = d11 * i11;
+    const double l21 = (H[4] - l20 * l10) * i11;
+    const double d22 = a22 - l20 * l20 - l21 * l21, i22 = rsq_r(d22), l22 = d22 * i22;
+    double* Y0 = sY + 3 * t * NRP;
+    if (j == 0) {
+      double z0 = 0.0, z1 = 0.0, z2 = 0.0;
+      if (live) {
         double* Lf = v.Lf + 6 * l;
         Lf[0] = l00; Lf[1] = l10; Lf[2] = l11; Lf[3] = l20; Lf[4] = l21; Lf[5] = l22;
         v.gl[3 * l] = H[6]; v.gl[3 * l + 1] = H[7]; v.gl[3 * l + 2] = H[8];
-        const double z0 = H[6] * i00, z1 = (H[7] - l10 * z0) * i11, z2 = (H[8] - l20 * z0 - l21 * z1) * i22;
-        Y0[NR - 1] = z0;
-        Y0[NRP + NR - 1] = z1;
-        Y0[2 * NRP + NR - 1] = z2;
+        z0 = H[6] * i00;
+        z1 = (H[7] - l10 * z0) * i11;
+        z2 = (H[8] - l20 * z0 - l21 * z1) * i22;
       }
-      const int f = o.frame;
-      if (has && f > 0) {
-        const double* Wo = v.W + (int64_t)(o0 + j) * 18;
+      Y0[NR - 1] = z0;
+      Y0[NRP + NR - 1] = z1;
+      Y0[2 * NRP + NR - 1] = z2;
+      uint32_t tm = 0;
+      for (uint32_t mm = fm; mm; mm &= mm - 1) {
+        const int ff = __builtin_ctz(mm);
+        tm |= (1u << (6 * (ff - 1) / 16)) | (1u << ((6 * (ff - 1) + 5) / 16));
+      }
+      s_tm[t] = tm;
+    }
+    if (f > 0) {
+      for (int pp = 0; pp < 6; ++pp) {
+        double wr[3];
+        ba_wrow(cpl, pp, wr);
+        const double y0 = wr[0] * i00;
+        const double y1 = (wr[1] - l10 * y0) * i11;
+        const double y2 = (wr[2] - l20 * y0 - l21 * y1) * i22;
+        const int col = 6 * (f - 1) + pp;
+        Y0[col] = y0;
+        Y0[NRP + col] = y1;
+        Y0[2 * NRP + col] = y2;
+      }
+    }
+    // zeros: the pose column blocks of frames that do not see the landmark, and the padding
+    // columns np .. NR-2 (column NR-1 is z)
+    for (int fb = 1 + j; fb < n; fb += GL)
+      if (!((fm >> fb) & 1u))
         for (int pp = 0; pp < 6; ++pp) {
-          const double y0 = Wo[3 * pp] * i00;
-          const double y1 = (Wo[3 * pp + 1] - l10 * y0) * i11;
-          const double y2 = (Wo[3 * pp + 2] - l20 * y0 - l21 * y1) * i22;
-          const int col = 6 * (f - 1) + pp;
-          Y0[col] = y0;
-          Y0[NRP + col] = y1;
-          Y0[2 * NRP + col] = y2;
+          const int col = 6 * (fb - 1) + pp;
+          Y0[col] = 0.0;
+          Y0[NRP + col] = 0.0;
+          Y0[2 * NRP + col] = 0.0;
         }
-        const uint32_t bits = (1u << (6 * (f - 1) / 16)) | (1u << ((6 * (f - 1) + 5) / 16));
-        atomicOr(&s_act[3 * t / 4], bits);
-        if ((3 * t + 2) / 4 != 3 * t / 4) atomicOr(&s_act[(3 * t + 2) / 4], bits);
-      }
+    for (int col = np + j; col < NR - 1; col += GL) {
+      Y0[col] = 0.0;
+      Y0[NRP + col] = 0.0;
+      Y0[2 * NRP + col] = 0.0;
     }
+    fetch_start(c + dm.NPART);  // the next chunk's landmark starts / position
     __syncthreads();
-    // G += Yt^T Yt on MFMA: A[i][k] = Yt[k][16I + i], B[k][j] = Yt[k][16J + j], lane holds k = lane >> 4;
-    // the active 4-row steps of the tile (every row's z column is live: J = NT-1 always
-    // counts), ascending into one accumulator per tile (fixed order)
-    const uint32_t actl = lane < rows / 4 ? s_act[lane] : 0u;
+    fetch_obs();  // the next chunk's observation record, in flight during the MFMA phase
+    // G += Yt^T Yt on MFMA: A[i][k] = Yt[k][16I + i], B[k][j] = Yt[k][16J + j], lane holds k = lane >> 4.
+    // A 4-row step g (rows 4g .. 4g+3: landmarks 4g/3 and (4g+3)/3) of tile (I, J) is skipped
+    // when those rows are zero in tile I's or J's columns (the z column tile NT-1 always
+    // counts); each tile's steps ascend into its own accumulator (fixed order), the wave's
+    // tiles advance together (independent accumulators in flight) and step g+1's operands
+    // are loaded before step g's MFMAs are issued.
+    const uint32_t actl = lane < rows / 4 ? (s_tm[(4 * lane) / 3] | s_tm[(4 * lane + 3) / 3]) : 0u;
 #pragma unroll
-    for (int lt = 0; lt < kLinMaxTiles; ++lt) {
-      const int k = kLinWaves * lt + wid;
-      if (k < ntiles) {
-        int I, J;
-        lin_tile(k, ntu, NT, I, J);
-        const double* ya = sY + (lane >> 4) * NRP + 16 * I + (lane & 15);
-        const double* yb = sY + (lane >> 4) * NRP + 16 * J + (lane & 15);
-        uint64_t m = __ballot(((actl >> I) & 1u) && (((actl >> J) & 1u) || J == NT - 1));
-        while (m) {
-          const int g = __builtin_ctzll(m);
-          m &= m - 1;
-          const double a = ya[4 * g * NRP], bv = yb[4 * g * NRP];
-          acc[lt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc[lt], 0, 0, 0);
-        }
+    for (int lt = 0; lt < MAXT; ++lt) {
+      const int I = tI[lt], J = tJ[lt];
+      if (I < 0) continue;
+      const double* ya = sY + (lane >> 4) * NRP + 16 * I + (lane & 15);
+      const double* yb = sY + (lane >> 4) * NRP + 16 * J + (lane & 15);
+      uint64_t m = __ballot(((actl >> I) & 1u) && (((actl >> J) & 1u) || J == NT - 1));
+      if (!m) continue;
+      int g = __builtin_ctzll(m);
+      double av = ya[4 * g * NRP], bv = yb[4 * g * NRP];
+      for (m &= m - 1; m; m &= m - 1) {
+        g = __builtin_ctzll(m);
+        const double an = ya[4 * g * NRP], bn = yb[4 * g * NRP];
+        acc[lt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[lt], 0, 0, 0);
+        av = an;
+        bv = bn;
       }
+      acc[lt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[lt], 0, 0, 0);
     }
-    __syncthreads();  // sY is rewritten by the next chunk
+    __syncthreads();  // sY / s_tm are rewritten by the next chunk
   }
   // f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
   double* Gc = v.Gp + (int64_t)part * NR * NR;
 #pragma unroll
-  for (int lt = 0; lt < kLinMaxTiles; ++lt) {
-    const int k = kLinWaves * lt + wid;
-    if (k < ntiles) {
-      int I, J;
-      lin_tile(k, ntu, NT, I, J);
-      for (int i = 0; i < 4; ++i)
-        Gc[(16 * I + (lane >> 4) + 4 * i) * NR + 16 * J + (lane & 15)] = acc[lt][i];
-    }
+  for (int lt = 0; lt < MAXT; ++lt) {
+    const int I = tI[lt], J = tJ[lt];
+    if (I >= 0)
+      for (int i = 0; i < 4; ++i) Gc[(16 * I + (lane >> 4) + 4 * i) * NR + 16 * J + (lane & 15)] = acc[lt][i];
   }
 }
 
-// reduced camera system, Cholesky, pose step and tentative poses; 512 threads per window
-constexpr int kSolveBlock = 512, kSGA = 16, kSGB = 32;  // kSGA x kSGB thread grid over (i, j)
+// With many k_ba_lin partials (NPART >= kGsumParts: 1080p / K = 20 has 16 of 128 x 128) their
+// sum is formed by the whole GPU first (k_ba_gsum, into partial 0, the order k_ba_solve's own
+// sum has), so the one block per window that assembles S reads one partial instead of NPART.
+constexpr int kGsumParts = 8;
+__global__ __launch_bounds__(256) void k_ba_gsum(void* ws, BaDims dm) {
+  const BaWin v = view(ws, dm, blockIdx.x);
+  const BaState* S = v.st;
+  if (!S->active) return;
+  const int nch0 = (S->L + dm.LPC - 1) / dm.LPC, nch = nch0 < dm.NPART ? nch0 : dm.NPART;
+  const int64_t NN = (int64_t)dm.NR * dm.NR;
+  const int64_t i2 = (int64_t)blockIdx.y * 256 + threadIdx.x;  // 2 consecutive doubles
+  if (2 * i2 >= NN) return;
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  d2* g = reinterpret_cast<d2*>(v.Gp) + i2;
+  d2 part[kLinParts];
+#pragma unroll
+  for (int c = 0; c < kLinParts; ++c)
+    if (c < nch) part[c] = g[c * (NN / 2)];
+  d2 gs = {0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < kLinParts; ++c)
+    if (c < nch) gs += part[c];
+  g[0] = gs;
+}
+
+// reduced camera system, Cholesky, pose step and tentative poses; 512 threads per window.
+// The system S (np x np, np = 6 (n-1) <= 120) lives in LDS padded to NP = 16 ceil(np / 16)
+// (identity in the padding) with row stride NP + 2 (== 2 mod 32 doubles: the 16 rows x 2
+// columns of a wave half's 16x16x4 MFMA operand fetch hit 32 distinct bank pairs).  Factor:
+// right-looking Cholesky by 16-column panels, three phases per panel —
+//   (A) the diagonal 16x16 tile by wave 0 in registers (lane = row i, column group of 4;
+//       pivots as rsq + one Newton step, columns broadcast by shuffles),
+//   (B) the panel below it, one thread per row (16-step substitution against the tile),
+//   (C) the trailing update S_IJ -= L_Ip L_Jp^T of every lower tile on
+//       v_mfma_f64_16x16x4_f64 (4 K-steps per panel), tiles spread over the 8 waves —
+// three barriers per panel instead of two per 4 columns; the update, the bulk of the
+// arithmetic, leaves the LDS-bound scalar loop for the matrix pipe.
+constexpr int kSolveBlock = 512, kSolveWaves = kSolveBlock / 64;
+__host__ __device__ constexpr int ba_np16(int np) { return (np + 15) & ~15; }
+__host__ __device__ constexpr int ba_sstride(int np16) { return np16 + 2; }
 __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
-  extern __shared__ double sS[];  // [np*np] + rhs[np]
+  extern __shared__ double sS[];  // [NP][NP + 2] S then L (lower), rhs[NP], rinv[NP]
+  __shared__ int s_fail;
   const BaWin v = view(ws, dm, blockIdx.x);
   BaState* S = v.st;
   if (!S->active) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int n = S->n, L = S->L, NR = dm.NR;
-  const int np = 6 * (n - 1);
-  const int nch0 = (L + dm.LPC - 1) / dm.LPC, nch = nch0 < dm.NPART ? nch0 : dm.NPART;  // partials used
+  const int np = 6 * (n - 1), NP = ba_np16(np), STR = ba_sstride(NP), NTl = NP / 16;
+  const int nch0 = (L + dm.LPC - 1) / dm.LPC;
+  const int nch = dm.NPART >= kGsumParts ? 1 : (nch0 < dm.NPART ? nch0 : dm.NPART);  // partials to sum (k_ba_gsum)
   const double lam = S->lam;
-  double* rhs = sS + np * np;
-  double* rinv = rhs + np;  // reciprocal pivots of the factor
+  double* rhs = sS + NP * STR;
+  double* rinv = rhs + NP;  // reciprocal pivots of the factor
+  if (tid == 0) s_fail = 0;
+  // padding: identity rows / columns past np
+  for (int t = tid; t < NP * NP; t += kSolveBlock) {
+    const int a = t / NP, b = t - a * NP;
+    if (a >= np || b >= np) sS[a * STR + b] = a == b ? 1.0 : 0.0;
+  }
   // S = H_pp + lam diag + 1e-6 I - sum_c G_c (upper triangle, mirrored).  A thread takes 4
   // consecutive columns b0..b0+3 of a row a (b0 from the row's diagonal 16 x 16 tile, which
   // k_ba_lin writes in full) and loads the 4-wide slices of every partial before summing, so
@@ -777,96 +931,100 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
         hv = S->Hpp[fa][q];
         if (i == j) hv += lam * hv + 1e-6;
       }
-      sS[a * np + bb] = hv - gs[u];
-      sS[bb * np + a] = hv - gs[u];
+      sS[a * STR + bb] = hv - gs[u];
+      sS[bb * STR + a] = hv - gs[u];
     }
   }
-  for (int a = tid; a < np; a += kSolveBlock) {
+  for (int a = tid; a < NP; a += kSolveBlock) {
     double gs = 0.0;
-    const double* gp = v.Gp + a * NR + NR - 1;
+    if (a < np) {
+      const double* gp = v.Gp + a * NR + NR - 1;
 #pragma unroll 8
-    for (int c = 0; c < nch; ++c) gs += gp[(int64_t)c * NR * NR];
-    rhs[a] = -S->Hpp[a / 6 + 1][21 + a % 6] + gs;
+      for (int c = 0; c < nch; ++c) gs += gp[(int64_t)c * NR * NR];
+      rhs[a] = -S->Hpp[a / 6 + 1][21 + a % 6] + gs;
+    } else {
+      rhs[a] = 0.0;
+    }
   }
   __syncthreads();
-  const int ta = tid / kSGB, tb = tid % kSGB;
-  // Right-looking Cholesky by panels of kChol columns, two barriers per panel: (A) every
-  // thread factors the panel's diagonal block itself (identical arithmetic everywhere, so
-  // the pivots need no broadcast), (B) one thread per row below solves the row's panel
-  // entries, (C) the 16 x 16 thread grid applies the panel to the trailing matrix.  Every
-  // element sees exactly the column-by-column algorithm's operations in the same order
-  // (updates S -= L_ic L_jc for c ascending, then the division by the pivot), so the factor
-  // is bit-identical to it; only the barrier count drops (np -> 2 np / kChol).
-  constexpr int kChol = 4;
-  bool fail = false;
-  for (int k = 0; k < np; k += kChol) {
-    const int pw = min(kChol, np - k);
-    // pivots as reciprocal square roots (rsq_r, one hardware estimate + one Newton step), so
-    // the entries below the diagonal are products and the panel's dependent chain holds no
-    // IEEE sqrt / division sequence
-    double Lb[kChol][kChol], rp[kChol];
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  for (int p = 0; p < NTl; ++p) {
+    const int c0 = 16 * p;
+    // (A) diagonal tile: lane (i = lane & 15, cg = lane >> 4) holds S[c0 + i][c0 + 4 cg .. +3]
+    if (wid == 0) {
+      const int i = lane & 15, cg = lane >> 4;
+      double d[4];
 #pragma unroll
-    for (int a2 = 0; a2 < kChol; ++a2) {
-      if (a2 < pw) {
-        double d = sS[(k + a2) * np + k + a2];
+      for (int q = 0; q < 4; ++q) d[q] = sS[(c0 + i) * STR + c0 + 4 * cg + q];
+      bool bad = false;
 #pragma unroll
-        for (int c = 0; c < kChol; ++c)
-          if (c < a2) d -= Lb[a2][c] * Lb[a2][c];
-        if (!(d > 0.0)) fail = true;
-        rp[a2] = rsq_r(d);
-        Lb[a2][a2] = d * rp[a2];
+      for (int c = 0; c < 16; ++c) {
+        const int colane = 16 * (c >> 2);  // lanes holding column c: colane + row
+        const double piv = __shfl(d[c & 3], colane + c, 64);
+        bad |= !(piv > 0.0);
+        const double rp = rsq_r(piv);
+        const double vc = d[c & 3] * rp;  // column c of L on the lanes of column group c >> 2
+        const double lic = __shfl(vc, colane + i, 64);
 #pragma unroll
-        for (int b2 = 0; b2 < kChol; ++b2) {
-          if (b2 > a2 && b2 < pw) {
-            double v2 = sS[(k + b2) * np + k + a2];
-#pragma unroll
-            for (int c = 0; c < kChol; ++c)
-              if (c < a2) v2 -= Lb[b2][c] * Lb[a2][c];
-            Lb[b2][a2] = v2 * rp[a2];
-          }
+        for (int q = 0; q < 4; ++q) {
+          const int j = 4 * cg + q;
+          const double ljc = __shfl(vc, colane + j, 64);
+          if (j > c && i >= j) d[q] -= lic * ljc;
         }
+        if (cg == (c >> 2)) d[c & 3] = i >= c ? vc : 0.0;
+        if (lane == 0) rinv[c0 + c] = rp;
       }
-    }
-    if (fail) break;  // uniform: every thread computed the same pivots
-    for (int i = k + pw + tid; i < np; i += kSolveBlock) {
-      double x[kChol];
 #pragma unroll
-      for (int a2 = 0; a2 < kChol; ++a2) {
-        if (a2 < pw) {
-          double v2 = sS[i * np + k + a2];
-#pragma unroll
-          for (int c = 0; c < kChol; ++c)
-            if (c < a2) v2 -= x[c] * Lb[a2][c];
-          x[a2] = v2 * rp[a2];
-          sS[i * np + k + a2] = x[a2];
-        }
-      }
+      for (int q = 0; q < 4; ++q) sS[(c0 + i) * STR + c0 + 4 * cg + q] = d[q];
+      if (bad && lane == 0) s_fail = 1;
     }
     __syncthreads();
-    for (int i = k + pw + ta; i < np; i += kSGA) {
-      double li[kChol];
+    if (s_fail) break;  // uniform: read after the barrier
+    // (B) the panel's rows below the tile: L_Ip = S_Ip L_pp^-T, one thread per row
+    const int nb = NP - c0 - 16;
+    if (tid < nb) {
+      double* row = sS + (c0 + 16 + tid) * STR + c0;
+      double x[16];
 #pragma unroll
-      for (int a2 = 0; a2 < kChol; ++a2) li[a2] = a2 < pw ? sS[i * np + k + a2] : 0.0;
-      for (int j = k + pw + tb; j <= i; j += kSGB) {
-        double v2 = sS[i * np + j];
+      for (int c = 0; c < 16; ++c) x[c] = row[c];
 #pragma unroll
-        for (int a2 = 0; a2 < kChol; ++a2)
-          if (a2 < pw) v2 -= li[a2] * sS[j * np + k + a2];
-        sS[i * np + j] = v2;
+      for (int c = 0; c < 16; ++c) {
+        const double* lc = sS + (c0 + c) * STR + c0;  // row c of the tile: uniform (broadcast) reads
+        double sv = x[c];
+#pragma unroll
+        for (int c2 = 0; c2 < c; ++c2) sv -= x[c2] * lc[c2];
+        x[c] = sv * rinv[c0 + c];
       }
+#pragma unroll
+      for (int c = 0; c < 16; ++c) row[c] = x[c];
     }
-    if (tid == 0) {  // the diagonal block's factor (no thread reads these rows in this phase)
-#pragma unroll
-      for (int a2 = 0; a2 < kChol; ++a2) {
-#pragma unroll
-        for (int b2 = 0; b2 < kChol; ++b2)
-          if (a2 < pw && b2 >= a2 && b2 < pw) sS[(k + b2) * np + k + a2] = Lb[b2][a2];
-        if (a2 < pw) rinv[k + a2] = rp[a2];
+    __syncthreads();
+    // (C) trailing update of the lower tiles (I, J), p < J <= I < NTl, on MFMA:
+    // acc = L_Ip L_Jp^T (A[i][k] = L[16I + i][c0 + k], B[k][j] = L[16J + j][c0 + k])
+    const int m = NTl - p - 1;
+    for (int t = wid; t < m * (m + 1) / 2; t += kSolveWaves) {
+      int I = p + 1, rem = t;
+      while (rem >= I - p) {
+        rem -= I - p;
+        ++I;
       }
+      const int J = p + 1 + rem;
+      const double* pa = sS + (16 * I + (lane & 15)) * STR + c0 + (lane >> 4);
+      const double* pb = sS + (16 * J + (lane & 15)) * STR + c0 + (lane >> 4);
+      const double a0 = pa[0], a1 = pa[4], a2 = pa[8], a3 = pa[12];
+      const double b0 = pb[0], b1 = pb[4], b2 = pb[8], b3 = pb[12];
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a3, b3, acc, 0, 0, 0);
+      double* pc = sS + (16 * I + (lane >> 4)) * STR + 16 * J + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pc[4 * r * STR] -= acc[r];
     }
     __syncthreads();
   }
-  if (fail) {
+  if (s_fail) {
     if (tid == 0) S->fail = 1;
     return;
   }
@@ -888,11 +1046,11 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
     const int c0 = min(r0, np - 1), c1 = min(r1, np - 1);
     double x0 = r0 < np ? rhs[r0] : 0.0, x1 = r1 < np ? rhs[r1] : 0.0;
     {
-      double a0 = sS[c0 * np], a1 = sS[c1 * np], rv = rinv[0];
+      double a0 = sS[c0 * STR], a1 = sS[c1 * STR], rv = rinv[0];
       auto fwd = [&](int j, auto hi_t) {
         constexpr bool HI = decltype(hi_t)::value;
         const int jn = min(j + 1, np - 1);
-        const double na0 = sS[c0 * np + jn], na1 = sS[c1 * np + jn], nrv = rinv[jn];
+        const double na0 = sS[c0 * STR + jn], na1 = sS[c1 * STR + jn], nrv = rinv[jn];
         const double yj = bcast(HI ? x1 : x0, j & 63) * rv;
         x0 = r0 == j ? yj : (r0 > j ? x0 - a0 * yj : x0);
         x1 = r1 == j ? yj : (r1 > j ? x1 - a1 * yj : x1);
@@ -903,11 +1061,11 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
       for (int j = 64; j < np; ++j) fwd(j, std::true_type{});
     }
     {
-      double b0 = sS[(np - 1) * np + c0], b1 = sS[(np - 1) * np + c1], rv = rinv[np - 1];
+      double b0 = sS[(np - 1) * STR + c0], b1 = sS[(np - 1) * STR + c1], rv = rinv[np - 1];
       auto bwd = [&](int j, auto hi_t) {
         constexpr bool HI = decltype(hi_t)::value;
         const int jn = max(j - 1, 0);
-        const double nb0 = sS[jn * np + c0], nb1 = sS[jn * np + c1], nrv = rinv[jn];
+        const double nb0 = sS[jn * STR + c0], nb1 = sS[jn * STR + c1], nrv = rinv[jn];
         const double xj = bcast(HI ? x1 : x0, j & 63) * rv;
         x0 = r0 == j ? xj : (r0 < j ? x0 - b0 * xj : x0);
         x1 = r1 == j ? xj : (r1 < j ? x1 - b1 * xj : x1);
@@ -939,64 +1097,110 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
   }
 }
 
-// landmark back-substitution + cost partials at the tentative point
+// landmark back-substitution + cost partials at the tentative point.  A group of GLU lanes per
+// landmark, LPU = kBlock / GLU landmarks per block: lane j takes the landmark's observations
+// j, j + GLU, ... (all of them at GLU = 1, one each at GLU >= K) and forms their W^T dp (W from
+// ba_eval_lw at the linearisation point, as k_ba_lin) and, after the step, their cost at the
+// tentative poses; the group sums both over its lanes (xor butterfly), the block sums the cost
+// (fixed order) into one partial per block.  GLU = 1 at K <= 16 (short tracks: per-lane loops
+// are short and the blocks few), 32 at K = 20.
+template <int GLU>
 __global__ __launch_bounds__(kBlock) void k_ba_upd(BaIn in, void* ws, BaDims dm, BaCam cam) {
+  constexpr int LPU = kBlock / GLU;
   __shared__ double s_red[kBlock / 64];
+  __shared__ double sT[kKMax][12], sTt[kKMax][12], sdp[kKMax][6];
   const BaWin v = view(ws, dm, blockIdx.x);
   const BaState* S = v.st;
   if (!S->active || S->fail) return;
   const int L = S->L, c = blockIdx.y;
-  if (c * kBlock >= L) return;
+  if (c * LPU >= L) return;
+  const int n = S->n;
+  for (int i = threadIdx.x; i < n * 12; i += kBlock) {
+    sT[i / 12][i % 12] = S->T[i / 12][i % 12];
+    sTt[i / 12][i % 12] = S->Tt[i / 12][i % 12];
+  }
+  for (int i = threadIdx.x; i < n * 6; i += kBlock) sdp[i / 6][i % 6] = S->dp[i];
   const double* X = cur_X(v, S);
   double* Xn = new_X(v, S);
-  const int l = c * kBlock + threadIdx.x;
-  double acc = 0;
-  if (l < L) {
-    const int o0 = v.lstart[l], o1 = v.lstart[l + 1];
-    double b[3] = {-v.gl[3 * l], -v.gl[3 * l + 1], -v.gl[3 * l + 2]};
-    for (int oi = o0; oi < o1; ++oi) {
-      const int f = v.obs[oi].frame;
-      if (f == 0) continue;
-      const double* Wo = v.W + (int64_t)oi * 18;
-      const double* dp = S->dp + 6 * f;
-      for (int k = 0; k < 3; ++k)
-        b[k] -= Wo[k] * dp[0] + Wo[3 + k] * dp[1] + Wo[6 + k] * dp[2] + Wo[9 + k] * dp[3] + Wo[12 + k] * dp[4] +
-                Wo[15 + k] * dp[5];
+  const int t = threadIdx.x / GLU, j = threadIdx.x % GLU, l = c * LPU + t;
+  const bool live = l < L;
+  int o0 = 0, o1 = 0;
+  double Xc[3] = {0.0, 0.0, 0.0};
+  if (live) {
+    o0 = v.lstart[l];
+    o1 = v.lstart[l + 1];
+    Xc[0] = X[3 * l];
+    Xc[1] = X[3 * l + 1];
+    Xc[2] = X[3 * l + 2];
+  }
+  __syncthreads();  // staged poses
+  double wd[3] = {0.0, 0.0, 0.0};  // sum of W^T dp over this lane's observations
+  for (int oi = o0 + j; oi < o1; oi += GLU) {
+    const BaObs o = v.obs[oi];
+    if (o.frame == 0) continue;
+    double r[3], rho, Jl[3][3];
+    BaCoupling cpl;
+    ba_eval_lw(sT[o.frame], Xc, o, cam, obs_is2(in, o), r, rho, Jl, cpl);
+    const double* dp = sdp[o.frame];
+    double ow[3] = {0.0, 0.0, 0.0};
+    for (int a = 0; a < 6; ++a) {
+      double wr[3];
+      ba_wrow(cpl, a, wr);
+      for (int k = 0; k < 3; ++k) ow[k] += wr[k] * dp[a];
     }
+    for (int k = 0; k < 3; ++k) wd[k] += ow[k];
+  }
+  for (int m = GLU >> 1; m >= 1; m >>= 1)
+    for (int k = 0; k < 3; ++k) wd[k] += __shfl_xor(wd[k], m, 64);
+  double rho = 0.0;
+  if (live) {
+    const double b0 = -v.gl[3 * l] - wd[0], b1 = -v.gl[3 * l + 1] - wd[1], b2 = -v.gl[3 * l + 2] - wd[2];
     const double* Lf = v.Lf + 6 * l;
-    const double y0 = b[0] / Lf[0], y1 = (b[1] - Lf[1] * y0) / Lf[2], y2 = (b[2] - Lf[3] * y0 - Lf[4] * y1) / Lf[5];
+    const double y0 = b0 / Lf[0], y1 = (b1 - Lf[1] * y0) / Lf[2], y2 = (b2 - Lf[3] * y0 - Lf[4] * y1) / Lf[5];
     const double x2 = y2 / Lf[5], x1 = (y1 - Lf[4] * x2) / Lf[2], x0 = (y0 - Lf[1] * x1 - Lf[3] * x2) / Lf[0];
-    const double Xl[3] = {X[3 * l] + x0, X[3 * l + 1] + x1, X[3 * l + 2] + x2};
-    Xn[3 * l] = Xl[0];
-    Xn[3 * l + 1] = Xl[1];
-    Xn[3 * l + 2] = Xl[2];
-    for (int oi = o0; oi < o1; ++oi) {
+    const double Xl[3] = {Xc[0] + x0, Xc[1] + x1, Xc[2] + x2};
+    if (j == 0) {
+      Xn[3 * l] = Xl[0];
+      Xn[3 * l + 1] = Xl[1];
+      Xn[3 * l + 2] = Xl[2];
+    }
+    for (int oi = o0 + j; oi < o1; oi += GLU) {
       const BaObs o = v.obs[oi];
-      double r[3], w, rho;
-      ba_eval<false>(S->Tt[o.frame], Xl, o, cam, obs_is2(in, o), r, w, rho, nullptr, nullptr);
-      acc += rho;
+      double r[3], w, ro;
+      ba_eval<false>(sTt[o.frame], Xl, o, cam, obs_is2(in, o), r, w, ro, nullptr, nullptr);
+      rho += ro;
     }
   }
-  const double t = block_sum(acc, s_red);
-  if (threadIdx.x == 0) v.cp[c] = t;
+  for (int m = GLU >> 1; m >= 1; m >>= 1) rho += __shfl_xor(rho, m, 64);
+  const double tot = block_sum(j == 0 ? rho : 0.0, s_red);
+  if (threadIdx.x == 0) v.cp[c] = tot;
 }
 
-__global__ void k_ba_accept(void* ws, BaDims dm) {
+// LM accept / reject from k_ba_upd's cost partials (LPU landmarks each): one wave sums them,
+// lane i the partials i, i + 64, ... in order, then a fixed xor tree
+__global__ __launch_bounds__(64) void k_ba_accept(void* ws, BaDims dm) {
   const BaWin v = view(ws, dm, blockIdx.x);
   BaState* S = v.st;
   if (!S->active) return;
   const int n = S->n;
   __shared__ int s_acc;
+  __shared__ double s_sum;
+  {
+    const int nc = (S->L + dm.LPU - 1) / dm.LPU;
+    double part = 0.0;
+    if (!S->fail)
+      for (int i = threadIdx.x; i < nc; i += 64) part += v.cp[i];
+    part = wave_sum(part);
+    if (threadIdx.x == 0) s_sum = 0.5 * part;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     s_acc = 0;
     if (S->fail) {
       S->lam = fmin(S->lam * 10.0, 1e7);
       S->fail = 0;
     } else {
-      const int nc = (S->L + kBlock - 1) / kBlock;
-      double c = 0;
-      for (int i = 0; i < nc; ++i) c += v.cp[i];
-      c *= 0.5;
+      double c = s_sum;
       if (c < S->cost) {
         S->cost = c;
         S->lam = fmax(S->lam / 10.0, 1e-7);
@@ -1077,6 +1281,8 @@ BaDims make_dims(const fvo_ctx* ctx) {
   d.NPART = d.NPART < 1 ? 1 : d.NPART > kLinParts ? kLinParts : d.NPART;
   if (d.NPART > d.NCH) d.NPART = d.NCH;
   d.NCU = (d.Lmax + kBlock - 1) / kBlock;
+  d.LPU = d.K <= 16 ? kBlock : kBlock / 32;  // k_ba_upd: landmarks per block (GLU = 1 / 32 lanes each)
+  d.NCUP = (d.Lmax + d.LPU - 1) / d.LPU;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
     int64_t r = o;
@@ -1091,9 +1297,8 @@ BaDims make_dims(const fvo_ctx* ctx) {
   d.oLs = take(4ll * (d.Lmax + 1));
   d.oObs = take((int64_t)sizeof(BaObs) * d.Omax);
   d.oFl = take(4ll * d.Omax);
-  d.oW = take(8ll * 18 * d.Omax);
   d.oGp = take(8ll * d.NPART * d.NR * d.NR);
-  d.oCp = take(8ll * d.NCU);
+  d.oCp = take(8ll * (d.NCU > d.NCUP ? d.NCU : d.NCUP));  // cost partials (k_ba_cost / k_ba_upd)
   d.oNext = take(4ll * kKMax * d.cap);
   d.oHdr = take(4ll * (8 + kKMax + 1));
   d.win = o;
@@ -1108,8 +1313,8 @@ size_t build_shm(const BaDims& d) {
 }
 size_t lin_shm(const BaDims& d) { return (size_t)8 * 3 * d.LPC * (d.NR + 2); }
 size_t solve_shm(int K) {
-  const int np = 6 * (K - 1);
-  return (size_t)8 * (np * np + 2 * np);  // S, rhs, pivot roots
+  const int np = 6 * (K - 1), NP = ba_np16(np);
+  return (size_t)8 * (NP * ba_sstride(NP) + 2 * NP);  // S / L (padded), rhs, reciprocal pivots
 }
 
 }  // namespace
@@ -1131,7 +1336,9 @@ int ba_init(fvo_ctx* ctx) {
   if (build_shm(d) > 65536)
     FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_build<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)build_shm(d)));
-  FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_lin, hipFuncAttributeMaxDynamicSharedMemorySize,
+  FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_lin<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lin_shm(d)));
+  FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_lin<kLinMaxTiles>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lin_shm(d)));
   if (solve_shm(c.ba_window) > 65536)
     FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1171,9 +1378,13 @@ void ba_windows_launch(fvo_ctx* ctx, const BaIn& in, const BaCam& cam, const BaD
       hipLaunchKernelGGL(k_ba_setcost, dim3(nw), dim3(64), 0, s, ws, d, 0);
     }
     hipLaunchKernelGGL(k_ba_pp, gfr, dim3(kBlock), 0, s, in, ws, d, cam);
-    hipLaunchKernelGGL(k_ba_lin, gch, dim3(kLinBlock), shl, s, in, ws, d, cam);
+    if (d.NR == 64) hipLaunchKernelGGL(k_ba_lin<1>, gch, dim3(kLinBlock), shl, s, in, ws, d, cam);
+    else hipLaunchKernelGGL(k_ba_lin<kLinMaxTiles>, gch, dim3(kLinBlock), shl, s, in, ws, d, cam);
+    if (d.NPART >= kGsumParts)
+      hipLaunchKernelGGL(k_ba_gsum, dim3(nw, (d.NR * d.NR / 2 + 255) / 256), dim3(256), 0, s, ws, d);
     hipLaunchKernelGGL(k_ba_solve, dim3(nw), dim3(kSolveBlock), shs, s, ws, d);
-    hipLaunchKernelGGL(k_ba_upd, gcu, dim3(kBlock), 0, s, in, ws, d, cam);
+    if (d.K <= 16) hipLaunchKernelGGL(k_ba_upd<1>, dim3(nw, d.NCUP), dim3(kBlock), 0, s, in, ws, d, cam);
+    else hipLaunchKernelGGL(k_ba_upd<32>, dim3(nw, d.NCUP), dim3(kBlock), 0, s, in, ws, d, cam);
     hipLaunchKernelGGL(k_ba_accept, dim3(nw), dim3(64), 0, s, ws, d);
   }
   hipLaunchKernelGGL(k_ba_final, dim3(nw), dim3(64), 0, s, in.Trel, ws, d, fe, Tout + 16 * (int64_t)w0,

@@ -566,6 +566,10 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
               ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)vpair >> 32)) << 32)),
       (short)0, (int)__builtin_amdgcn_readfirstlane((int)vbytes), 0x00020000);
   const uint32_t voffV = (uint32_t)(((int64_t)(yy >> 2) * plane4 + (yy & 3) * D + q * DQ) * 2);
+  // rows 1..3 of a group read V(y-1) from memory although the same wave loads those bytes as
+  // the row above's own V: taking them from those lanes by a cross-lane permute instead (only
+  // row 0 / stripe-top lanes loading) was measured slower (r4: 3.90 -> 4.06 ms; the duplicate
+  // loads are L1 hits, the 3 ds_bpermute + select per column are not free)
   const uint32_t voffP = pzero ? 0x80000000u : (uint32_t)((prow + q * DQ) * 2);
   // the previous row's minimum over d, [group][x1][4] u16 (zero above row 0)
   const uint16_t* mpair = Mvol + (int64_t)b * (p.HG4 + p.nstripes) * W1 * 4;
