@@ -82,7 +82,7 @@ static void release(fvo_ctx* c) {
                   c->ncand,      c->nsel1,     c->nsel2,     c->koff,     c->scratch, c->fast_rec, c->rt.xofs,  c->rt.xc1,
                   c->rt.yofs,    c->rt.yc1,    c->umax,      c->bf_sidx,  c->bf_sdist, c->bf_tidx, c->sg_ckpt,
                   c->sg_V,      c->sg_M,      c->sg_raw,    c->pnp_hyp,  c->pnp_good,
-                  c->pnp_sub,    c->rs_table, c->pnp_models, c->pnp_ws, c->pnp_state, c->ba_ws,
+                  c->pnp_sub,    c->rs_table, c->pnp_models, c->pnp_ws, c->pnp_state, c->pnp_plan, c->ba_ws,
                   c->em_x, c->em_models, c->em_good, c->em_nmod, c->em_state, c->em_ws};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -385,7 +385,8 @@ int fvo_timing_read(fvo_ctx* c, double* ms, int32_t* launches) {
 // Debug/test hook: device pointer + size of an internal workspace buffer of the last call.
 // which: 0 pyramid, 1 blurred pyramid, 2 FAST score map (all [max_batch][total_px] u8),
 //        3 per-level candidate counts, 4 after retainBest(2n), 5 after retainBest(n) (i32 [B][L]),
-//        6 PnP RANSAC inlier count per iteration (i32 [B][1000]), 7 PnP hypotheses (f64 [B][1000][6]).
+//        6 PnP RANSAC inlier count per iteration (i32 [B][1000]), 7 PnP hypotheses (f64 [B][1000][6]),
+//        8 PnP RANSAC state (i32 [B][4]: best inlier count, iteration bound, best iteration, points).
 int fvo_debug_buffer(fvo_ctx* c, int which, void** ptr, int64_t* bytes) {
   if (!c || !ptr || !bytes) return -1;
   const int64_t B = c->cfg.max_batch;
@@ -402,6 +403,7 @@ int fvo_debug_buffer(fvo_ctx* c, int which, void** ptr, int64_t* bytes) {
     case 5: *ptr = c->nsel2; *bytes = B * c->g.nlevels * 4; return 0;
     case 6: *ptr = c->pnp_good; *bytes = B * c->pnp_max_iters * 4; return 0;
     case 7: *ptr = c->pnp_models; *bytes = B * c->pnp_max_iters * 6 * 8; return 0;
+    case 8: *ptr = c->pnp_state; *bytes = B * 16; return 0;
     default: return fvo_fail(c, "unknown debug buffer");
   }
 }

@@ -117,12 +117,10 @@ __device__ __forceinline__ void sort_desc(const double* w, double* sw, int* so) 
   }
 }
 
-// A (m x n row-major, m >= n) = U diag(W) V^T, W descending (one-sided Jacobi).
+// One-sided Jacobi on u (m x n row-major, starts as A) accumulating v (n x n, starts as I);
+// the columns of u end up as U diag(W) in unsorted order.
 template <int M, int N>
-__device__ void dsvd(const double* A, double* W, double* U, double* V) {
-  double u[M * N], v[N * N], w[N];
-  #pragma unroll
-  for (int i = 0; i < M * N; ++i) u[i] = A[i];
+__device__ __forceinline__ void dsvd_jacobi(double (&u)[M * N], double (&v)[N * N]) {
   #pragma unroll
   for (int i = 0; i < N * N; ++i) v[i] = (i % (N + 1) == 0) ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 60; ++sweep) {
@@ -161,6 +159,12 @@ __device__ void dsvd(const double* A, double* W, double* U, double* V) {
       }
     if (off < 1e-15) break;
   }
+}
+
+// Column norms of u sorted descending (stable): sw = W, ord = source column of each.
+template <int M, int N>
+__device__ __forceinline__ void dsvd_order(const double (&u)[M * N], double* sw, int* ord) {
+  double w[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     double s = 0;
@@ -168,11 +172,29 @@ __device__ void dsvd(const double* A, double* W, double* U, double* V) {
     for (int i = 0; i < M; ++i) s += u[i * N + j] * u[i * N + j];
     w[j] = sqrt(s);
   }
+  sort_desc<N>(w, sw, ord);
+}
+
+// column j (runtime) of a register matrix by compile-time selects (a runtime column index
+// would put the matrix in scratch for the whole decomposition)
+template <int R, int N>
+__device__ __forceinline__ double dsel(const double (&m)[R * N], int i, int j) {
+  double x = 0.0;
+#pragma unroll
+  for (int c = 0; c < N; ++c) x = (c == j) ? m[i * N + c] : x;
+  return x;
+}
+
+// A (m x n row-major, m >= n) = U diag(W) V^T, W descending (one-sided Jacobi).
+template <int M, int N>
+__device__ void dsvd(const double* A, double* W, double* U, double* V) {
+  double u[M * N], v[N * N];
+  #pragma unroll
+  for (int i = 0; i < M * N; ++i) u[i] = A[i];
+  dsvd_jacobi<M, N>(u, v);
   double sw[N];
   int ord[N];
-  sort_desc<N>(w, sw, ord);
-  // column ord[jj] picked by compile-time selects (a runtime column index would put u and v
-  // in scratch for the whole decomposition)
+  dsvd_order<M, N>(u, sw, ord);
 #pragma unroll
   for (int jj = 0; jj < N; ++jj) {
     const int j = ord[jj];
@@ -180,19 +202,9 @@ __device__ void dsvd(const double* A, double* W, double* U, double* V) {
     W[jj] = wj;
     const double inv = wj > 0 ? 1.0 / wj : 0.0;
 #pragma unroll
-    for (int i = 0; i < M; ++i) {
-      double x = 0.0;
+    for (int i = 0; i < M; ++i) U[i * N + jj] = dsel<M, N>(u, i, j) * inv;
 #pragma unroll
-      for (int c = 0; c < N; ++c) x = (c == j) ? u[i * N + c] : x;
-      U[i * N + jj] = x * inv;
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      double x = 0.0;
-#pragma unroll
-      for (int c = 0; c < N; ++c) x = (c == j) ? v[i * N + c] : x;
-      V[i * N + jj] = x;
-    }
+    for (int i = 0; i < N; ++i) V[i * N + jj] = dsel<N, N>(v, i, j);
   }
 }
 
@@ -294,25 +306,36 @@ __device__ bool chol_solve6(const double* A, const double* b, double* x) {
   return true;
 }
 
+// x = V diag(1/W) U^T b over the singular values above DBL_EPSILON * max(m, n) * W[0]
+// (cv::solve DECOMP_SVD); U and V are read from the Jacobi's u and v in place -- the same
+// products and sums as forming them first, without holding both copies.
 template <int M, int N>
 __device__ void dsolve(const double* A, const double* b, double* x) {
-  double W[N], U[M * N], V[N * N], tmp[N];
-  dsvd<M, N>(A, W, U, V);
-  double thr = DBL_EPSILON * (M > N ? M : N) * W[0];
+  double u[M * N], v[N * N], tmp[N];
 #pragma unroll
-  for (int j = 0; j < N; ++j) {
-    tmp[j] = 0.0;
-    if (W[j] <= thr) continue;
+  for (int i = 0; i < M * N; ++i) u[i] = A[i];
+  dsvd_jacobi<M, N>(u, v);
+  double sw[N];
+  int ord[N];
+  dsvd_order<M, N>(u, sw, ord);
+  const double thr = DBL_EPSILON * (M > N ? M : N) * sw[0];
+#pragma unroll
+  for (int jj = 0; jj < N; ++jj) {
+    const int j = ord[jj];
+    const double wj = sw[jj];
+    tmp[jj] = 0.0;
+    if (wj <= thr) continue;
+    const double inv = wj > 0 ? 1.0 / wj : 0.0;
     double s = 0;
 #pragma unroll
-    for (int i = 0; i < M; ++i) s += U[i * N + j] * b[i];
-    tmp[j] = s / W[j];
+    for (int i = 0; i < M; ++i) s += (dsel<M, N>(u, i, j) * inv) * b[i];
+    tmp[jj] = s / wj;
   }
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     double s = 0;
 #pragma unroll
-    for (int j = 0; j < N; ++j) s += V[i * N + j] * tmp[j];
+    for (int jj = 0; jj < N; ++jj) s += dsel<N, N>(v, i, ord[jj]) * tmp[jj];
     x[i] = s;
   }
 }
@@ -834,14 +857,18 @@ struct EPnPd {
 #pragma nounroll
     for (int it = 0; it < 5; ++it) {
       double A[24], b[6], x[4] = {0, 0, 0, 0};
+      // L and rho are re-read every iteration: hoisted out of the loop they held 66 doubles
+      // in registers (hyp_b at 256 VGPRs + AGPRs, one wave per SIMD)
+      int o = 0;
+      asm volatile("" : "+v"(o));
       #pragma unroll
       for (int i = 0; i < 6; ++i) {
-        const double* r = L + 10 * i;
+        const double* r = L + o + 10 * i;
         A[i * 4 + 0] = 2 * r[0] * betas[0] + r[1] * betas[1] + r[3] * betas[2] + r[6] * betas[3];
         A[i * 4 + 1] = r[1] * betas[0] + 2 * r[2] * betas[1] + r[4] * betas[2] + r[7] * betas[3];
         A[i * 4 + 2] = r[3] * betas[0] + r[4] * betas[1] + 2 * r[5] * betas[2] + r[8] * betas[3];
         A[i * 4 + 3] = r[6] * betas[0] + r[7] * betas[1] + r[8] * betas[2] + 2 * r[9] * betas[3];
-        b[i] = rho[i] - (r[0] * betas[0] * betas[0] + r[1] * betas[0] * betas[1] + r[2] * betas[1] * betas[1] +
+        b[i] = rho[o + i] - (r[0] * betas[0] * betas[0] + r[1] * betas[0] * betas[1] + r[2] * betas[1] * betas[1] +
                          r[3] * betas[0] * betas[2] + r[4] * betas[1] * betas[2] + r[5] * betas[2] * betas[2] +
                          r[6] * betas[0] * betas[3] + r[7] * betas[1] * betas[3] + r[8] * betas[2] * betas[3] +
                          r[9] * betas[3] * betas[3]);
@@ -883,27 +910,26 @@ struct EPnPd {
   // Second half: L (6x10) and rho from the null space and the control points ...
   __device__ void prep(const double (*nv)[12], double* L, double* rho) const {
     const double* vv[4] = {nv[3], nv[2], nv[1], nv[0]};
-    double dv[4][6][3];
     constexpr int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 6; ++j)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) dv[i][j][k] = vv[i][3 * pa[j] + k] - vv[i][3 * pb[j] + k];
+    // one control-point pair at a time (all 6 pairs' differences held at once were 72 doubles)
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
+      double dv[4][3];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dv[a][k] = vv[a][3 * pa[i] + k] - vv[a][3 * pb[i] + k];
       double* r = L + 10 * i;
-      r[0] = dot3(dv[0][i], dv[0][i]);
-      r[1] = 2.0f * dot3(dv[0][i], dv[1][i]);
-      r[2] = dot3(dv[1][i], dv[1][i]);
-      r[3] = 2.0f * dot3(dv[0][i], dv[2][i]);
-      r[4] = 2.0f * dot3(dv[1][i], dv[2][i]);
-      r[5] = dot3(dv[2][i], dv[2][i]);
-      r[6] = 2.0f * dot3(dv[0][i], dv[3][i]);
-      r[7] = 2.0f * dot3(dv[1][i], dv[3][i]);
-      r[8] = 2.0f * dot3(dv[2][i], dv[3][i]);
-      r[9] = dot3(dv[3][i], dv[3][i]);
+      r[0] = dot3(dv[0], dv[0]);
+      r[1] = 2.0f * dot3(dv[0], dv[1]);
+      r[2] = dot3(dv[1], dv[1]);
+      r[3] = 2.0f * dot3(dv[0], dv[2]);
+      r[4] = 2.0f * dot3(dv[1], dv[2]);
+      r[5] = dot3(dv[2], dv[2]);
+      r[6] = 2.0f * dot3(dv[0], dv[3]);
+      r[7] = 2.0f * dot3(dv[1], dv[3]);
+      r[8] = 2.0f * dot3(dv[2], dv[3]);
+      r[9] = dot3(dv[3], dv[3]);
     }
     rho[0] = dist2(cws[0], cws[1]); rho[1] = dist2(cws[0], cws[2]); rho[2] = dist2(cws[0], cws[3]);
     rho[3] = dist2(cws[1], cws[2]); rho[4] = dist2(cws[1], cws[3]); rho[5] = dist2(cws[2], cws[3]);
@@ -1280,71 +1306,146 @@ __global__ void k_pnp_subsets(const int32_t* __restrict__ npts, int batch, int c
 constexpr int PNP_WS = 256;  // doubles per subset: nv 48 | cws 12 | alphas 20 | pws 15 | us 10 | pad | MtM 144
 constexpr int PW_NV = 0, PW_CWS = 48, PW_AL = 60, PW_PWS = 80, PW_US = 95, PW_MTM = 112;
 
+// Round 1 runs every frame's first PNP_FIRST iterations on a (chunks, frames) grid. Round 2
+// runs only where round 1's adaptive bound left iterations over -- usually none, sometimes one
+// hard frame (a large motion, few inliers) needing up to maxIters: k_pnp_plan turns the frames'
+// remaining iterations into prefix sums of work units, and a fixed grid strides over the flat
+// unit space with round 1's grid size, so the hard frames share the whole grid and the easy
+// case dispatches one round-1 grid of blocks that exit at once. (A (chunks, frames) grid there was thousands of blocks that only
+// read the bound, each waiting for a register slot while the next step's disparity kernels
+// hold the CUs; a few blocks per frame serialised the hard frame.)
+constexpr int PNP_FIRST = 128;
+constexpr int PNP_CS = 64, PNP_CA = 8, PNP_CB = 16;  // iterations per setup / hyp_a / hyp_b unit
+
+__global__ __launch_bounds__(64) void k_pnp_plan(int batch, int maxIters, const PnpState* __restrict__ state,
+                                                 int32_t* __restrict__ plan) {
+  const int lane = threadIdx.x;
+  int carry[3] = {0, 0, 0};
+  const int C[3] = {PNP_CS, PNP_CA, PNP_CB};
+  for (int b0 = 0; b0 < batch; b0 += 64) {
+    const int b = b0 + lane;
+    int rem = 0;
+    if (b < batch) {
+      const PnpState st = state[b];
+      if (st.n >= 6) rem = max(0, min(st.niters, maxIters) - PNP_FIRST);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      int v = (rem + C[k] - 1) / C[k];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
+      }
+      const int incl = v, excl = incl - (rem + C[k] - 1) / C[k];
+      if (b < batch) plan[k * (batch + 1) + b] = carry[k] + excl;
+      carry[k] += __shfl(incl, 63, 64);
+    }
+  }
+  if (lane < 3) plan[lane * (batch + 1) + batch] = carry[lane];
+}
+
+// Work unit u of round 2 (granularity k) -> frame and its first iteration; wave-uniform.
+__device__ __forceinline__ void pnp_unit(const int32_t* __restrict__ pre, int batch, int u, int C, int& b, int& base) {
+  int lo = 0, hi = batch - 1;  // the largest b with pre[b] <= u
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pre[mid] <= u) lo = mid; else hi = mid - 1;
+  }
+  b = lo;
+  base = PNP_FIRST + (u - pre[lo]) * C;
+}
+
+// Drives a kernel body over its units: round 1 (plan == nullptr) one unit per block at
+// (blockIdx.x, blockIdx.y); round 2 the flat unit space, grid-strided. (One call site for the
+// body: two inlined copies cost hyp_a 64 VGPRs.)
+template <int C, typename Body>
+__device__ __forceinline__ void pnp_units(const int32_t* __restrict__ plan, int k, int batch, int maxIters,
+                                          const PnpState* __restrict__ state, Body body) {
+  const int32_t* pre = plan ? plan + k * (batch + 1) : nullptr;
+  const int total = plan ? pre[batch] : (int)blockIdx.x + 1;
+  for (int u = blockIdx.x; u < total; u += gridDim.x) {
+    int b, base, lim;
+    if (plan) {
+      pnp_unit(pre, batch, u, C, b, base);
+      lim = maxIters;
+    } else {
+      b = blockIdx.y;
+      base = u * C;
+      lim = PNP_FIRST;
+    }
+    const PnpState st = state[b];
+    const int hi = min(min(st.niters, maxIters), lim);
+    if (st.n < 6 || base >= hi) continue;
+    body(b, base, hi, st.n);
+  }
+}
+
 // lane per subset: points, control points, barycentric coordinates, M^T M -> workspace (the
 // register-heavy part, kept out of the long Jacobi kernel so that one stays small)
 __global__ __launch_bounds__(64, 4) void k_pnp_setup(const float* __restrict__ P3all, const float* __restrict__ p2all,
-                                                  int cap, Cam K, int maxIters, int it_lo,
+                                                  int cap, Cam K, int maxIters, int batch,
+                                                  const int32_t* __restrict__ plan,
                                                   const int16_t* __restrict__ table, int table_iters,
                                                   const PnpState* __restrict__ state, double* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) double smt[];  // [144][64]: one M^T M column per lane
-  const int b = blockIdx.y;
-  const int it = it_lo + blockIdx.x * 64 + threadIdx.x;
-  const PnpState st = state[b];
-  const int n = st.n;
-  if (n < 6 || it_lo + (int)blockIdx.x * 64 >= min(st.niters, maxIters)) return;
-  if (it >= maxIters) return;
-  double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
-  const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
-  const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
-  const int16_t* sb = table + ((int64_t)n * table_iters + it) * 5;
-  EPnPd<5> e;
-  e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    int j = sb[i];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) e.pws[3 * i + c] = (double)P3[j * 3 + c];
-    double xy[2];
-    dundistort(K, (double)p2[j * 2], (double)p2[j * 2 + 1], xy);
-    float fx = (float)xy[0], fy = (float)xy[1];
-    e.us[2 * i] = fx * K.fx + K.cx;
-    e.us[2 * i + 1] = fy * K.fy + K.cy;
-  }
   double* mt = smt + threadIdx.x;
-  e.build_mtm<64>(mt);
+  pnp_units<PNP_CS>(plan, 0, batch, maxIters, state, [&](int b, int base, int hi, int n) {
+    const int it = base + threadIdx.x;
+    if (it >= hi) return;
+    const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
+    const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
+    double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
+    const int16_t* sb = table + ((int64_t)n * table_iters + it) * 5;
+    EPnPd<5> e;
+    e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      int j = sb[i];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) e.pws[3 * i + c] = (double)P3[j * 3 + c];
+      double xy[2];
+      dundistort(K, (double)p2[j * 2], (double)p2[j * 2 + 1], xy);
+      float fx = (float)xy[0], fy = (float)xy[1];
+      e.us[2 * i] = fx * K.fx + K.cx;
+      e.us[2 * i + 1] = fy * K.fy + K.cy;
+    }
+    e.build_mtm<64>(mt);
 #pragma unroll 8
-  for (int k = 0; k < 144; ++k) w[PW_MTM + k] = mt[k * 64];
+    for (int k = 0; k < 144; ++k) w[PW_MTM + k] = mt[k * 64];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) w[PW_CWS + r * 3 + k] = e.cws[r][k];
+      for (int k = 0; k < 3; ++k) w[PW_CWS + r * 3 + k] = e.cws[r][k];
 #pragma unroll
-  for (int k = 0; k < 20; ++k) w[PW_AL + k] = e.alphas[k];
+    for (int k = 0; k < 20; ++k) w[PW_AL + k] = e.alphas[k];
 #pragma unroll
-  for (int k = 0; k < 15; ++k) w[PW_PWS + k] = e.pws[k];
+    for (int k = 0; k < 15; ++k) w[PW_PWS + k] = e.pws[k];
 #pragma unroll
-  for (int k = 0; k < 10; ++k) w[PW_US + k] = e.us[k];
+    for (int k = 0; k < 10; ++k) w[PW_US + k] = e.us[k];
+  });
 }
 
 // 8-lane group per subset: the null space of its M^T M (staged in LDS)
-__global__ __launch_bounds__(64) void k_pnp_hyp_a(int maxIters, int it_lo, const PnpState* __restrict__ state,
-                                                  double* __restrict__ ws) {
+__global__ __launch_bounds__(64) void k_pnp_hyp_a(int maxIters, int batch, const int32_t* __restrict__ plan,
+                                                  const PnpState* __restrict__ state, double* __restrict__ ws) {
   __shared__ double su[8][144];  // M^T M of the block's 8 subsets (one 8-lane group each)
-  const int b = blockIdx.y, g = threadIdx.x >> 3, l = threadIdx.x & 7;
-  const int it = it_lo + blockIdx.x * 8 + g;
-  const PnpState st = state[b];
-  if (st.n < 6 || it_lo + (int)blockIdx.x * 8 >= min(st.niters, maxIters)) return;
-  if (it >= maxIters) return;  // the whole group
+  const int g = threadIdx.x >> 3, l = threadIdx.x & 7;
   double* u = su[g];
-  double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
-  for (int k = l; k < 144; k += 8) u[k] = w[PW_MTM + k];
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  jacobi12_null4_group(u, l, w + PW_NV);
+  pnp_units<PNP_CA>(plan, 1, batch, maxIters, state, [&](int b, int base, int hi, int) {
+    const int it = base + g;
+    if (it >= hi) return;  // the whole group
+    double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
+    for (int k = l; k < 144; k += 8) u[k] = w[PW_MTM + k];
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    jacobi12_null4_group(u, l, w + PW_NV);
+  });
 }
 
 __global__ __launch_bounds__(64) void k_pnp_hyp_b(const float* __restrict__ P3all, const float* __restrict__ p2all,
-                                                  int cap, Cam K, float thr2, int maxIters, int it_lo,
+                                                  int cap, Cam K, float thr2, int maxIters, int batch,
+                                                  const int32_t* __restrict__ plan,
                                                   const PnpState* __restrict__ state, const double* __restrict__ ws,
                                                   double* __restrict__ model, int32_t* __restrict__ good) {
   // a 4-lane group per subset: lanes 0..2 run the three beta approximations side by side (the
@@ -1352,56 +1453,56 @@ __global__ __launch_bounds__(64) void k_pnp_hyp_b(const float* __restrict__ P3al
   // smaller error -- is applied to their results in order), then all four lanes score the
   // model over a quarter of the points each
   __shared__ double sL[16][66];  // per group: L (6x10) then rho (6)
-  const int b = blockIdx.y, g = threadIdx.x >> 2, l = threadIdx.x & 3;
-  const int it = it_lo + blockIdx.x * 16 + g;
-  const PnpState st = state[b];
-  const int n = st.n;
-  if (n < 6 || it_lo + (int)blockIdx.x * 16 >= min(st.niters, maxIters)) return;
-  if (it >= maxIters) return;  // the whole group
-  const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
-  const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
-  const double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
-  EPnPd<5, true> e;
-  e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
-  e.pws = w + PW_PWS;
-  e.us = w + PW_US;
-  e.alphas = w + PW_AL;
-  e.cws = reinterpret_cast<const double (*)[3]>(w + PW_CWS);
-  const double (*nv)[12] = reinterpret_cast<const double (*)[12]>(w + PW_NV);
-  // L (6x10) and rho are the same for the group's three approximations: lane 0 forms them
+  const int g = threadIdx.x >> 2, l = threadIdx.x & 3;
   double* L = sL[g];
-  if (l == 0) e.prep(nv, L, L + 60);
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  double R[9], t[3];
-  const double err = e.approx(l < 3 ? l + 1 : 3, L, L + 60, nv, R, t);
-  const int base = threadIdx.x & ~3;
-  const double e1 = __shfl(err, base + 1, 64), e2 = __shfl(err, base + 2, 64);
-  int sel = 0;
-  double best = __shfl(err, base, 64);
-  if (e1 < best) { best = e1; sel = 1; }
-  if (e2 < best) sel = 2;
+  pnp_units<PNP_CB>(plan, 2, batch, maxIters, state, [&](int b, int base, int hi, int n) {
+    const int it = base + g;
+    if (it >= hi) return;  // the whole group
+    const float* __restrict__ P3 = P3all + (int64_t)b * cap * 3;
+    const float* __restrict__ p2 = p2all + (int64_t)b * cap * 2;
+    const double* w = ws + ((int64_t)b * maxIters + it) * PNP_WS;
+    EPnPd<5, true> e;
+    e.fu = K.fx; e.fv = K.fy; e.uc = K.cx; e.vc = K.cy;
+    e.pws = w + PW_PWS;
+    e.us = w + PW_US;
+    e.alphas = w + PW_AL;
+    e.cws = reinterpret_cast<const double (*)[3]>(w + PW_CWS);
+    const double (*nv)[12] = reinterpret_cast<const double (*)[12]>(w + PW_NV);
+    // L (6x10) and rho are the same for the group's three approximations: lane 0 forms them
+    if (l == 0) e.prep(nv, L, L + 60);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    double R[9], t[3];
+    const double err = e.approx(l < 3 ? l + 1 : 3, L, L + 60, nv, R, t);
+    const int gb = threadIdx.x & ~3;
+    const double e1 = __shfl(err, gb + 1, 64), e2 = __shfl(err, gb + 2, 64);
+    int sel = 0;
+    double best = __shfl(err, gb, 64);
+    if (e1 < best) { best = e1; sel = 1; }
+    if (e2 < best) sel = 2;
 #pragma unroll
-  for (int k = 0; k < 9; ++k) R[k] = __shfl(R[k], base + sel, 64);
+    for (int k = 0; k < 9; ++k) R[k] = __shfl(R[k], gb + sel, 64);
 #pragma unroll
-  for (int k = 0; k < 3; ++k) t[k] = __shfl(t[k], base + sel, 64);
-  double r[3], dR[27];
-  rod_R2r(R, r);
-  if (l == 0) {
-    double* mo = model + ((int64_t)b * maxIters + it) * 6;
-    for (int i = 0; i < 3; ++i) { mo[i] = r[i]; mo[3 + i] = t[i]; }
-  }
-  rod_r2R(r, R, dR);
-  int gcount = 0;
-  for (int i = l; i < n; i += 4) {
-    double M[3] = {(double)P3[3 * i], (double)P3[3 * i + 1], (double)P3[3 * i + 2]}, uv[2];
-    dproject(K, R, dR, t, M, uv, nullptr);
-    float du = p2[2 * i] - (float)uv[0], dv = p2[2 * i + 1] - (float)uv[1];
-    gcount += (du * du + dv * dv) <= thr2;
-  }
-  gcount += __shfl_xor(gcount, 1, 4);
-  gcount += __shfl_xor(gcount, 2, 4);
-  if (l == 0) good[(int64_t)b * maxIters + it] = gcount;
+    for (int k = 0; k < 3; ++k) t[k] = __shfl(t[k], gb + sel, 64);
+    double r[3], dR[27];
+    rod_R2r(R, r);
+    if (l == 0) {
+      double* mo = model + ((int64_t)b * maxIters + it) * 6;
+      for (int i = 0; i < 3; ++i) { mo[i] = r[i]; mo[3 + i] = t[i]; }
+    }
+    rod_r2R(r, R, dR);
+    int gcount = 0;
+#pragma nounroll
+    for (int i = l; i < n; i += 4) {
+      double M[3] = {(double)P3[3 * i], (double)P3[3 * i + 1], (double)P3[3 * i + 2]}, uv[2];
+      dproject(K, R, dR, t, M, uv, nullptr);
+      float du = p2[2 * i] - (float)uv[0], dv = p2[2 * i + 1] - (float)uv[1];
+      gcount += (du * du + dv * dv) <= thr2;
+    }
+    gcount += __shfl_xor(gcount, 1, 4);
+    gcount += __shfl_xor(gcount, 2, 4);
+    if (l == 0) good[(int64_t)b * maxIters + it] = gcount;
+  });
 }
 
 // One wave per frame: 64 iterations' counts loaded at once, then walked in order with
@@ -1507,7 +1608,8 @@ int pose_init(fvo_ctx* ctx) {
       (rc = fvo_alloc(ctx, &ctx->pnp_ws, it * PNP_WS)) ||
       (rc = hipFuncSetAttribute((const void*)k_pnp_setup, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 144 * 64 * (int)sizeof(double)) == hipSuccess ? 0 : fvo_fail(ctx, "pnp: LDS attribute")) ||
-      (rc = fvo_alloc(ctx, &ctx->pnp_good, it)) || (rc = fvo_alloc(ctx, (PnpState**)&ctx->pnp_state, B)))
+      (rc = fvo_alloc(ctx, &ctx->pnp_good, it)) || (rc = fvo_alloc(ctx, (PnpState**)&ctx->pnp_state, B)) ||
+      (rc = fvo_alloc(ctx, &ctx->pnp_plan, 3 * (B + 1))))
     return rc;
   return 0;
 }
@@ -1545,20 +1647,25 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
   const float thr2 = (float)((double)reproj * reproj);
   const int maxIters = iters;
   PnpState* st = (PnpState*)ctx->pnp_state;
-  const int first = std::min(maxIters, 128);
-  auto hyp = [&](int lo, int hi) {
-    hipLaunchKernelGGL(k_pnp_setup, dim3((hi - lo + 63) / 64, batch), dim3(64), 144 * 64 * sizeof(double), s, P3, p2,
-                       cap, c, maxIters, lo,
+  const int first = std::min(maxIters, PNP_FIRST);
+  auto hyp = [&](const int32_t* plan, dim3 gs, dim3 ga, dim3 gb, int lo, int hi) {
+    hipLaunchKernelGGL(k_pnp_setup, gs, dim3(64), 144 * 64 * sizeof(double), s, P3, p2, cap, c, maxIters, batch, plan,
                        ctx->rs_table, ctx->rs_table_iters, st, ctx->pnp_ws);
-    hipLaunchKernelGGL(k_pnp_hyp_a, dim3((hi - lo + 7) / 8, batch), dim3(64), 0, s, maxIters, lo, st, ctx->pnp_ws);
-    hipLaunchKernelGGL(k_pnp_hyp_b, dim3((hi - lo + 15) / 16, batch), dim3(64), 0, s, P3, p2, cap, c, thr2, maxIters,
-                       lo, st, ctx->pnp_ws, ctx->pnp_models, ctx->pnp_good);
+    hipLaunchKernelGGL(k_pnp_hyp_a, ga, dim3(64), 0, s, maxIters, batch, plan, st, ctx->pnp_ws);
+    hipLaunchKernelGGL(k_pnp_hyp_b, gb, dim3(64), 0, s, P3, p2, cap, c, thr2, maxIters, batch, plan, st, ctx->pnp_ws,
+                       ctx->pnp_models, ctx->pnp_good);
     hipLaunchKernelGGL(k_pnp_replay, dim3(batch), dim3(64), 0, s, maxIters, lo, hi, conf, ctx->pnp_good, st);
   };
   FVO_TIMED(ctx, KN_PNP, s, {
     hipLaunchKernelGGL(k_pnp_subsets, dim3((batch + 63) / 64), dim3(64), 0, s, npts, batch, cap, maxIters, st);
-    hyp(0, first);
-    if (maxIters > first) hyp(first, maxIters);
+    hyp(nullptr, dim3((first + PNP_CS - 1) / PNP_CS, batch), dim3((first + PNP_CA - 1) / PNP_CA, batch),
+        dim3((first + PNP_CB - 1) / PNP_CB, batch), 0, first);
+    if (maxIters > first) {
+      hipLaunchKernelGGL(k_pnp_plan, dim3(1), dim3(64), 0, s, batch, maxIters, st, ctx->pnp_plan);
+      const int gs = batch * ((PNP_FIRST + PNP_CS - 1) / PNP_CS), ga = batch * ((PNP_FIRST + PNP_CA - 1) / PNP_CA),
+                gb = batch * ((PNP_FIRST + PNP_CB - 1) / PNP_CB);
+      hyp(ctx->pnp_plan, dim3(gs), dim3(ga), dim3(gb), first, maxIters);
+    }
     hipLaunchKernelGGL(k_pnp_refine, dim3(batch), dim3(64), 0, s, P3, p2, cap, c, thr2, maxIters, st,
                        ctx->pnp_models, rvec, tvec, T, status, inliers, ctx->pnp_sub, ctx->pnp_hyp);
   });

@@ -310,7 +310,8 @@ int fvo_timing_read(fvo_ctx* ctx, double* ms, int32_t* launches);
 /* Debug hook: device pointer and byte size of an internal buffer of the most recent ORB
  * call (0 pyramid, 1 blurred pyramid, 2 FAST score map, 3/4/5 per-level counts before /
  * after the two retainBest passes, 6/7 PnP RANSAC per-iteration inlier counts / hypotheses of the
- * last fvo_pnp_ransac).  For stage-by-stage parity tests only. */
+ * last fvo_pnp_ransac, 8 its per-frame RANSAC state: int32 best count, iteration bound, best
+ * iteration, points).  For stage-by-stage parity tests only. */
 int fvo_debug_buffer(fvo_ctx* ctx, int which, void** ptr, int64_t* bytes);
 
 #ifdef __cplusplus

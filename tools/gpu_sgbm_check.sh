@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 [ -n "$SKIP_TESTS" ] || timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_parity_configs.py -x -v -k "sgbm or disparity or config or middlebury" --timeout 200 --timeout-method thread > gpurun_out/sg/tests.log 2>&1 || exit 1
 for v in ${VARIANTS:-DEFAULT=1}; do
   for rep in 1 2; do
-    env $v timeout -k 10 120 python tools/bench_sgbm.py >> gpurun_out/sg/bench_$v.log 2>&1 || exit 1
+    env $v timeout -k 10 120 python tools/bench_sgbm.py >> "gpurun_out/sg/bench_$(echo $v | tr -c "A-Za-z0-9=_.\n" "_").log" 2>&1 || exit 1
   done
 done
 exit 0

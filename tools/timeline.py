@@ -41,6 +41,8 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--last-ms", type=float, default=200.0)
     ap.add_argument("--gaps", type=int, default=12)
+    ap.add_argument("--kernels", type=int, default=40, help="per-kernel totals over the window (0: none)")
+    ap.add_argument("--calls", default="", help="substring: list each call of matching kernels in the last 2 windows/10")
     a = ap.parse_args()
     rows = load(a.csv)
     t_end = max(r[1] for r in rows)
@@ -74,6 +76,30 @@ def main():
     print(f"idle total {sum(g[0] for g in gaps) / 1e6:.2f} ms in {len(gaps)} gaps; longest:")
     for g, p, n in gaps[:a.gaps]:
         print(f"  {g / 1e3:8.1f} us  after {p}  before {n}")
+    if a.calls:
+        calls(rows, a.calls, int(a.last_ms * 1e6 / 5))
+    if a.kernels:
+        tot = defaultdict(lambda: [0, 0])
+        for s, e, _, n in rows:
+            tot[n][0] += e - s
+            tot[n][1] += 1
+        print("kernel                                            calls    total     per call")
+        for n, (t, c) in sorted(tot.items(), key=lambda kv: -kv[1][0])[:a.kernels]:
+            print(f"{n:48s} {c:6d} {t / 1e6:8.2f} ms {t / c / 1e3:9.1f} us")
+
+
+def calls(rows, pat, span_ns):
+    t_hi = max(r[1] for r in rows)
+    t_lo = t_hi - span_ns
+    sel = [r for r in rows if pat in r[3] and r[0] >= t_lo]
+    print(f"calls of *{pat}* in the last {span_ns / 1e6:.1f} ms (start offset, duration, what else ran):")
+    for s, e, q, n in sel:
+        other = defaultdict(int)
+        for s2, e2, q2, n2 in rows:
+            if q2 != q and s2 < e and e2 > s:
+                other[n2] += min(e, e2) - max(s, s2)
+        top = ", ".join(f"{k} {v / 1e3:.0f}" for k, v in sorted(other.items(), key=lambda kv: -kv[1])[:3])
+        print(f"  {(s - t_lo) / 1e3:9.1f} us  {n:24s} q{q}  {(e - s) / 1e3:8.1f} us   [{top}]")
 
 
 if __name__ == "__main__":
