@@ -802,9 +802,11 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
     // G += Yt^T Yt on MFMA: A[i][k] = Yt[k][16I + i], B[k][j] = Yt[k][16J + j], lane holds k = lane >> 4.
     // A 4-row step g (rows 4g .. 4g+3: landmarks 4g/3 and (4g+3)/3) of tile (I, J) is skipped
     // when those rows are zero in tile I's or J's columns (the z column tile NT-1 always
-    // counts); each tile's steps ascend into its own accumulator (fixed order), the wave's
-    // tiles advance together (independent accumulators in flight) and step g+1's operands
-    // are loaded before step g's MFMAs are issued.
+    // counts); each tile's steps ascend into its own accumulator (fixed order) and step g+1's
+    // operands are loaded before step g's MFMA is issued.  (Walking the union of the wave's
+    // tiles' steps with every active tile issued back to back -- independent accumulators in
+    // flight -- measured slower: 1080p BA 5.0 -> 6.8 ms, 600p 1.87 -> 2.21 ms, the operand
+    // arrays spilling at 128 VGPRs.)
     const uint32_t actl = lane < rows / 4 ? (s_tm[(4 * lane) / 3] | s_tm[(4 * lane + 3) / 3]) : 0u;
 #pragma unroll
     for (int lt = 0; lt < MAXT; ++lt) {

@@ -5,10 +5,11 @@
 // k_gather_matches  one block per frame pair: mkpts0 = kp0[queryIdx].xy, mkpts1 = kp1[trainIdx].xy.
 // k_em_prep         one thread per frame: RANSAC subsets with OpenCV's RNG(-1) (ransac.h) and
 //                   the RANSAC state; normalised fp64 points written once per frame.
-// k_em_hyp          one lane per RANSAC iteration: the 5-point solver (null space of the 5x9
-//                   epipolar system as OpenCV's JacobiSVD builds it, 10x20 cubic constraints, Gauss-Jordan,
-//                   degree-10 det B(z), Durand-Kerner roots as solvePoly, up to 10 models) and
-//                   the float32 Sampson-type error of every model over all points from LDS.
+// k_em_coef / k_em_elim / k_em_roots / k_em_hyp  the 5-point solver per RANSAC iteration (null
+//                   space of the 5x9 epipolar system as OpenCV's JacobiSVD builds it, 10x20 cubic
+//                   constraints, Gauss-Jordan, degree-10 det B(z), Durand-Kerner roots as
+//                   solvePoly, up to 10 models), then the float32 Sampson-type error of every
+//                   model over all points from LDS.
 // k_em_replay       the serial acceptance rule of RANSACPointSetRegistrator::run over
 //                   (iteration, model) in order: goodCount > max(best, 4), adaptive niters.
 // k_em_final        one wave per frame: E and the inlier mask of the winning model.
@@ -523,12 +524,14 @@ __global__ void k_em_prep(const float* __restrict__ p0all, const float* __restri
 //   k_em_elim   16-lane group per subset: Gauss-Jordan on the 10x20 matrix with a row per lane
 //               (pivot = first maximum found by a group butterfly, rows swapped by relabelling,
 //               pivot row broadcast by shuffles), then B(z) and det B(z) -> workspace.
-//   k_em_hyp    lane per subset: Durand-Kerner on det B(z) with the roots in registers (300
-//               iterations unless the roots stop moving -- OpenCV's rule, so almost always
-//               300), the models, then every model of the wave scored over the points in LDS
-//               with the (subset, model) pairs spread evenly over the lanes.
+//   k_em_roots  16-lane row per subset, lane i = root i: Durand-Kerner on det B(z) (300
+//               sweeps unless the roots stop moving -- OpenCV's rule, so almost always 300) with
+//               the Gauss-Seidel sweep's products split over the lanes, then the models.
+//   k_em_hyp    every model of 64 subsets scored over the points in LDS, the (subset, model)
+//               pairs spread evenly over the lanes.
 // Before: one lane ran five_point() whole (1.9 KB of scratch per lane for the 10x20 matrix and
-// the root array, 1 wave per SIMD) -- 13 ms per 64 frames.
+// the root array, 1 wave per SIMD) -- 13 ms per 64 frames; then a lane per subset ran the whole
+// Durand-Kerner sweep (one wave's 300-sweep chain per launch) -- 4.1 ms.
 constexpr int EM_WS = 288;  // doubles per subset: basis 36 | A 200 | b 39 | det 11 | ok
 constexpr int EMW_BASIS = 0, EMW_A = 36, EMW_B = 236, EMW_C = 275, EMW_OK = 286;
 
@@ -726,9 +729,93 @@ __global__ __launch_bounds__(64) void k_em_elim(int maxIters, int it_lo, const E
   w[EMW_OK] = 1.0;
 }
 
-// solve_poly with every index static (roots in registers); identical arithmetic.  The stop
-// test uses max |num|^2 instead of max |num|: both are <= 0 exactly when every |num|^2 is 0.
-__device__ int solve_poly_reg(const double* c, Cx* roots) {
+// solvePoly's Durand-Kerner sweep by a 16-lane row per subset, lane i owning root i.  The
+// sweep is Gauss-Seidel: root i's update reads roots 0..i-1 already updated in this sweep and
+// roots i+1.. from the previous one, and its denominator multiplies the factors (p_i - root_j)
+// in ascending j.  So: every lane evaluates its numerator (Horner at its own root, which no
+// other update changes) at the start of the sweep; at step i lane i multiplies its remaining
+// factors j > i (previous-sweep roots), divides and publishes its new root (DPP row broadcast),
+// and every lane k > i multiplies factor j = i (the new root) into its denominator -- the same
+// products in the same order as the serial loop, the sweep's dependent chain cut from ten full
+// evaluations to ~n^2/2 products.  Lanes >= n (degree trimmed) and 10..15 idle; rows whose
+// polynomials all have degree 10 (the usual case) run a copy without the degree tests.
+constexpr int EM_G = 16, EM_GPW = 4;  // lanes per subset (one DPP row), subsets per wave
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// lane i of the row (i a compile-time constant after unrolling)
+__device__ __forceinline__ Cx row_bcast(Cx v, int i) {
+  switch (i) {
+#define FVO_BC(k) case k: return {dpp_d<0x150 + k>(v.re), dpp_d<0x150 + k>(v.im)};
+    FVO_BC(0) FVO_BC(1) FVO_BC(2) FVO_BC(3) FVO_BC(4) FVO_BC(5) FVO_BC(6) FVO_BC(7) FVO_BC(8) FVO_BC(9)
+#undef FVO_BC
+    default: return v;
+  }
+}
+// max over the 16-lane row: quad xor 1, xor 2, half-row mirror, row mirror
+__device__ __forceinline__ double row_max(double m) {
+  m = fmax(m, dpp_d<0xB1>(m));
+  m = fmax(m, dpp_d<0x4E>(m));
+  m = fmax(m, dpp_d<0x141>(m));
+  return fmax(m, dpp_d<0x140>(m));
+}
+
+template <bool FULL>
+__device__ __forceinline__ void dk_sweeps(Cx (&R)[10], Cx& own, const double (&cc)[11], int n, int l, bool mine) {
+  for (int iter = 0; iter < 300; ++iter) {
+    const Cx p = own;
+    Cx num{cc[0], 0}, den{cc[0], 0};
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      if (FULL || j < n) {
+        num = cmul(num, p);
+        num.re += cc[j + 1];
+      }
+    double mx = 0.0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      if (FULL || i < n) {
+        if (mine && l == i) {
+#pragma unroll
+          for (int j = i + 1; j < 10; ++j)
+            if (FULL || j < n) {
+              const Cx d{p.re - R[j].re, p.im - R[j].im};
+              if (d.re != 0 || d.im != 0) den = cmul(den, d);
+            }
+          const Cx q = cdiv(num, den);
+          own = {p.re - q.re, p.im - q.im};
+          mx = q.re * q.re + q.im * q.im;
+        }
+        R[i] = row_bcast(own, i);
+        if (mine && l > i) {
+          const Cx d{p.re - R[i].re, p.im - R[i].im};
+          if (d.re != 0 || d.im != 0) den = cmul(den, d);
+        }
+      }
+    }
+    // the sweep's max |step|^2 (fmax: order-free and NaN-ignoring like the serial fold)
+    if (row_max(mx) <= 0) break;  // row-uniform
+  }
+}
+
+__global__ __launch_bounds__(64) void k_em_roots(int maxIters, int it_lo, const EmState* __restrict__ state,
+                                                 const double* __restrict__ ws, double* __restrict__ models,
+                                                 int8_t* __restrict__ nmod) {
+  const int b = blockIdx.y, lane = threadIdx.x, g = lane >> 4, l = lane & 15, base = g * EM_G;
+  const int it = it_lo + blockIdx.x * EM_GPW + g;
+  const EmState st = state[b];
+  if (st.n < 5 || it_lo + (int)blockIdx.x * EM_GPW >= min(st.niters, maxIters)) return;  // block-uniform
+  const bool active = em_active(st, it, maxIters);                                      // row-uniform
+  const int64_t slot = (int64_t)b * maxIters + (active ? it : 0);
+  const double* w = ws + slot * EM_WS;
+  const bool solve = active && w[EMW_OK] != 0.0;
+  double c[11];
+#pragma unroll
+  for (int k = 0; k < 11; ++k) c[k] = solve ? w[EMW_C + k] : 0.0;
   int n = 10;
 #pragma unroll
   for (int k = 10; k >= 2; --k)
@@ -741,46 +828,69 @@ __device__ int solve_poly_reg(const double* c, Cx* roots) {
     for (int k = 0; k <= 10; ++k) v = (n - m == k) ? c[k] : v;
     cc[m] = v;
   }
+  Cx R[10];  // every root, kept current on every lane of the row
   {
     Cx p{1, 0}, r{1, 1};
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-      roots[i] = p;
+      R[i] = p;
       p = cmul(p, r);
     }
   }
-  for (int iter = 0; iter < 300; ++iter) {
-    double mx = 0;
+  Cx own{0, 0};
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      if (i < n) {
-        const Cx p = roots[i];
-        Cx num{cc[0], 0}, den{cc[0], 0};
+  for (int i = 0; i < 10; ++i)
+    if (l == i) own = R[i];
+  const bool mine = solve && l < n;
+  if (__ballot(solve && n != 10) == 0ull) dk_sweeps<true>(R, own, cc, n, l, mine);
+  else dk_sweeps<false>(R, own, cc, n, l, mine);
+  // models: root i (real, |im| <= 1e-10) -> B(z) null vector -> E; lane i, compacted in root order
+  bool valid = false;
+  double e[9];
+  if (mine && !(fabs(own.im) > 1e-10)) {
+    const double* bb = w + EMW_B;
+    const double* basis = w + EMW_BASIS;
+    const double z1 = own.re, z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
+    double bz[9];
 #pragma unroll
-        for (int j = 0; j < 10; ++j) {
-          if (j < n) {
-            num = cmul(num, p);
-            num.re += cc[j + 1];
-            if (j != i) {
-              const Cx d{p.re - roots[j].re, p.im - roots[j].im};
-              if (d.re != 0 || d.im != 0) den = cmul(den, d);
-            }
-          }
-        }
-        num = cdiv(num, den);
-        roots[i] = {p.re - num.re, p.im - num.im};
-        mx = fmax(mx, num.re * num.re + num.im * num.im);
-      }
+    for (int j = 0; j < 3; ++j) {
+      const double* br = bb + j * 13;
+      bz[j * 3 + 0] = br[0] * z3 + br[1] * z2 + br[2] * z1 + br[3];
+      bz[j * 3 + 1] = br[4] * z3 + br[5] * z2 + br[6] * z1 + br[7];
+      bz[j * 3 + 2] = br[8] * z4 + br[9] * z3 + br[10] * z2 + br[11] * z1 + br[12];
     }
-    if (mx <= 0) break;
+    double v[3];
+    null3(bz, v);
+    if (!(fabs(v[2]) < 1e-10)) {
+      const double xx = v[0] / v[2], yy = v[1] / v[2];
+      double n2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        e[k] = basis[k] * xx + basis[9 + k] * yy + basis[18 + k] * z1 + basis[27 + k];
+        n2 += e[k] * e[k];
+      }
+      const double nrm = sqrt(n2);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) e[k] = e[k] / nrm;
+      valid = true;
+    }
   }
-  return n;
+  const uint64_t vm = __ballot(valid), gm = 0xFFFFull << base;
+  const int rank = __popcll(vm & gm & ((1ull << lane) - 1ull));
+  if (valid) {
+    double* eo = models + slot * 90 + rank * 9;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) eo[k] = e[k];
+  }
+  if (active && l == 0) nmod[slot] = (int8_t)__popcll(vm & gm);
 }
 
+// Scoring: every (subset, model) pair of the block's 64 subsets spread evenly over the lanes,
+// the points staged in LDS.
 __global__ __launch_bounds__(64) void k_em_hyp(const double* __restrict__ xn, int cap, float thr2, int maxIters,
                                                int it_lo, const EmState* __restrict__ state,
-                                               const double* __restrict__ ws, double* __restrict__ models,
-                                               int32_t* __restrict__ good, int8_t* __restrict__ nmod) {
+                                               const double* __restrict__ models, int32_t* __restrict__ good,
+                                               const int8_t* __restrict__ nmod) {
   extern __shared__ __attribute__((aligned(16))) double sx[];  // [n][4]
   __shared__ int mlist[640];                                   // (lane << 4 | model) of the wave's models
   const int b = blockIdx.y, lane = threadIdx.x;
@@ -791,50 +901,7 @@ __global__ __launch_bounds__(64) void k_em_hyp(const double* __restrict__ xn, in
   const double* x = xn + (int64_t)b * cap * 4;
   for (int i = lane; i < 4 * n; i += 64) sx[i] = x[i];
   const bool active = em_active(st, it, maxIters);
-  const int64_t slot = (int64_t)b * maxIters + (active ? it : 0);
-  const double* w = ws + slot * EM_WS;
-  int count = 0;
-  if (active && w[EMW_OK] != 0.0) {
-    double cz[11];
-#pragma unroll
-    for (int k = 0; k < 11; ++k) cz[k] = w[EMW_C + k];
-    Cx roots[10];
-    const int nr = solve_poly_reg(cz, roots);
-    double* mo = models + slot * 90;
-    const double* bb = w + EMW_B;
-    const double* basis = w + EMW_BASIS;
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      if (i < nr && !(fabs(roots[i].im) > 1e-10)) {
-        const double z1 = roots[i].re, z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
-        double bz[9];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const double* br = bb + j * 13;
-          bz[j * 3 + 0] = br[0] * z3 + br[1] * z2 + br[2] * z1 + br[3];
-          bz[j * 3 + 1] = br[4] * z3 + br[5] * z2 + br[6] * z1 + br[7];
-          bz[j * 3 + 2] = br[8] * z4 + br[9] * z3 + br[10] * z2 + br[11] * z1 + br[12];
-        }
-        double v[3];
-        null3(bz, v);
-        if (!(fabs(v[2]) < 1e-10)) {
-          const double xx = v[0] / v[2], yy = v[1] / v[2];
-          double e[9], n2 = 0.0;
-#pragma unroll
-          for (int k = 0; k < 9; ++k) {
-            e[k] = basis[k] * xx + basis[9 + k] * yy + basis[18 + k] * z1 + basis[27 + k];
-            n2 += e[k] * e[k];
-          }
-          const double nrm = sqrt(n2);
-          double* eo = mo + count * 9;
-#pragma unroll
-          for (int k = 0; k < 9; ++k) eo[k] = e[k] / nrm;
-          ++count;
-        }
-      }
-    }
-  }
-  if (active) nmod[slot] = (int8_t)count;
+  const int count = active ? (int)nmod[(int64_t)b * maxIters + it] : 0;
   // spread the wave's (subset, model) pairs over the lanes: exclusive scan of the counts
   int off = count;
 #pragma unroll
@@ -1037,16 +1104,17 @@ int essential_run(fvo_ctx* ctx, const float* p0, const float* p1, const int32_t*
   if (shm + 640 * sizeof(int) > 160 * 1024) return fvo_fail(ctx, "essential: point capacity exceeds LDS (cap <= 5040)");
   if (shm > 64 * 1024)
     FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_em_hyp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-  // the first chunk's width hardly matters (measured 64..384 subsets: 3.94..4.08 ms per 64
-  // frames): a wave's Durand-Kerner chain (300 iterations) sets the time of each launch
+  // round 1: the first 128 subsets of every frame (the adaptive bound usually ends below)
   const int first = std::min(maxIters, 128);
   auto solve = [&](int lo, int hi) {
     const int nit = hi - lo;
     hipLaunchKernelGGL(k_em_coef, dim3((nit + 63) / 64, batch), dim3(64), 0, s, ctx->em_x, cap, maxIters, lo,
                        ctx->rs_table, ctx->rs_table_iters, st, ctx->em_ws);
     hipLaunchKernelGGL(k_em_elim, dim3((nit + 3) / 4, batch), dim3(64), 0, s, maxIters, lo, st, ctx->em_ws);
+    hipLaunchKernelGGL(k_em_roots, dim3((nit + EM_GPW - 1) / EM_GPW, batch), dim3(64), 0, s, maxIters, lo, st,
+                       ctx->em_ws, ctx->em_models, ctx->em_nmod);
     hipLaunchKernelGGL(k_em_hyp, dim3((nit + 63) / 64, batch), dim3(64), shm, s, ctx->em_x, cap, thr2, maxIters, lo,
-                       st, ctx->em_ws, ctx->em_models, ctx->em_good, ctx->em_nmod);
+                       st, ctx->em_models, ctx->em_good, ctx->em_nmod);
     hipLaunchKernelGGL(k_em_replay, dim3(batch), dim3(64), 0, s, maxIters, lo, hi, prob, ctx->em_good, ctx->em_nmod,
                        st);
   };
