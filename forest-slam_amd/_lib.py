@@ -31,7 +31,13 @@ class FvoConfig(ctypes.Structure):
             "ba_max_obs", "sgbm_max_batch")]
 
 
-ABI_VERSION = 5  # FVO_ABI_VERSION of include/fvo.h
+class FvoRegion(ctypes.Structure):
+    """fvo_region of include/fvo.h."""
+    _fields_ = [("dst", ctypes.c_void_p), ("src", ctypes.c_void_p), ("bytes", ctypes.c_int64)]
+
+
+FVO_MAX_REGIONS = 32
+ABI_VERSION = 6  # FVO_ABI_VERSION of include/fvo.h
 STAGE_ORB, STAGE_BF, STAGE_SGBM, STAGE_POSE, STAGE_BA, STAGE_MONO = 1, 2, 4, 8, 16, 32
 
 # name -> (restype, argtypes); mirrors include/fvo.h
@@ -66,6 +72,8 @@ SIGNATURES = {
     "fvo_undistort_gray": (ctypes.c_int, [_P, _P, _I, _L, _I, _P, _P, _P, _L, _I, _P]),
     "fvo_map_transform": (ctypes.c_int, [_P, _P, _I, _P, _I, _L, _P, _P, _L, _P, _P, _P]),
     "fvo_chain_poses": (ctypes.c_int, [_P, _P, _P, _P, _I, _I, _P, _P, _P, _P]),
+    "fvo_copy_regions": (ctypes.c_int, [_P, _I, _P, _P]),
+    "fvo_count_guard": (ctypes.c_int, [_P, _P, _P, _I, _I, _P, _I, _P, _P]),
     "fvo_voxel_workspace_bytes": (ctypes.c_int64, [_L]),
     "fvo_voxel_down_sample": (ctypes.c_int, [_P, _P, _L, ctypes.c_double, _P, _L, _P, _P, _P, _P]),
     "fvo_motion_blur": (ctypes.c_int, [_P, _P, _I, _L, _I, _I, ctypes.c_double, _P, _P, _I, _P, _P, _L, _I, _P]),
@@ -408,6 +416,37 @@ class Context:
         self._check(self.L.fvo_chain_poses(self.h, _ptr(T), _ptr(status), _ptr(n_points), S, n, _ptr(cum_state),
                                            _ptr(cum), _ptr(npo), _stream(self.device)))
         return cum, npo
+
+    def copy_regions(self, pairs):
+        """Device-to-device copies ``dst.copy_(src)`` for every (dst, src) in pairs, batched
+        into fvo_copy_regions launches of up to FVO_MAX_REGIONS (same-dtype contiguous pairs;
+        any other pair is copied by torch).  No destination may overlap any source or other
+        destination (the library refuses it)."""
+        batch = []
+        for d, src in pairs:
+            nb = d.numel() * d.element_size()
+            if d.dtype != src.dtype or d.shape != src.shape or not (d.is_contiguous() and src.is_contiguous()):
+                d.copy_(src)
+                continue
+            if nb:
+                batch.append((d.data_ptr(), src.data_ptr(), nb))
+        for k in range(0, len(batch), FVO_MAX_REGIONS):
+            part = batch[k:k + FVO_MAX_REGIONS]
+            arr = (FvoRegion * len(part))(*[FvoRegion(dp, sp, nb) for dp, sp, nb in part])
+            self._check(self.L.fvo_copy_regions(self.h, len(part), ctypes.cast(arr, _P), _stream(self.device)))
+
+    def count_guard(self, counts, n, sets=1, q_counts=None, status=None, code=0, clamped_out=None):
+        """fvo_count_guard: status[i] = code where any counts[s*n + i] / q_counts[s*n + i]
+        (s < sets) is negative; clamped_out[i] = max(counts[i], 0)."""
+        for t in (counts, q_counts, status, clamped_out):
+            if t is not None and (t.dtype != torch.int32 or not t.is_contiguous()):
+                raise TypeError("count_guard takes contiguous int32 tensors")
+        if counts.numel() < sets * n or (q_counts is not None and q_counts.numel() < sets * n):
+            raise ValueError("count_guard: counts shorter than sets * n")
+        if (status is not None and status.numel() < n) or (clamped_out is not None and clamped_out.numel() < n):
+            raise ValueError("count_guard: outputs shorter than n")
+        self._check(self.L.fvo_count_guard(self.h, _ptr(counts), _ptr(q_counts), n, sets, _ptr(status), code,
+                                           _ptr(clamped_out), _stream(self.device)))
 
     def voxel_down_sample(self, points, voxel_size, workspace=None):
         """Open3D voxel_down_sample (mono_slam.py:155): points f64 [N,3] (device) ->

@@ -18,7 +18,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libfvo.so")
 OBJ = os.path.join(HERE, "build", "obj")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
-SOURCES = ["capi.cpp", "orb.hip", "bf.hip", "sgbm.hip", "pose.hip", "ba.hip", "essential.hip", "ingest.hip", "map.hip"]
+SOURCES = ["capi.cpp", "orb.hip", "bf.hip", "sgbm.hip", "pose.hip", "ba.hip", "essential.hip", "ingest.hip", "map.hip", "util.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
          "-Wno-unused-result", "-Wno-unused-function", "-Wno-unused-variable"]

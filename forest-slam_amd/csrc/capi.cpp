@@ -328,6 +328,43 @@ int fvo_chain_poses(fvo_ctx* c, const double* T, const int32_t* status, const in
   return chain_poses_run(c, T, status, n_points, n_seq, n, cum_state, cum_out, n_points_out, (hipStream_t)stream);
 }
 
+int fvo_copy_regions(fvo_ctx* c, int32_t count, const fvo_region* regions, fvo_stream stream) {
+  if (!c) return -1;
+  if (count < 0 || count > FVO_MAX_REGIONS) return fvo_fail(c, "copy_regions: count out of [0, FVO_MAX_REGIONS]");
+  if (count == 0) return 0;
+  if (!regions) return fvo_fail(c, "null pointer argument");
+  int used = 0;
+  fvo_region live[FVO_MAX_REGIONS];
+  for (int i = 0; i < count; ++i) {
+    const fvo_region& g = regions[i];
+    if (g.bytes < 0) return fvo_fail(c, "copy_regions: bytes < 0");
+    if (g.bytes == 0) continue;
+    if (!g.dst || !g.src) return fvo_fail(c, "copy_regions: null region pointer");
+    live[used++] = g;
+  }
+  auto overlap = [](const void* a, const void* b, int64_t na, int64_t nb) {
+    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+    return x < y + (uintptr_t)nb && y < x + (uintptr_t)na;
+  };
+  for (int i = 0; i < used; ++i)
+    for (int j = 0; j < used; ++j) {
+      if (overlap(live[i].dst, live[j].src, live[i].bytes, live[j].bytes) ||
+          (i != j && overlap(live[i].dst, live[j].dst, live[i].bytes, live[j].bytes)))
+        return fvo_fail(c, "copy_regions: a destination overlaps a source or another destination");
+    }
+  if (used == 0) return 0;
+  return copy_regions_run(c, used, live, (hipStream_t)stream);
+}
+
+int fvo_count_guard(fvo_ctx* c, const int32_t* counts, const int32_t* q_counts, int32_t n, int32_t sets,
+                    int32_t* status, int32_t code, int32_t* counts_clamped, fvo_stream stream) {
+  if (!c) return -1;
+  if (n < 0 || sets < 1 || sets > 8) return fvo_fail(c, "count_guard: n < 0 or sets outside [1, 8]");
+  if (n == 0) return 0;
+  if (!counts) return fvo_fail(c, "null pointer argument");
+  return count_guard_run(c, counts, q_counts, n, sets, status, code, counts_clamped, (hipStream_t)stream);
+}
+
 int64_t fvo_voxel_workspace_bytes(int64_t n_points) {
   if (n_points < 1 || n_points > INT32_MAX) return -1;
   return voxel_workspace_bytes(n_points);

@@ -527,8 +527,8 @@ __global__ void k_em_prep(const float* __restrict__ p0all, const float* __restri
 //   k_em_roots  16-lane row per subset, lane i = root i: Durand-Kerner on det B(z) (300
 //               sweeps unless the roots stop moving -- OpenCV's rule, so almost always 300) with
 //               the Gauss-Seidel sweep's products split over the lanes, then the models.
-//   k_em_hyp    every model of 64 subsets scored over the points in LDS, the (subset, model)
-//               pairs spread evenly over the lanes.
+//   k_em_hyp    every model of 64 subsets scored over the points in LDS: the (subset, model)
+//               pairs spread over a 256-thread block, 4 lanes per pair splitting the points.
 // Before: one lane ran five_point() whole (1.9 KB of scratch per lane for the 10x20 matrix and
 // the root array, 1 wave per SIMD) -- 13 ms per 64 frames; then a lane per subset ran the whole
 // Durand-Kerner sweep (one wave's 300-sweep chain per launch) -- 4.1 ms.
@@ -764,6 +764,14 @@ __device__ __forceinline__ double row_max(double m) {
   return fmax(m, dpp_d<0x140>(m));
 }
 
+// den * (p - r), skipped when p - r is exactly 0 (solvePoly's test), without a branch
+__device__ __forceinline__ Cx dk_factor(Cx den, Cx p, Cx r) {
+  const Cx d{p.re - r.re, p.im - r.im};
+  const Cx m = cmul(den, d);
+  const bool nz = d.re != 0 || d.im != 0;
+  return {nz ? m.re : den.re, nz ? m.im : den.im};
+}
+
 template <bool FULL>
 __device__ __forceinline__ void dk_sweeps(Cx (&R)[10], Cx& own, const double (&cc)[11], int n, int l, bool mine) {
   for (int iter = 0; iter < 300; ++iter) {
@@ -782,19 +790,13 @@ __device__ __forceinline__ void dk_sweeps(Cx (&R)[10], Cx& own, const double (&c
         if (mine && l == i) {
 #pragma unroll
           for (int j = i + 1; j < 10; ++j)
-            if (FULL || j < n) {
-              const Cx d{p.re - R[j].re, p.im - R[j].im};
-              if (d.re != 0 || d.im != 0) den = cmul(den, d);
-            }
+            if (FULL || j < n) den = dk_factor(den, p, R[j]);
           const Cx q = cdiv(num, den);
           own = {p.re - q.re, p.im - q.im};
           mx = q.re * q.re + q.im * q.im;
         }
         R[i] = row_bcast(own, i);
-        if (mine && l > i) {
-          const Cx d{p.re - R[i].re, p.im - R[i].im};
-          if (d.re != 0 || d.im != 0) den = cmul(den, d);
-        }
+        if (mine && l > i) den = dk_factor(den, p, R[i]);
       }
     }
     // the sweep's max |step|^2 (fmax: order-free and NaN-ignoring like the serial fold)
@@ -887,42 +889,51 @@ __global__ __launch_bounds__(64) void k_em_roots(int maxIters, int it_lo, const 
 
 // Scoring: every (subset, model) pair of the block's 64 subsets spread evenly over the lanes,
 // the points staged in LDS.
-__global__ __launch_bounds__(64) void k_em_hyp(const double* __restrict__ xn, int cap, float thr2, int maxIters,
-                                               int it_lo, const EmState* __restrict__ state,
-                                               const double* __restrict__ models, int32_t* __restrict__ good,
-                                               const int8_t* __restrict__ nmod) {
+constexpr int EM_SC_THREADS = 256, EM_SC_PARTS = 4;  // scoring block; lanes per (subset, model) pair
+__global__ __launch_bounds__(EM_SC_THREADS) void k_em_hyp(const double* __restrict__ xn, int cap, float thr2,
+                                                          int maxIters, int it_lo, const EmState* __restrict__ state,
+                                                          const double* __restrict__ models,
+                                                          int32_t* __restrict__ good, const int8_t* __restrict__ nmod) {
   extern __shared__ __attribute__((aligned(16))) double sx[];  // [n][4]
-  __shared__ int mlist[640];                                   // (lane << 4 | model) of the wave's models
-  const int b = blockIdx.y, lane = threadIdx.x;
-  const int it = it_lo + blockIdx.x * 64 + lane;
+  __shared__ int mlist[640];                                   // (subset << 4 | model) of the block's models
+  __shared__ int s_total;
+  const int b = blockIdx.y, tid = threadIdx.x;
   const EmState st = state[b];
   const int n = st.n;
   if (n < 5 || it_lo + (int)blockIdx.x * 64 >= min(st.niters, maxIters)) return;  // block-uniform
   const double* x = xn + (int64_t)b * cap * 4;
-  for (int i = lane; i < 4 * n; i += 64) sx[i] = x[i];
-  const bool active = em_active(st, it, maxIters);
-  const int count = active ? (int)nmod[(int64_t)b * maxIters + it] : 0;
-  // spread the wave's (subset, model) pairs over the lanes: exclusive scan of the counts
-  int off = count;
+  for (int i = tid; i < 4 * n; i += EM_SC_THREADS) sx[i] = x[i];
+  if (tid < 64) {  // the block's 64 subsets: exclusive scan of their model counts
+    const int it = it_lo + blockIdx.x * 64 + tid;
+    const int count = em_active(st, it, maxIters) ? (int)nmod[(int64_t)b * maxIters + it] : 0;
+    int off = count;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int t = __shfl_up(off, d, 64);
-    if (lane >= d) off += t;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int t = __shfl_up(off, d, 64);
+      if (tid >= d) off += t;
+    }
+    if (tid == 63) s_total = off;
+    off -= count;
+    for (int k = 0; k < count; ++k) mlist[off + k] = (tid << 4) | k;
   }
-  const int total = __shfl(off, 63, 64);
-  off -= count;
-  for (int k = 0; k < count; ++k) mlist[off + k] = (lane << 4) | k;
   __syncthreads();
-  for (int m = lane; m < total; m += 64) {
-    const int who = mlist[m] >> 4, k = mlist[m] & 15;
+  // EM_SC_PARTS consecutive lanes per pair, each counting every EM_SC_PARTS-th point (integer
+  // counts: the sum is order-free)
+  const int total = s_total, part = tid % EM_SC_PARTS;
+  for (int m0 = tid / EM_SC_PARTS; m0 < total; m0 += EM_SC_THREADS / EM_SC_PARTS) {  // uniform per pair's lanes
+    const int ml = mlist[m0];
+    const int who = ml >> 4, k = ml & 15;
     const int64_t s2 = (int64_t)b * maxIters + it_lo + blockIdx.x * 64 + who;
     const double* mE = models + s2 * 90 + k * 9;
     double E[9];
 #pragma unroll
     for (int q = 0; q < 9; ++q) E[q] = mE[q];
     int g = 0;
-    for (int i = 0; i < n; ++i) g += em_error(E, sx[4 * i], sx[4 * i + 1], sx[4 * i + 2], sx[4 * i + 3]) <= thr2;
-    good[s2 * 10 + k] = g;
+    for (int i = part; i < n; i += EM_SC_PARTS)
+      g += em_error(E, sx[4 * i], sx[4 * i + 1], sx[4 * i + 2], sx[4 * i + 3]) <= thr2;
+#pragma unroll
+    for (int o = 1; o < EM_SC_PARTS; o <<= 1) g += __shfl_xor(g, o, EM_SC_PARTS);
+    if (part == 0) good[s2 * 10 + k] = g;
   }
 }
 
@@ -937,7 +948,7 @@ __global__ __launch_bounds__(64) void k_em_replay(int maxIters, int it_lo, int i
   if (st.n < 6) return;
   for (int base = it_lo; base < it_hi && base < st.niters; base += 64) {
     const int it = base + lane;
-    int nm = 0, g[10];
+    int nm = 0, g[10], gmax = -1;
 #pragma unroll
     for (int k = 0; k < 10; ++k) g[k] = 0;
     if (it < it_hi && it < st.niters) {
@@ -945,10 +956,16 @@ __global__ __launch_bounds__(64) void k_em_replay(int maxIters, int it_lo, int i
       nm = nmod[slot];
 #pragma unroll
       for (int k = 0; k < 10; ++k)
-        if (k < nm) g[k] = good[slot * 10 + k];
+        if (k < nm) {
+          g[k] = good[slot * 10 + k];
+          gmax = max(gmax, g[k]);
+        }
     }
     for (int j = 0; j < 64; ++j) {
       if (base + j >= it_hi || base + j >= st.niters) break;
+      // an iteration whose best model does not beat the current record changes nothing: only
+      // the (rare) record-setting iterations walk their models one by one
+      if (__builtin_amdgcn_readlane(gmax, j) <= max(st.maxGood, 4)) continue;
       const int nmj = __builtin_amdgcn_readlane(nm, j);
 #pragma unroll
       for (int k = 0; k < 10; ++k) {
@@ -1113,7 +1130,7 @@ int essential_run(fvo_ctx* ctx, const float* p0, const float* p1, const int32_t*
     hipLaunchKernelGGL(k_em_elim, dim3((nit + 3) / 4, batch), dim3(64), 0, s, maxIters, lo, st, ctx->em_ws);
     hipLaunchKernelGGL(k_em_roots, dim3((nit + EM_GPW - 1) / EM_GPW, batch), dim3(64), 0, s, maxIters, lo, st,
                        ctx->em_ws, ctx->em_models, ctx->em_nmod);
-    hipLaunchKernelGGL(k_em_hyp, dim3((nit + 63) / 64, batch), dim3(64), shm, s, ctx->em_x, cap, thr2, maxIters, lo,
+    hipLaunchKernelGGL(k_em_hyp, dim3((nit + 63) / 64, batch), dim3(EM_SC_THREADS), shm, s, ctx->em_x, cap, thr2, maxIters, lo,
                        st, ctx->em_models, ctx->em_good, ctx->em_nmod);
     hipLaunchKernelGGL(k_em_replay, dim3(batch), dim3(64), 0, s, maxIters, lo, hi, prob, ctx->em_good, ctx->em_nmod,
                        st);

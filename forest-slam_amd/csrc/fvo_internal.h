@@ -167,6 +167,12 @@ int map_transform_run(fvo_ctx* ctx, const float* pts, int stride, const int32_t*
                       const double* T, int32_t* count, int64_t map_cap, double* out64, float* out32, hipStream_t s);
 int chain_poses_run(fvo_ctx* ctx, const double* T, const int32_t* status, const int32_t* npts, int n_seq, int n,
                     double* cum, double* cum_out, int32_t* npts_out, hipStream_t s);
+struct FvoRegions {
+  fvo_region r[FVO_MAX_REGIONS];
+};
+int copy_regions_run(fvo_ctx* ctx, int count, const fvo_region* regions, hipStream_t s);
+int count_guard_run(fvo_ctx* ctx, const int32_t* cnt, const int32_t* q_cnt, int n, int sets, int32_t* status,
+                    int32_t code, int32_t* nkp_out, hipStream_t s);
 int64_t voxel_workspace_bytes(int64_t n);
 int voxel_run(fvo_ctx* ctx, const double* pts, int64_t n, double voxel, void* ws, size_t ws_bytes, double* out,
               int32_t* n_out, int32_t* status, hipStream_t s);

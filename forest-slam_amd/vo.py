@@ -165,34 +165,27 @@ class StereoFrontEnd:
                 L.record_stream(fs)
                 R.record_stream(fs)
         with torch.cuda.stream(fs):
-            # ---- front stage: SGBM of the previous pairs (needs only images), ORB + BF
-            disp = self._front_sgbm(L, R, n)
-            self.imgs[:n].copy_(L)
-            self.imgs[n:2 * n].copy_(R)
+            # ---- front stage: SGBM of the previous pairs (needs only images), ORB + BF.  The
+            # step's buffer moves go in three batched launches (fvo_copy_regions) instead of a
+            # dozen separate copies: (A) the SGBM pairs and the ORB images, (B) after ORB the
+            # query sets (previous descriptors / counts / keypoints) and the last images,
+            # (C) after BF the last frame's keypoints / descriptors / counts
+            ctx.copy_regions(self._sgbm_pairs(L, R, n) + [(self.imgs[:n], L), (self.imgs[n:2 * n], R)])
+            disp = ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n])
             kp, desc, cnt = ctx.orb(self.imgs[:2 * n], out=(self.kp[:2 * n], self.desc[:2 * n], self.cnt[:2 * n]))
-            # query (previous) descriptor sets: left frames then right frames
-            self.q_desc[0].copy_(self.last_desc[0])
-            self.q_cnt[0:1].copy_(self.last_cnt[0:1])
-            if n > 1:
-                self.q_desc[1:n].copy_(desc[:n - 1])
-                self.q_cnt[1:n].copy_(cnt[:n - 1])
-            self.q_desc[n].copy_(self.last_desc[1])
-            self.q_cnt[n:n + 1].copy_(self.last_cnt[1:2])
-            if n > 1:
-                self.q_desc[n + 1:2 * n].copy_(desc[n:2 * n - 1])
-                self.q_cnt[n + 1:2 * n].copy_(cnt[n:2 * n - 1])
+            # query (previous) sets: left frames then right frames; previous-left keypoints
+            ctx.copy_regions([(self.q_desc[0], self.last_desc[0]), (self.q_cnt[0:1], self.last_cnt[0:1]),
+                              (self.q_desc[1:n], desc[:n - 1]), (self.q_cnt[1:n], cnt[:n - 1]),
+                              (self.q_desc[n], self.last_desc[1]), (self.q_cnt[n:n + 1], self.last_cnt[1:2]),
+                              (self.q_desc[n + 1:2 * n], desc[n:2 * n - 1]), (self.q_cnt[n + 1:2 * n], cnt[n:2 * n - 1]),
+                              (self.q_kp[0], self.last_kp), (self.q_kp[1:n], kp[:n - 1]),
+                              (self.sg_lastL, L[n - 1]), (self.sg_lastR, R[n - 1])])
             nb = 2 * n if self.match_right else n
             m, nm = ctx.bf_match(self.q_desc[:nb], self.q_cnt[:nb], desc[:nb], cnt[:nb],
                                  out=(self.matches[:nb], self.nmatch[:nb]))
-            # previous-left keypoints for back-projection
-            self.q_kp[0].copy_(self.last_kp)
-            if n > 1:
-                self.q_kp[1:n].copy_(kp[:n - 1])
-            self.last_kp.copy_(kp[n - 1])
-            self.last_desc[0].copy_(desc[n - 1])
-            self.last_desc[1].copy_(desc[2 * n - 1])
-            self.last_cnt[0:1].copy_(cnt[n - 1:n])
-            self.last_cnt[1:2].copy_(cnt[2 * n - 1:2 * n])
+            ctx.copy_regions([(self.last_kp, kp[n - 1]), (self.last_desc[0], desc[n - 1]),
+                              (self.last_desc[1], desc[2 * n - 1]), (self.last_cnt[0:1], cnt[n - 1:n]),
+                              (self.last_cnt[1:2], cnt[2 * n - 1:2 * n])])
         if self.overlap_sgbm:
             main.wait_stream(fs)
         # ---- back stage: back-projection, PnP, local BA
@@ -203,11 +196,12 @@ class StereoFrontEnd:
                                                self.inl[:n]))
         # ORB writes -(needed) when a frame has more keypoints than kp_capacity (its outputs
         # are then unspecified): mark the frame STATUS_KP_OVERFLOW instead of letting it pass
-        # as a "fewer than 6 points" skip (device-side, no host sync)
-        over = (cnt[:n] < 0) | (self.q_cnt[:n] < 0)
-        if self.match_right:  # the right sets feed bf_match too
-            over |= (cnt[n:2 * n] < 0) | (self.q_cnt[n:2 * n] < 0)
-        st.masked_fill_(over, STATUS_KP_OVERFLOW)
+        # as a "fewer than 6 points" skip (device-side, no host sync; the right sets feed
+        # bf_match too).  An overflowed frame enters the BA history as a frame without
+        # keypoints (clamped count): the BA kernels never see a negative count.
+        ctx.count_guard(cnt, n, 2 if self.match_right else 1, q_counts=self.q_cnt, status=st,
+                        code=STATUS_KP_OVERFLOW,
+                        clamped_out=self.hnkp[self.ba_window - 1:self.ba_window - 1 + n] if self.ba_window else None)
         out = T
         if self.ba_window:
             out = self._local_ba(n, kp, cnt, m, nm, disp, T)
@@ -216,16 +210,11 @@ class StereoFrontEnd:
         self.k += 1
         return out, st
 
-    def _front_sgbm(self, L, R, n):
-        """SGBM of the step's previous pairs (the last pair of the previous step, then L/R[:n-1])."""
-        self.prevL[0].copy_(self.sg_lastL)
-        self.prevR[0].copy_(self.sg_lastR)
-        if n > 1:
-            self.prevL[1:n].copy_(L[:n - 1])
-            self.prevR[1:n].copy_(R[:n - 1])
-        self.sg_lastL.copy_(L[n - 1])
-        self.sg_lastR.copy_(R[n - 1])
-        return self.ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n])
+    def _sgbm_pairs(self, L, R, n):
+        """Copy list for SGBM's previous pairs (the last pair of the previous step, then
+        L/R[:n-1])."""
+        return [(self.prevL[0], self.sg_lastL), (self.prevR[0], self.sg_lastR),
+                (self.prevL[1:n], L[:n - 1]), (self.prevR[1:n], R[:n - 1])]
 
     def _select(self, slot: int):
         """Point the per-step buffer names at one of the two slots."""
@@ -237,25 +226,24 @@ class StereoFrontEnd:
     def _local_ba(self, n, kp, cnt, m, nm, disp, T):
         Kw, ctx = self.ba_window, self.ctx
         a, b = Kw - 2, Kw - 1  # first pair slot, first new-frame slot
-        self.hkp[b:b + n].copy_(kp[:n])
-        # an overflowed frame (count -(needed), outputs unspecified) enters the BA history as a
-        # frame without keypoints: the BA kernels never see a negative count
-        self.hnkp[b:b + n].copy_(cnt[:n].clamp(min=0))
-        self.hmatch[a:a + n].copy_(m[:n])
-        self.hnmatch[a:a + n].copy_(nm[:n])
-        self.hT[a:a + n].copy_(T[:n])
+        # (hnkp[b:b+n], the clamped counts, came from count_guard)
+        ctx.copy_regions([(self.hkp[b:b + n], kp[:n]), (self.hmatch[a:a + n], m[:n]),
+                          (self.hnmatch[a:a + n], nm[:n]), (self.hT[a:a + n], T[:n])])
         ctx.keypoint_stereo(disp[:n], self.q_kp[:n], self.hnkp[a:a + n], self.K, self.baseline,
                             out=self.hstereo[a:a + n])
         F = b + n
         Tba, _ = ctx.ba_windows(self.hkp[:F], self.hnkp[:F], self.hmatch[:F], self.hnmatch[:F], self.hstereo[:F],
                                 self.hT[:F], b, n, self.valid_from, self.K, self.baseline, iterations=self.ba_iters,
                                 out=(self.T_ba[:n], self.ba_stats[:n]))
-        # slide the history: frames [n, n+K-1) -> [0, K-1), pair data [n, n+K-2) -> [0, K-2)
-        self.hkp[:b].copy_(self.hkp[n:n + b].clone())
-        self.hnkp[:b].copy_(self.hnkp[n:n + b].clone())
-        if a > 0:
-            for t in (self.hmatch, self.hnmatch, self.hstereo, self.hT):
-                t[:a].copy_(t[n:n + a].clone())
+        # slide the history: frames [n, n+K-1) -> [0, K-1), pair data [n, n+K-2) -> [0, K-2);
+        # one launch when source and destination do not overlap (n >= K-1), else via clones
+        slides = [(self.hkp, b), (self.hnkp, b)] + ([(t, a) for t in (self.hmatch, self.hnmatch, self.hstereo, self.hT)]
+                                                    if a > 0 else [])
+        if n >= b:
+            ctx.copy_regions([(t[:k], t[n:n + k]) for t, k in slides])
+        else:
+            for t, k in slides:
+                t[:k].copy_(t[n:n + k].clone())
         self.valid_from = max(0, self.valid_from - n)
         return Tba
 

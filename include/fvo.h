@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define FVO_ABI_VERSION 5
+#define FVO_ABI_VERSION 6
 
 typedef struct fvo_ctx fvo_ctx;
 typedef void* fvo_stream; /* hipStream_t */
@@ -286,6 +286,26 @@ int fvo_map_transform(fvo_ctx* ctx, const float* points, int32_t point_stride, c
  * n_points may be NULL (n_points_out then NULL too). */
 int fvo_chain_poses(fvo_ctx* ctx, const double* T, const int32_t* status, const int32_t* n_points, int32_t n_seq,
                     int32_t n, double* cum_state, double* cum_out, int32_t* n_points_out, fvo_stream stream);
+
+/* Step bookkeeping in one launch each (no reference call: the reference keeps these per frame
+ * as Python lists; a batched front end would otherwise issue a dozen small copies and
+ * elementwise ops per step, each a separate dispatch).  Any stage; no workspace.
+ * fvo_copy_regions: `count` (0..FVO_MAX_REGIONS) device-to-device copies of regions[i].bytes
+ * from regions[i].src to regions[i].dst, in one launch.  No region's destination may overlap
+ * another region's source or destination, or its own source (refused: copy through a
+ * temporary).  The region array is host memory, read before the call returns.
+ * fvo_count_guard: for i < n, status[i] = code when any of counts[s*n + i] or
+ * q_counts[s*n + i] (s < sets; q_counts may be NULL) is negative -- ORB's -(needed) overflow
+ * report; counts_clamped[i] = max(counts[i], 0) (status and counts_clamped may be NULL). */
+#define FVO_MAX_REGIONS 32
+typedef struct {
+  void* dst;
+  const void* src;
+  int64_t bytes;
+} fvo_region;
+int fvo_copy_regions(fvo_ctx* ctx, int32_t count, const fvo_region* regions, fvo_stream stream);
+int fvo_count_guard(fvo_ctx* ctx, const int32_t* counts, const int32_t* q_counts, int32_t n, int32_t sets,
+                    int32_t* status, int32_t code, int32_t* counts_clamped, fvo_stream stream);
 
 int64_t fvo_voxel_workspace_bytes(int64_t n_points);
 int fvo_voxel_down_sample(fvo_ctx* ctx, const double* points, int64_t n_points, double voxel_size, void* workspace,

@@ -168,6 +168,29 @@ int main() {
   reset(); rejected(c, fvo_chain_poses(c, f64, i32, nullptr, -1, 3, f64, f64, nullptr, nullptr));
   reset(); CHECK(fvo_chain_poses(c, f64, i32, nullptr, 0, 3, f64, f64, nullptr, nullptr) == 0 && g_last_launch.empty());
   reset(); reached(fvo_chain_poses(c, f64, i32, i32, 2, 3, f64, f64, i32, nullptr), "chain_poses_run");
+  {  // step bookkeeping: region count / overlap validation, count guard ranges
+    static char buf[4096];
+    fvo_region r[FVO_MAX_REGIONS + 1];
+    for (int i = 0; i <= FVO_MAX_REGIONS; ++i) r[i] = fvo_region{buf + 64 * i, buf + 3000, 16};
+    reset(); rejected(c, fvo_copy_regions(c, FVO_MAX_REGIONS + 1, r, nullptr));
+    reset(); rejected(c, fvo_copy_regions(c, 2, nullptr, nullptr));
+    reset(); CHECK(fvo_copy_regions(c, 0, nullptr, nullptr) == 0 && g_last_launch.empty());
+    reset(); reached(fvo_copy_regions(c, 2, r, nullptr), "copy_regions_run");
+    fvo_region ov[2] = {{buf, buf + 8, 16}, {buf + 100, buf + 200, 16}};  // own source overlaps
+    reset(); rejected(c, fvo_copy_regions(c, 2, ov, nullptr));
+    fvo_region dd[2] = {{buf, buf + 1000, 16}, {buf + 8, buf + 2000, 16}};  // destinations overlap
+    reset(); rejected(c, fvo_copy_regions(c, 2, dd, nullptr));
+    fvo_region xs[2] = {{buf, buf + 1000, 16}, {buf + 1000, buf + 2000, 16}};  // dst 0 = src 0? no: dst 1 = src 0
+    reset(); rejected(c, fvo_copy_regions(c, 2, xs, nullptr));
+    fvo_region nb[1] = {{buf, buf + 100, -1}};
+    reset(); rejected(c, fvo_copy_regions(c, 1, nb, nullptr));
+    fvo_region z[1] = {{nullptr, nullptr, 0}};  // empty regions are skipped
+    reset(); CHECK(fvo_copy_regions(c, 1, z, nullptr) == 0 && g_last_launch.empty());
+    reset(); rejected(c, fvo_count_guard(c, i32, i32, 4, 0, i32, -3, nullptr, nullptr));
+    reset(); rejected(c, fvo_count_guard(c, nullptr, i32, 4, 1, i32, -3, nullptr, nullptr));
+    reset(); CHECK(fvo_count_guard(c, i32, nullptr, 0, 1, nullptr, -3, nullptr, nullptr) == 0 && g_last_launch.empty());
+    reset(); reached(fvo_count_guard(c, i32, nullptr, 4, 2, i32, -3, i32, nullptr), "count_guard_run");
+  }
   CHECK(fvo_voxel_workspace_bytes(0) == -1 && fvo_voxel_workspace_bytes(10) > 0);
   reset(); rejected(c, fvo_voxel_down_sample(c, f64, 10, 0.0, u8, 1 << 16, f64, i32, i32, nullptr));
   reset(); rejected(c, fvo_voxel_down_sample(c, f64, 10, 0.5, u8, -1, f64, i32, i32, nullptr));

@@ -107,6 +107,10 @@ int chain_poses_run(fvo_ctx*, const double*, const int32_t*, const int32_t*, int
                     hipStream_t) {
   return hit("chain_poses_run");
 }
+int copy_regions_run(fvo_ctx*, int, const fvo_region*, hipStream_t) { return hit("copy_regions_run"); }
+int count_guard_run(fvo_ctx*, const int32_t*, const int32_t*, int, int, int32_t*, int32_t, int32_t*, hipStream_t) {
+  return hit("count_guard_run");
+}
 int64_t voxel_workspace_bytes(int64_t n) { return 64 * n + 4096; }
 int voxel_run(fvo_ctx*, const double*, int64_t, double, void*, size_t, double*, int32_t*, int32_t*, hipStream_t) {
   return hit("voxel_run");

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(path)
     missing = [n for n in _declared() if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.fvo_abi_version() == 5
+    assert lib.fvo_abi_version() == 6
 
 
 def test_binding_signatures_cover_header():

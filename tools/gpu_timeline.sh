@@ -13,5 +13,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d /tmp/tl -o tl 
   python3 "$root/bench.py" --steps 10 --warmup 3 --cpu-frames 0 --ate-frames 0 "$@" > /tmp/tl.out 2>&1
 cd "$root"
 f=$(find /tmp/tl -name "*kernel_trace.csv" | head -1)
-python3 tools/timeline.py "$f" --last-ms 120 --calls "${TL_CALLS:-k_pnp}" > gpurun_out/tl/timeline.txt
+python3 tools/timeline.py "$f" --last-ms 120 --calls "${TL_CALLS:-k_pnp}" --queue "${TL_QUEUE:-}" > gpurun_out/tl/timeline.txt
 grep '^{' /tmp/tl.out > gpurun_out/tl/bench_under_trace.json || true

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--gaps", type=int, default=12)
     ap.add_argument("--kernels", type=int, default=40, help="per-kernel totals over the window (0: none)")
     ap.add_argument("--calls", default="", help="substring: list each call of matching kernels in the last 2 windows/10")
+    ap.add_argument("--queue", default="", help="with --calls: only this queue's calls")
     a = ap.parse_args()
     rows = load(a.csv)
     t_end = max(r[1] for r in rows)
@@ -61,7 +62,7 @@ def main():
         for s, e, qq, n in rows:
             if qq == q:
                 names[n] += e - s
-        top = ", ".join(f"{k} {v / 1e6:.1f}" for k, v in sorted(names.items(), key=lambda kv: -kv[1])[:6])
+        top = ", ".join(f"{k} {v / 1e6:.1f}" for k, v in sorted(names.items(), key=lambda kv: -kv[1])[:12])
         print(f"queue {q}: busy {b / 1e6:.2f} ms  [{top}]")
     print(f"overlap (>=2 queues busy, 2-queue estimate): {both / 1e6:.2f} ms")
     gaps = []
@@ -77,7 +78,7 @@ def main():
     for g, p, n in gaps[:a.gaps]:
         print(f"  {g / 1e3:8.1f} us  after {p}  before {n}")
     if a.calls:
-        calls(rows, a.calls, int(a.last_ms * 1e6 / 5))
+        calls(rows, a.calls, int(a.last_ms * 1e6 / 5), a.queue)
     if a.kernels:
         tot = defaultdict(lambda: [0, 0])
         for s, e, _, n in rows:
@@ -88,10 +89,10 @@ def main():
             print(f"{n:48s} {c:6d} {t / 1e6:8.2f} ms {t / c / 1e3:9.1f} us")
 
 
-def calls(rows, pat, span_ns):
+def calls(rows, pat, span_ns, queue=""):
     t_hi = max(r[1] for r in rows)
     t_lo = t_hi - span_ns
-    sel = [r for r in rows if pat in r[3] and r[0] >= t_lo]
+    sel = [r for r in rows if (pat == "*" or pat in r[3]) and r[0] >= t_lo and (not queue or r[2] == queue)]
     print(f"calls of *{pat}* in the last {span_ns / 1e6:.1f} ms (start offset, duration, what else ran):")
     for s, e, q, n in sel:
         other = defaultdict(int)
