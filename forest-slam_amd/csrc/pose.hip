@@ -1443,7 +1443,14 @@ __global__ __launch_bounds__(64) void k_pnp_hyp_a(int maxIters, int batch, const
   });
 }
 
-__global__ __launch_bounds__(64) void k_pnp_hyp_b(const float* __restrict__ P3all, const float* __restrict__ p2all,
+// Register budgets (hyp_b <= 168 VGPRs, 416 B of scratch; refine <= 256, 1040 B): in the
+// overlapped pipeline this stage runs beside the disparity kernels, whose waves hold 128 VGPRs
+// each, and a wave needing more than a few of their slots on one SIMD waits for them to drain
+// (hyp_b at 276 registers: 2.6-3.4 ms per launch beside k_sg_rows).  Measured (bench.py, 20
+// steps, 2 runs each): unbounded 5110 frames/s; hyp_b at 256 / 168 / 128 VGPRs 5130 / 5177 /
+// 5173; then refine at 256 / 168 VGPRs 5237 / 5222 (in-order PnP 1.57 -> 1.73 ms).  Forcing
+// k_ba_build (512 threads) to 128 VGPRs instead collapsed the overlapped step (21 ms).
+__global__ __launch_bounds__(64, 3) void k_pnp_hyp_b(const float* __restrict__ P3all, const float* __restrict__ p2all,
                                                   int cap, Cam K, float thr2, int maxIters, int batch,
                                                   const int32_t* __restrict__ plan,
                                                   const PnpState* __restrict__ state, const double* __restrict__ ws,
@@ -1528,7 +1535,7 @@ __global__ __launch_bounds__(64) void k_pnp_replay(int maxIters, int it_lo, int 
   if (lane == 0) state[b] = st;
 }
 
-__global__ __launch_bounds__(64) void k_pnp_refine(const float* __restrict__ P3all, const float* __restrict__ p2all,
+__global__ __launch_bounds__(64, 2) void k_pnp_refine(const float* __restrict__ P3all, const float* __restrict__ p2all,
                                                    int cap, Cam K, float thr2, int maxIters,
                                                    const PnpState* __restrict__ state,
                                                    const double* __restrict__ model, double* __restrict__ rvec,

@@ -12,7 +12,9 @@
 
 namespace {
 
-__global__ __launch_bounds__(256) void k_copy_regions(FvoRegions r) {
+// single-wave blocks: the back stage issues these beside the front stage's kernels, and a
+// one-wave block needs one free wave slot, not four on the same CU
+__global__ __launch_bounds__(64) void k_copy_regions(FvoRegions r) {
   const fvo_region g = r.r[blockIdx.y];
   const uint8_t* src = static_cast<const uint8_t*>(g.src);
   uint8_t* dst = static_cast<uint8_t*>(g.dst);
@@ -51,17 +53,16 @@ int copy_regions_run(fvo_ctx* ctx, int count, const fvo_region* regions, hipStre
     r.r[i] = regions[i];
     most = std::max(most, regions[i].bytes);
   }
-  // enough blocks for the largest region at 16 B per thread, at most 1024 per region
-  const int64_t bx = std::min<int64_t>(1024, std::max<int64_t>(1, (most / 16 + 255) / 256));
-  hipLaunchKernelGGL(k_copy_regions, dim3((unsigned)bx, count), dim3(256), 0, s, r);
+  // enough blocks for the largest region at 16 B per thread, at most 4096 per region
+  const int64_t bx = std::min<int64_t>(4096, std::max<int64_t>(1, (most / 16 + 63) / 64));
+  hipLaunchKernelGGL(k_copy_regions, dim3((unsigned)bx, count), dim3(64), 0, s, r);
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }
 
 int count_guard_run(fvo_ctx* ctx, const int32_t* cnt, const int32_t* q_cnt, int n, int sets, int32_t* status,
                     int32_t code, int32_t* nkp_out, hipStream_t s) {
-  hipLaunchKernelGGL(k_count_guard, dim3((n + 255) / 256), dim3(256), 0, s, cnt, q_cnt, n, sets, status, code,
-                     nkp_out);
+  hipLaunchKernelGGL(k_count_guard, dim3((n + 63) / 64), dim3(64), 0, s, cnt, q_cnt, n, sets, status, code, nkp_out);
   FVO_LAUNCH_CHECK(ctx);
   return 0;
 }
