@@ -12,8 +12,10 @@ of the last K = 10 frames of every frame (north_star "extract+match+local-BA"). 
 one batch of B consecutive frames of the rank's own sequence (seed = rank), inputs
 resident in HBM before timing.
 Multi-GPU: one sequence per GPU (weak scaling); the data-path collective is the per-step
-map exchange (RCCL all-gather of the step's refined poses and the latest keyframe
-window's landmarks, ~100 KB per rank), plus the timing barrier / max-over-ranks.
+map exchange (RCCL all-gather of every rank's step poses, statuses and every posed frame's
+points3D, dist.exchange_frame_map, placed on the device by dist.GlobalMap), plus the timing
+barrier / max-over-ranks.  `--gpus N` without WORLD_SIZE starts the N ranks itself
+(torch.distributed.run, 127.0.0.1) before any GPU call.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement for the roofline definition.
 """
@@ -235,9 +237,9 @@ def pmc_mfma(shape: str, kernel: str = "k_ba_lin"):
     command)."""
     rows, src = _pmc_rows("mfma_per_kernel.csv", shape)
     for row in rows:
-        if row["kernel"] == kernel:
+        if row["kernel"] == kernel or row["kernel"].startswith(kernel + "<"):  # k_ba_lin<MAXT> (r4)
             tf = float(row["f64_mfma_tflops"])
-            return {"kernel": kernel, "dtype": "f64", "mfma_util": float(row["mfma_util"]),
+            return {"kernel": row["kernel"], "dtype": "f64", "mfma_util": float(row["mfma_util"]),
                     "achieved_tflops": tf, "peak_tflops": F64_MFMA_PEAK_TFLOPS,
                     "frac": round(tf / F64_MFMA_PEAK_TFLOPS, 4),
                     "flops_per_launch": float(row["avg_f64_mfma_flops"]),
@@ -540,8 +542,8 @@ def main():
         gm = rank_step.gmap.flush()
         torch.cuda.synchronize()
         global_map = {"points": len(gm), "sequences": world, "steps_placed": rank_step.gmap.steps,
-                      "what": "every posed frame's points3D of every rank, all-gathered over RCCL each step and "
-                              "placed on the device with each sequence's chained poses (dist.GlobalMap: "
+                      "what": f"every posed frame's points3D of every rank, all-gathered over {rk.backend} each "
+                              "step and placed on the device with each sequence's chained poses (dist.GlobalMap: "
                               "fvo_chain_poses + fvo_map_transform)"}
     frames = world * B * args.steps
     value = frames / elapsed
