@@ -45,6 +45,9 @@ struct BaCam {
 };
 
 constexpr int kKMax = 21;
+// parallel problem construction scratch per window (ints): births per birth frame [kKMax],
+// their observations [kKMax], created landmarks / observations [2], observations per frame [kKMax]
+constexpr int kBldL = 0, kBldO = kKMax, kBldTot = 2 * kKMax, kBldF = 2 * kKMax + 2, kBldInts = 3 * kKMax + 2;
 constexpr int kBlock = 256;
 // k_ba_lin: blocks per window NPART = (chunk capacity) / kLinChunksPerPart, clamped to [1,
 // kLinParts]; block p reduces the landmark chunks p, p + NPART, ...
@@ -79,13 +82,13 @@ struct BaState {
 
 struct BaDims {
   int Lmax, Omax, K, cap, NR, LPC, NCH, NCU, NPART, LPU, NCUP;
-  int64_t oSt, oX0, oX1, oL, oG, oLs, oObs, oFl, oGp, oCp, oNext, oHdr, win;
+  int64_t oSt, oX0, oX1, oL, oG, oLs, oObs, oFl, oGp, oCp, oNext, oHdr, oBld, win;
 };
 
 struct BaWin {
   BaState* st;
   double *X0, *X1, *Lf, *gl, *Gp, *cp;
-  int *lstart, *flist, *next, *hdr;
+  int *lstart, *flist, *next, *hdr, *bld;
   BaObs* obs;
 };
 
@@ -104,6 +107,7 @@ __device__ __forceinline__ BaWin view(void* base, const BaDims& d, int w) {
   v.cp = (double*)(p + d.oCp);
   v.next = (int*)(p + d.oNext);
   v.hdr = (int*)(p + d.oHdr);
+  v.bld = (int*)(p + d.oBld);
   return v;
 }
 // hdr: [8 + f] per-frame observation list offsets
@@ -338,11 +342,13 @@ __device__ __forceinline__ bool ba_outlier(const double* T, const double* X, con
 }
 
 // ------------------------------------------------------------------ problem construction
-// One 512-thread block per window.  The forward match maps of the window's frames live in
-// LDS as u16 (LMAP; the global v.next copy when they do not fit), so following a track -- a
-// chain of dependent lookups up to K-1 long -- costs LDS latency, not L2 / HBM latency; each
-// candidate records its chain in registers on the first walk, and the keypoints along it are
-// then loaded all at once.
+// k_ba_build: one 512-thread block per window, birth frames in order.  Since r4 it runs only
+// when the window's u16 match maps do not fit in LDS (LMAP = false: the maps in the global
+// v.next copy); otherwise k_ba_births / k_ba_emit / k_ba_lists build the same problem on a
+// (window, frame) grid (below; 1080p 0.55 ms -> BA 5.0 -> 4.63 ms, 600p 1.86 -> 1.81 ms,
+// bit-identical results).  Following a track -- a chain of dependent lookups up to K-1 long --
+// costs LDS latency with the maps in LDS; each candidate records its chain in registers on
+// the first walk, and the keypoints along it are then loaded all at once.
 constexpr int kBuildBlock = 512;
 template <bool LMAP>
 __global__ __launch_bounds__(kBuildBlock) void k_ba_build(BaIn in, void* ws, BaDims dm, int first_end, int first_valid) {
@@ -552,6 +558,266 @@ __global__ __launch_bounds__(kBuildBlock) void k_ba_build(BaIn in, void* ws, BaD
     S->cost0 = 0.0;
   }
   for (int i = tid; i < n * 12; i += kBuildBlock) S->T[i / 12][i % 12] = sT[i / 12][i % 12];
+}
+
+// ---- parallel construction (r4): the same landmarks, ids, observations and per-frame lists
+// as k_ba_build<true>, from a (window, frame) grid instead of one block per window.  A
+// landmark is born at frame j from j's match rows alone (the tracked test reads frame j-1's
+// matches, the track follows the maps of frames j+1..), so every birth frame is counted and
+// emitted by its own block; the ids come from prefix sums over the birth frames, and the
+// lists per observed frame from a scan over the landmarks.  Creation stops at the first
+// candidate in (frame, row) order that does not fit: both prefix sums are monotone, so a
+// candidate is created iff its all-candidate prefixes fit -- the same set as the serial stop.
+constexpr int kBirthBlock = 256;
+
+struct BirthFrame {
+  int e, s, n, f, M;
+  const int32_t* m;
+};
+__device__ __forceinline__ BirthFrame birth_frame(const BaIn& in, const BaDims& dm, int w, int j, int first_end,
+                                                  int first_valid) {
+  BirthFrame b;
+  b.e = first_end + w;
+  b.s = max(first_valid, b.e - dm.K + 1);
+  b.n = b.e - b.s + 1;
+  b.f = b.s + j;
+  b.M = (b.n >= 3 && j + 1 < b.n) ? min(max(in.nmatch[b.f], 0), dm.cap) : 0;
+  b.m = in.matches + (int64_t)b.f * dm.cap * 3;
+  return b;
+}
+
+// the u16 forward maps of frames j+1 .. n-2 and frame j's tracked flags (from frame j-1's rows)
+__device__ void birth_maps(const BaIn& in, const BaDims& dm, const BirthFrame& b, int j, uint16_t* s_next,
+                           uint8_t* s_tr) {
+  const int cap = dm.cap, tid = threadIdx.x;
+  for (int k = j + 1; k + 1 < b.n; ++k)
+    for (int i = tid; i < cap; i += kBirthBlock) s_next[k * cap + i] = 0xFFFF;
+  for (int i = tid; i < cap; i += kBirthBlock) s_tr[i] = 0;
+  __syncthreads();
+  for (int k = j + 1; k + 1 < b.n; ++k) {
+    const int f = b.s + k, M = min(max(in.nmatch[f], 0), cap);
+    const int32_t* m = in.matches + (int64_t)f * cap * 3;
+    for (int r = tid; r < M; r += kBirthBlock) s_next[k * cap + m[3 * r]] = (uint16_t)m[3 * r + 1];
+  }
+  if (j > 0) {
+    const int Mp = min(max(in.nmatch[b.f - 1], 0), cap);
+    const int32_t* mp = in.matches + (int64_t)(b.f - 1) * cap * 3;
+    for (int r = tid; r < Mp; r += kBirthBlock) s_tr[mp[3 * r + 1]] = 1;
+  }
+  __syncthreads();
+}
+
+// row r of frame j: candidate test and track (len observations, keypoints bs[] in j+1, ...)
+__device__ __forceinline__ bool birth_track(const BaIn& in, const BaDims& dm, const BirthFrame& b, int j, int r,
+                                            const uint16_t* s_next, const uint8_t* s_tr, int& len, int& q,
+                                            int (&bs)[kKMax - 1], float4& sp) {
+  len = 0;
+  q = 0;
+  sp = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (r >= b.M) return false;
+  q = b.m[3 * r];
+  bs[0] = b.m[3 * r + 1];
+  sp = in.stereo[(int64_t)b.f * dm.cap + q];
+  if (s_tr[q] || !(sp.z > 0.f)) return false;
+  len = 2;
+  bool go = true;
+#pragma unroll
+  for (int kk = 1; kk < kKMax - 1; ++kk) {
+    const int k = j + kk;
+    if (go && k + 1 < b.n) {
+      const int nb = s_next[k * dm.cap + bs[kk - 1]];
+      if (nb == 0xFFFF) go = false;
+      else { bs[kk] = nb; ++len; }
+    } else {
+      go = false;
+    }
+  }
+  return true;
+}
+
+__device__ __forceinline__ int block_isum(int v, int* s_tmp) {  // all threads get the sum
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) s_tmp[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int t = 0;
+#pragma unroll
+  for (int k = 0; k < kBirthBlock / 64; ++k) t += s_tmp[k];
+  __syncthreads();
+  return t;
+}
+
+// (window, birth frame): candidate and observation counts of the frame's rows
+__global__ __launch_bounds__(kBirthBlock) void k_ba_births(BaIn in, void* ws, BaDims dm, int first_end,
+                                                           int first_valid) {
+  extern __shared__ uint8_t s_dyn[];  // [K-1][cap] u16 maps, then [cap] tracked flags
+  __shared__ int s_tmp[kBirthBlock / 64];
+  const int w = blockIdx.x, j = blockIdx.y;
+  BaWin v = view(ws, dm, w);
+  const BirthFrame b = birth_frame(in, dm, w, j, first_end, first_valid);
+  if (j == 0 && threadIdx.x < kBldInts - kBldTot) v.bld[kBldTot + threadIdx.x] = 0;  // emit's totals
+  if (b.n < 3 || j + 1 >= b.n) {
+    if (threadIdx.x == 0) { v.bld[kBldL + j] = 0; v.bld[kBldO + j] = 0; }
+    return;
+  }
+  uint16_t* s_next = reinterpret_cast<uint16_t*>(s_dyn);
+  uint8_t* s_tr = s_dyn + 2 * (dm.K - 1) * dm.cap;
+  birth_maps(in, dm, b, j, s_next, s_tr);
+  int nl = 0, no = 0;
+  for (int r = threadIdx.x; r < b.M; r += kBirthBlock) {
+    int len, q, bs[kKMax - 1];
+    float4 sp;
+    if (birth_track(in, dm, b, j, r, s_next, s_tr, len, q, bs, sp)) { ++nl; no += len; }
+  }
+  nl = block_isum(nl, s_tmp);
+  no = block_isum(no, s_tmp);
+  if (threadIdx.x == 0) { v.bld[kBldL + j] = nl; v.bld[kBldO + j] = no; }
+}
+
+// (window, birth frame): ids from the prefix over earlier birth frames, then the landmarks and
+// their observations exactly as k_ba_build writes them
+__global__ __launch_bounds__(kBirthBlock) void k_ba_emit(BaIn in, void* ws, BaDims dm, int first_end,
+                                                         int first_valid) {
+  extern __shared__ uint8_t s_dyn[];
+  __shared__ double sTj[12];
+  __shared__ int s_tmp[kBirthBlock / 64];
+  __shared__ int s_fc[kKMax];
+  const int w = blockIdx.x, j = blockIdx.y, tid = threadIdx.x;
+  BaWin v = view(ws, dm, w);
+  const BirthFrame b = birth_frame(in, dm, w, j, first_end, first_valid);
+  if (b.M == 0) return;
+  int L0 = 0, O0 = 0;
+  for (int jj = 0; jj < j; ++jj) {
+    L0 += v.bld[kBldL + jj];
+    O0 += v.bld[kBldO + jj];
+  }
+  if (L0 >= dm.Lmax || O0 >= dm.Omax) return;  // every candidate of this frame fails
+  if (tid < kKMax) s_fc[tid] = 0;
+  if (tid == 0) {  // the pose of frame j: T_0 = I, T_{k+1} = rel_{s+k} T_k (k_ba_build's chain)
+    double T[12], U[12];
+    for (int i = 0; i < 12; ++i) T[i] = (i < 9 && i % 4 == 0) ? 1.0 : 0.0;
+    for (int k = 0; k < j; ++k) {
+      const double* M = in.Trel + (int64_t)(b.s + k) * 16;
+      const double A[12] = {M[0], M[1], M[2], M[4], M[5], M[6], M[8], M[9], M[10], M[3], M[7], M[11]};
+      mat_mul_T(A, T, U);
+      for (int i = 0; i < 12; ++i) T[i] = U[i];
+    }
+    for (int i = 0; i < 12; ++i) sTj[i] = T[i];
+  }
+  uint16_t* s_next = reinterpret_cast<uint16_t*>(s_dyn);
+  uint8_t* s_tr = s_dyn + 2 * (dm.K - 1) * dm.cap;
+  birth_maps(in, dm, b, j, s_next, s_tr);  // (barriers: sTj / s_fc visible after it)
+  int okl = 0, oko = 0;
+  for (int base = 0; base < b.M; base += kBirthBlock) {
+    const int r = base + tid;
+    int len, q, bs[kKMax - 1];
+    float4 sp;
+    const bool cand = birth_track(in, dm, b, j, r, s_next, s_tr, len, q, bs, sp);
+    int tp;
+    const int packed = block_scan_n<kBirthBlock>((len << 10) | (cand ? 1 : 0), s_tmp, &tp);
+    const int lid = packed & 1023, oof = packed >> 10;
+    const bool ok = cand && L0 + lid < dm.Lmax && O0 + oof + len <= dm.Omax;
+    if (ok) {
+      const int id = L0 + lid;
+      int o = O0 + oof;
+      const double Xc[3] = {(double)sp.x - sTj[9], (double)sp.y - sTj[10], (double)sp.z - sTj[11]};
+      for (int i = 0; i < 3; ++i) v.X0[3 * id + i] = sTj[i] * Xc[0] + sTj[3 + i] * Xc[1] + sTj[6 + i] * Xc[2];
+      v.lstart[id] = o;
+      const float* kq = in.kp + ((int64_t)b.f * dm.cap + q) * FVO_KP_STRIDE;
+      const int oq = min(max((int)kq[5], 0), in.nlev - 1);
+      v.obs[o++] = BaObs{id, (short)j, (short)oq, kq[0], kq[1], kq[0] - sp.w};
+      float ku[kKMax - 1], kvv[kKMax - 1], ko[kKMax - 1];
+#pragma unroll
+      for (int kk = 0; kk < kKMax - 1; ++kk)
+        if (kk < len - 1) {
+          const float* kb = in.kp + ((int64_t)(b.f + 1 + kk) * dm.cap + bs[kk]) * FVO_KP_STRIDE;
+          ku[kk] = kb[0];
+          kvv[kk] = kb[1];
+          ko[kk] = kb[5];
+        }
+#pragma unroll
+      for (int kk = 0; kk < kKMax - 1; ++kk)
+        if (kk < len - 1) {
+          const int ob = min(max((int)ko[kk], 0), in.nlev - 1);
+          v.obs[o++] = BaObs{id, (short)(j + 1 + kk), (short)ob, ku[kk], kvv[kk], __builtin_nanf("")};
+        }
+      for (int k = 0; k < len; ++k) atomicAdd(&s_fc[j + k], 1);
+      ++okl;
+      oko += len;
+    }
+    L0 += tp & 1023;
+    O0 += tp >> 10;
+    if (L0 >= dm.Lmax || O0 >= dm.Omax) break;  // uniform: the rest fails
+  }
+  okl = block_isum(okl, s_tmp);
+  oko = block_isum(oko, s_tmp);
+  if (tid == 0) {
+    atomicAdd(&v.bld[kBldTot], okl);
+    atomicAdd(&v.bld[kBldTot + 1], oko);
+  }
+  if (tid < kKMax && s_fc[tid]) atomicAdd(&v.bld[kBldF + tid], s_fc[tid]);
+}
+
+// (window, frame k): frame k's observation list in landmark order (a scan over the landmarks);
+// block (w, 0) also writes the window's header, poses and LM state
+__global__ __launch_bounds__(kBirthBlock) void k_ba_lists(BaIn in, void* ws, BaDims dm, int first_end,
+                                                          int first_valid) {
+  __shared__ int s_tmp[kBirthBlock / 64];
+  const int w = blockIdx.x, k = blockIdx.y, tid = threadIdx.x;
+  BaWin v = view(ws, dm, w);
+  BaState* S = v.st;
+  const int e = first_end + w, s = max(first_valid, e - dm.K + 1), n = e - s + 1;
+  const bool live = n >= 3;
+  const int L = live ? v.bld[kBldTot] : 0, O = live ? v.bld[kBldTot + 1] : 0;
+  if (k == 0 && tid == 0) {
+    S->L = L;
+    S->O = O;
+    S->n = n;
+    S->s = s;
+    S->active = L > 0;
+    if (live) {
+      v.lstart[L] = O;
+      S->lam = kLam0;
+      S->parity = 0;
+      S->fail = 0;
+      S->acc = 0;
+      S->cost = 0.0;
+      S->cost0 = 0.0;
+      int acc = 0;
+      for (int f = 0; f < n; ++f) {
+        v.hdr[8 + f] = acc;
+        acc += v.bld[kBldF + f];
+      }
+      v.hdr[8 + n] = acc;
+      double T[12], U[12];
+      for (int i = 0; i < 12; ++i) T[i] = (i < 9 && i % 4 == 0) ? 1.0 : 0.0;
+      for (int f = 0; f < n; ++f) {
+        for (int i = 0; i < 12; ++i) S->T[f][i] = T[i];
+        if (f + 1 < n) {
+          const double* M = in.Trel + (int64_t)(s + f) * 16;
+          const double A[12] = {M[0], M[1], M[2], M[4], M[5], M[6], M[8], M[9], M[10], M[3], M[7], M[11]};
+          mat_mul_T(A, T, U);
+          for (int i = 0; i < 12; ++i) T[i] = U[i];
+        }
+      }
+    }
+  }
+  if (!live || k >= n || L == 0) return;
+  int pos = 0;
+  for (int f = 0; f < k; ++f) pos += v.bld[kBldF + f];
+  for (int base = 0; base < L; base += kBirthBlock) {
+    const int l = base + tid;
+    int o0 = 0, jl = 0, len = 0;
+    if (l < L) {
+      o0 = v.lstart[l];
+      len = (l + 1 < L ? v.lstart[l + 1] : O) - o0;
+      jl = v.obs[o0].frame;
+    }
+    const bool sees = l < L && jl <= k && k < jl + len;
+    int tot;
+    const int rank = block_scan_n<kBirthBlock>(sees ? 1 : 0, s_tmp, &tot);
+    if (sees) v.flist[pos + rank] = o0 + (k - jl);
+    pos += tot;
+  }
 }
 
 // ------------------------------------------------------------------ LM iteration kernels
@@ -1303,6 +1569,7 @@ BaDims make_dims(const fvo_ctx* ctx) {
   d.oCp = take(8ll * (d.NCU > d.NCUP ? d.NCU : d.NCUP));  // cost partials (k_ba_cost / k_ba_upd)
   d.oNext = take(4ll * kKMax * d.cap);
   d.oHdr = take(4ll * (8 + kKMax + 1));
+  d.oBld = take(4ll * kBldInts);
   d.win = o;
   return d;
 }
@@ -1335,9 +1602,12 @@ int ba_init(fvo_ctx* ctx) {
   FVO_HIP(ctx, hipEventCreateWithFlags(&ctx->ba_fork, hipEventDisableTiming));
   FVO_HIP(ctx, hipEventCreateWithFlags(&ctx->ba_join, hipEventDisableTiming));
   // dynamic LDS above 64 KiB: the MFMA slice always, the reduced system for K > 11, the match maps
-  if (build_shm(d) > 65536)
-    FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_build<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  if (build_shm(d) > 65536) {
+    FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_births, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)build_shm(d)));
+    FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_emit, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)build_shm(d)));
+  }
   FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_lin<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lin_shm(d)));
   FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_lin<kLinMaxTiles>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1366,10 +1636,13 @@ void ba_windows_launch(fvo_ctx* ctx, const BaIn& in, const BaCam& cam, const BaD
   void* ws = static_cast<char*>(ctx->ba_ws) + (int64_t)d.win * w0;
   const int fe = first_end + w0;
   const size_t shb = build_shm(d);
-  if (shb > (size_t)d.cap)
-    hipLaunchKernelGGL(k_ba_build<true>, dim3(nw), dim3(kBuildBlock), shb, s, in, ws, d, fe, first_valid);
-  else
+  if (shb > (size_t)d.cap) {  // the match maps fit in LDS: the parallel construction
+    hipLaunchKernelGGL(k_ba_births, dim3(nw, d.K - 1), dim3(kBirthBlock), shb, s, in, ws, d, fe, first_valid);
+    hipLaunchKernelGGL(k_ba_emit, dim3(nw, d.K - 1), dim3(kBirthBlock), shb, s, in, ws, d, fe, first_valid);
+    hipLaunchKernelGGL(k_ba_lists, dim3(nw, d.K), dim3(kBirthBlock), 0, s, in, ws, d, fe, first_valid);
+  } else {
     hipLaunchKernelGGL(k_ba_build<false>, dim3(nw), dim3(kBuildBlock), shb, s, in, ws, d, fe, first_valid);
+  }
   const dim3 gcu(nw, d.NCU), gch(nw, d.NPART), gfr(nw, d.K - 1);
   const size_t shl = lin_shm(d), shs = solve_shm(d.K);
   hipLaunchKernelGGL(k_ba_cost, gcu, dim3(kBlock), 0, s, in, ws, d, cam, 0);
