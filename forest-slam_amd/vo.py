@@ -70,6 +70,9 @@ class StereoFrontEnd:
         self.prevL = e((B, height, width), torch.uint8)
         self.prevR = e((B, height, width), torch.uint8)
         self.disp_buf = two((B, height, width), torch.int16)
+        # the BA's per-keypoint stereo points of the step's previous-left frames, computed in the
+        # front stage (they need only its disparities and keypoints) into a slot like disp
+        self.kstereo_buf = two((B, cap, 4), torch.float32) if self.ba_window else [None, None]
         self._select(0)
         self.P3 = e((B, cap, 3), torch.float32)
         self.p2 = e((B, cap, 2), torch.float32)
@@ -171,6 +174,7 @@ class StereoFrontEnd:
             # query sets (previous descriptors / counts / keypoints) and the last images,
             # (C) after BF the last frame's keypoints / descriptors / counts
             ctx.copy_regions(self._sgbm_pairs(L, R, n) + [(self.imgs[:n], L), (self.imgs[n:2 * n], R)])
+            # SGBM first: ORB + BF first measured slower (r3 4242 vs 4284, r4 5051 vs 5227 frames/s)
             disp = ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n])
             kp, desc, cnt = ctx.orb(self.imgs[:2 * n], out=(self.kp[:2 * n], self.desc[:2 * n], self.cnt[:2 * n]))
             # query (previous) sets: left frames then right frames; previous-left keypoints
@@ -186,6 +190,9 @@ class StereoFrontEnd:
             ctx.copy_regions([(self.last_kp, kp[n - 1]), (self.last_desc[0], desc[n - 1]),
                               (self.last_desc[1], desc[2 * n - 1]), (self.last_cnt[0:1], cnt[n - 1:n]),
                               (self.last_cnt[1:2], cnt[2 * n - 1:2 * n])])
+            if self.ba_window:  # (a negative count -- ORB overflow -- reads as no keypoints)
+                ctx.keypoint_stereo(disp[:n], self.q_kp[:n], self.q_cnt[:n], self.K, self.baseline,
+                                    out=self.kstereo[:n])
         if self.overlap_sgbm:
             main.wait_stream(fs)
         # ---- back stage: back-projection, PnP, local BA
@@ -222,15 +229,15 @@ class StereoFrontEnd:
         self.q_cnt, self.q_kp = self.q_cnt_buf[slot], self.q_kp_buf[slot]
         self.matches, self.nmatch = self.matches_buf[slot], self.nmatch_buf[slot]
         self.disp = self.disp_buf[slot]
+        self.kstereo = self.kstereo_buf[slot]
 
     def _local_ba(self, n, kp, cnt, m, nm, disp, T):
         Kw, ctx = self.ba_window, self.ctx
         a, b = Kw - 2, Kw - 1  # first pair slot, first new-frame slot
         # (hnkp[b:b+n], the clamped counts, came from count_guard)
         ctx.copy_regions([(self.hkp[b:b + n], kp[:n]), (self.hmatch[a:a + n], m[:n]),
-                          (self.hnmatch[a:a + n], nm[:n]), (self.hT[a:a + n], T[:n])])
-        ctx.keypoint_stereo(disp[:n], self.q_kp[:n], self.hnkp[a:a + n], self.K, self.baseline,
-                            out=self.hstereo[a:a + n])
+                          (self.hnmatch[a:a + n], nm[:n]), (self.hT[a:a + n], T[:n]),
+                          (self.hstereo[a:a + n], self.kstereo[:n])])
         F = b + n
         Tba, _ = ctx.ba_windows(self.hkp[:F], self.hnkp[:F], self.hmatch[:F], self.hnmatch[:F], self.hstereo[:F],
                                 self.hT[:F], b, n, self.valid_from, self.K, self.baseline, iterations=self.ba_iters,
