@@ -197,6 +197,45 @@ def test_pnp_ransac_matches_oracle(oracle_mod):
         assert np.abs(tvec[i] - t_ref).max() <= 1e-4 * scale + 1e-9, (i, tvec[i], t_ref)
 
 
+def test_pnp_ransac_round2_plan_matches_oracle(oracle_mod):
+    """Many frames past round 1's 128 iterations at once (RANSAC round 2 runs over the flat
+    work-unit plan of k_pnp_plan): outlier fractions 0.45-0.7 (iteration bounds ~150-1000),
+    interleaved with easy frames and frames below 6 points, against the oracle."""
+    from forest_slam_amd import _lib, synth
+    K, dist = synth.K0, synth.DIST_L
+    fr = [0.45, 0.0, 0.6, 0.5, 0.7, 0.1, 0.55, 0.65, 0.0, 0.5]
+    sizes = [400, 200, 350, 5, 600, 300, 250, 450, 3, 500]
+    B = len(fr)
+    ctx = _lib.Context(960, 600, max_batch=B)
+    cap = ctx.kp_cap
+    P3 = np.zeros((B, cap, 3), np.float32)
+    p2 = np.zeros((B, cap, 2), np.float32)
+    npts = np.zeros(B, np.int32)
+    data = []
+    for i, (f, n) in enumerate(zip(fr, sizes)):
+        P, uv, rv, tv = _pnp_case(100 + i, n, f, 0.3, K, dist, oracle_mod)
+        P3[i, :n], p2[i, :n], npts[i] = P, uv, n
+        data.append((P, uv))
+    rvec, tvec, T, st, inl = ctx.pnp_ransac(torch.from_numpy(P3).cuda(), torch.from_numpy(p2).cuda(),
+                                            torch.from_numpy(npts).cuda(), K, dist)
+    torch.cuda.synchronize()
+    state = ctx.debug_buffer(8).view(torch.int32).view(-1, 4)[:B].numpy()  # maxGood, niters, best, n
+    rvec, tvec, st, inl = rvec.cpu().numpy(), tvec.cpu().numpy(), st.cpu().numpy(), inl.cpu().numpy()
+    assert (state[:, 1] > 128).sum() >= 4  # the case exercises round 2 on several frames
+    for i, (P, uv) in enumerate(data):
+        n = len(P)
+        if n < 6:
+            assert st[i] == -1
+            continue
+        ok, r_ref, t_ref, inl_ref, iters, best = oracle_mod.solve_pnp_ransac(P.astype(np.float64), uv, K, dist)
+        assert st[i] == int(ok)
+        assert state[i, 0] == best, i
+        assert np.array_equal(np.nonzero(inl[i, :n])[0], inl_ref), i
+        scale = max(np.abs(r_ref).max(), np.abs(t_ref).max(), 1e-3)
+        assert np.abs(rvec[i] - r_ref).max() <= 1e-4 * scale + 1e-9, (i, rvec[i], r_ref)
+        assert np.abs(tvec[i] - t_ref).max() <= 1e-4 * scale + 1e-9, (i, tvec[i], t_ref)
+
+
 def test_frontend_matches_oracle_pipeline(oracle_mod, frames):
     """End-to-end stereo_slam.py iteration (:232-306) on 2 frame pairs: matches bit-exact,
     3D points bit-exact (float32), relative pose within 1e-4."""
