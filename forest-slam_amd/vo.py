@@ -304,7 +304,7 @@ class MonoFrontEnd:
     cv2.recoverPose would raise; T is the identity there."""
 
     def __init__(self, width: int, height: int, K: np.ndarray, batch: int, nfeatures: int = 500, device=None,
-                 prob: float = 0.999, threshold: float = 1.0, **params):
+                 prob: float = 0.999, threshold: float = 1.0, overlap: bool = False, **params):
         self.B = batch
         self.K = np.asarray(K, np.float64)
         self.focal = float(self.K[0, 0])
@@ -317,14 +317,21 @@ class MonoFrontEnd:
         self.cap = cap = self.ctx.kp_cap
         B, dev = batch, self.dev
         e = lambda shape, dt: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
-        self.kp = e((B, cap, _lib.KP_STRIDE), torch.float32)
-        self.desc = e((B, cap, _lib.DESC_BYTES), torch.uint8)
-        self.cnt = e((B,), torch.int32)
-        self.q_kp = e((B, cap, _lib.KP_STRIDE), torch.float32)
+        # overlap: the front stage (ORB + BF, throughput-bound) of step k+1 runs on its own
+        # stream beside the back stage (gather, essential-matrix RANSAC, recoverPose --
+        # latency-bound) of step k, as StereoFrontEnd(overlap_sgbm=True) does; the front
+        # stage's outputs then have two slots.  Identical results either way.
+        self.overlap = bool(overlap)
+        two = lambda shape, dt: [e(shape, dt), e(shape, dt)]  # noqa: E731
+        self.kp_buf = two((B, cap, _lib.KP_STRIDE), torch.float32)
+        self.desc_buf = two((B, cap, _lib.DESC_BYTES), torch.uint8)
+        self.cnt_buf = two((B,), torch.int32)
+        self.q_kp_buf = two((B, cap, _lib.KP_STRIDE), torch.float32)
+        self.q_cnt_buf = two((B,), torch.int32)
+        self.matches_buf = two((B, cap, 3), torch.int32)
+        self.nmatch_buf = two((B,), torch.int32)
         self.q_desc = e((B, cap, _lib.DESC_BYTES), torch.uint8)
-        self.q_cnt = e((B,), torch.int32)
-        self.matches = e((B, cap, 3), torch.int32)
-        self.nmatch = e((B,), torch.int32)
+        self._select(0)
         self.p0 = e((B, cap, 2), torch.float32)
         self.p1 = e((B, cap, 2), torch.float32)
         self.npts = e((B,), torch.int32)
@@ -338,7 +345,16 @@ class MonoFrontEnd:
         self.last_kp = e((cap, _lib.KP_STRIDE), torch.float32)
         self.last_desc = e((cap, _lib.DESC_BYTES), torch.uint8)
         self.last_cnt = e((1,), torch.int32)
+        self.s_front = torch.cuda.Stream(dev) if self.overlap else None
+        self.primed = None
+        self.main_done = [None, None]
+        self.k = 0
         self.has_prev = False
+
+    def _select(self, slot: int):
+        self.kp, self.desc, self.cnt = self.kp_buf[slot], self.desc_buf[slot], self.cnt_buf[slot]
+        self.q_kp, self.q_cnt = self.q_kp_buf[slot], self.q_cnt_buf[slot]
+        self.matches, self.nmatch = self.matches_buf[slot], self.nmatch_buf[slot]
 
     def prime(self, img0: torch.Tensor):
         kp, desc, cnt = self.ctx.orb(img0.to(self.dev)[None])
@@ -346,33 +362,55 @@ class MonoFrontEnd:
         self.last_desc.copy_(desc[0])
         self.last_cnt.copy_(cnt[:1])
         self.has_prev = True
+        self.primed = torch.cuda.current_stream(self.dev).record_event() if self.overlap else None
 
-    def step(self, imgs: torch.Tensor):
+    def step(self, imgs: torch.Tensor, inputs_ready=None):
         """imgs: u8 [n,H,W] device tensor of the next n <= B selected frames.  Returns
-        (T f64[n,4,4], status i32[n]) device tensors (async)."""
+        (T f64[n,4,4], status i32[n]) device tensors (async).  With overlap the images must
+        be complete when step() is called (or pass inputs_ready, an event)."""
         if not self.has_prev:
             raise RuntimeError("call prime() with the first frame first")
         n, ctx = imgs.shape[0], self.ctx
         if n > self.B:
             raise ValueError("more frames than the configured batch")
-        kp, desc, cnt = ctx.orb(imgs, out=(self.kp[:n], self.desc[:n], self.cnt[:n]))
-        self.q_kp[0].copy_(self.last_kp)
-        self.q_desc[0].copy_(self.last_desc)
-        self.q_cnt[0:1].copy_(self.last_cnt)
-        if n > 1:
-            self.q_kp[1:n].copy_(kp[:n - 1])
-            self.q_desc[1:n].copy_(desc[:n - 1])
-            self.q_cnt[1:n].copy_(cnt[:n - 1])
-        m, nm = ctx.bf_match(self.q_desc[:n], self.q_cnt[:n], desc, cnt, out=(self.matches[:n], self.nmatch[:n]))
+        main = torch.cuda.current_stream(self.dev)
+        slot = self.k % 2
+        self._select(slot)
+        fs = self.s_front if self.overlap else main
+        capturing = torch.cuda.is_current_stream_capturing()
+        if self.overlap:
+            if capturing:
+                fs.wait_stream(main)
+            else:
+                if self.primed is not None:
+                    fs.wait_event(self.primed)
+                    self.primed = None
+                if inputs_ready is not None:
+                    fs.wait_event(inputs_ready)
+                if self.main_done[slot] is not None:  # the back stage of step k-2 read this slot
+                    fs.wait_event(self.main_done[slot])
+                imgs.record_stream(fs)
+        with torch.cuda.stream(fs):
+            # ---- front stage: ORB of the new frames, query sets, BF (buffer moves batched)
+            kp, desc, cnt = ctx.orb(imgs, out=(self.kp[:n], self.desc[:n], self.cnt[:n]))
+            ctx.copy_regions([(self.q_kp[0], self.last_kp), (self.q_desc[0], self.last_desc),
+                              (self.q_cnt[0:1], self.last_cnt), (self.q_kp[1:n], kp[:n - 1]),
+                              (self.q_desc[1:n], desc[:n - 1]), (self.q_cnt[1:n], cnt[:n - 1])])
+            m, nm = ctx.bf_match(self.q_desc[:n], self.q_cnt[:n], desc, cnt, out=(self.matches[:n], self.nmatch[:n]))
+            ctx.copy_regions([(self.last_kp, kp[n - 1]), (self.last_desc, desc[n - 1]),
+                              (self.last_cnt, cnt[n - 1:n])])
+        if self.overlap:
+            main.wait_stream(fs)
+        # ---- back stage: gather, essential-matrix RANSAC, recoverPose, overflow statuses
         p0, p1, npts = ctx.gather_matches(self.q_kp[:n], kp, m, nm, out=(self.p0[:n], self.p1[:n], self.npts[:n]))
         E, _, st = ctx.find_essential(p0, p1, npts, self.focal, self.pp, self.prob, self.threshold,
                                       out=(self.E[:n], self.mask[:n], self.status[:n]))
         _, _, T, _ = ctx.recover_pose(E, p0, p1, npts, self.focal, self.pp, e_status=st,
                                       out=(self.R[:n], self.t[:n], self.T[:n], self.ngood[:n]))
-        st.masked_fill_((cnt[:n] < 0) | (self.q_cnt[:n] < 0), STATUS_KP_OVERFLOW)
-        self.last_kp.copy_(kp[n - 1])
-        self.last_desc.copy_(desc[n - 1])
-        self.last_cnt.copy_(cnt[n - 1:n])
+        ctx.count_guard(cnt, n, 1, q_counts=self.q_cnt, status=st, code=STATUS_KP_OVERFLOW)
+        if self.overlap and not capturing:
+            self.main_done[slot] = main.record_event()
+        self.k += 1
         return T, st
 
 

@@ -232,3 +232,29 @@ def test_gpu_mono_frontend_benchmark_shape_matches_oracle(oracle_mod):
         if rst == 1:
             assert np.abs(E2[b] - rE).max() < 1e-9, b
             assert np.array_equal(mask2[b, :len(sets[b][0])], rmask), b
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
+def test_gpu_mono_overlapped_steps_equal_in_order():
+    """MonoFrontEnd(overlap=True) -- ORB + BF of step k+1 on a side stream beside step k's
+    essential-matrix stage, double-buffered -- returns exactly the in-order results over
+    several steps (incl. a short last step)."""
+    from forest_slam_amd import synth, vo
+    B, W, H = 8, 640, 400
+    seq = synth.StereoSequence(seed=5, n_frames=3 * B + 1, W=W, H=H, device="cuda", start=40)
+    I, _ = seq.frames(range(3 * B + 1))
+    torch.cuda.synchronize()
+    outs = []
+    for ov in (False, True):
+        fe = vo.MonoFrontEnd(W, H, seq.K, batch=B, nfeatures=500, device="cuda:0", overlap=ov)
+        fe.prime(I[0])
+        Ts, sts = [], []
+        for s, e in ((1, 1 + B), (1 + B, 1 + 2 * B), (1 + 2 * B, 3 * B + 1 - 3)):
+            T, st = fe.step(I[s:e].contiguous())
+            Ts.append(T.clone())
+            sts.append(st.clone())
+        torch.cuda.synchronize()
+        outs.append((torch.cat(Ts).cpu().numpy(), torch.cat(sts).cpu().numpy()))
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert np.array_equal(outs[0][0], outs[1][0])

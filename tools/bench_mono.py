@@ -22,13 +22,14 @@ def main():
     ap.add_argument("--width", type=int, default=960)
     ap.add_argument("--height", type=int, default=600)
     ap.add_argument("--interval", type=int, default=1, help="mono_slam.py frame_interval")
+XX
     a = ap.parse_args()
     from forest_slam_amd import synth, vo
     dev = torch.device("cuda", 0)
     B = a.batch
     seq = synth.StereoSequence(seed=0, n_frames=(B + 1) * a.interval, W=a.width, H=a.height, device=dev, start=100)
     L, _ = seq.frames(range(0, (B + 1) * a.interval, a.interval))
-    fe = vo.MonoFrontEnd(a.width, a.height, seq.K, batch=B, nfeatures=a.nfeatures, device=dev)
+    fe = vo.MonoFrontEnd(a.width, a.height, seq.K, batch=B, nfeatures=a.nfeatures, device=dev, overlap=bool(a.overlap))
     fe.prime(L[0])
     Lb = L[1:].contiguous()
     for _ in range(a.warmup):
@@ -49,7 +50,7 @@ def main():
     print(json.dumps({"metric": "mono frames/sec (ORB + BF + findEssentialMat + recoverPose)", "value":
                       round(B * a.steps / el, 2), "unit": "frames/s", "ms_per_step": round(el / a.steps * 1e3, 3),
                       "config": {"workload": "configs[2] mono", "width": a.width, "height": a.height,
-                                 "nfeatures": a.nfeatures, "frames_per_step": B},
+                                 "nfeatures": a.nfeatures, "frames_per_step": B, "overlap": bool(a.overlap)},
                       "stages_ms_per_step": stages, "status_ok": int((st == 1).sum()),
                       "mean_cheirality_inliers": float(ng[st == 1].float().mean()) if (st == 1).any() else None}))
 
