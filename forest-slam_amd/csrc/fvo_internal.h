@@ -92,6 +92,7 @@ struct fvo_ctx {
   double* pnp_ws = nullptr;       // [B][max_iters][PNP_WS] EPnP null space + subset state between launches
   int32_t* pnp_good = nullptr;    // [B][max_iters] inlier counts
   void* pnp_state = nullptr;      // [B] PnpState
+  float* pnp_pts = nullptr;        // [B][5 * cap] the refinement's compacted inliers past its LDS
   int32_t* pnp_plan = nullptr;    // [3][B + 1] round-2 work-unit prefix sums (units of 64, 8, 16 iterations)
   int32_t pnp_max_iters = 0;
   uint8_t* fast_rec = nullptr;    // [B][tiles][kTRec] per FAST tile: row keep words + prefixes + kept scores

@@ -1002,6 +1002,8 @@ __device__ __forceinline__ double wsum_d(double v) {
 }
 
 // ------------------------------------------------------------------ RANSAC + refine
+constexpr int kRefineLds = 1024;  // inliers staged in k_pnp_refine's LDS (20 KB)
+
 struct PnpShared {
   double dlt[5][144];  // DLT 12x12 SVD: input, work u / v, outputs U / V (lane 0 only)
   int sub[kChunk][5];
@@ -1009,21 +1011,168 @@ struct PnpShared {
   double model[kChunk][6];
   double best[6];
   double param[6];
+  double jtj[21], jte[6];  // the LM normal equations (J^T J packed upper triangle, J^T e)
+  double llp[78];          // the DLT's packed A^T A, wave-summed
+  double rrt[12];          // the DLT null vector (non-planar)
+  double rt[9], t3[3];     // the planar case's frame (Rt, T)
+  double prev[6];          // the LM step's base point
   int maxGood, niters, done, next_iter;
   uint64_t rng;
   int ninl;
   int flag;
 };
 
-__device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const float* p2, const int* inl, int n,
-                          double* mn) {
+// The DLT's pose (lane 0): R, t from the null vector, or the planar homography's
+// decomposition, into sh.param.  noinline, as lm_eval / lm_step below: the refinement runs as
+// one wave per frame, so its code is fetched cold -- one copy of each phase instead of the
+// inlined copies (a 219 KB kernel) keeps the LM loop in the instruction cache.
+__device__ __attribute__((noinline)) void dlt_pose(PnpShared& sh, bool planar) {
+  double param[6] = {0, 0, 0, 0, 0, 0};
+  double R[9];
+  if (!planar) {
+    double RR[9] = {sh.rrt[0], sh.rrt[1], sh.rrt[2], sh.rrt[4], sh.rrt[5], sh.rrt[6], sh.rrt[8], sh.rrt[9], sh.rrt[10]};
+    double tt[3] = {sh.rrt[3], sh.rrt[7], sh.rrt[11]};
+    if (ddet3(RR) < 0) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) RR[i] = -RR[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) tt[i] = -tt[i];
+    }
+    double sc = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) sc += RR[i] * RR[i];
+    sc = sqrt(sc);
+    double Wr[3], Ur[9], Vr[9];
+    dsvd<3, 3>(RR, Wr, Ur, Vr);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) R[i * 3 + j] = Ur[i * 3] * Vr[j * 3] + Ur[i * 3 + 1] * Vr[j * 3 + 1] + Ur[i * 3 + 2] * Vr[j * 3 + 2];
+    double nR = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) nR += R[i] * R[i];
+    nR = sqrt(nR);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) param[3 + i] = tt[i] * nR / sc;
+    rod_R2r(R, param);
+  } else {
+    double* AtA = sh.dlt[0];
+    double* U9 = sh.dlt[3];
+    double* V9 = sh.dlt[4];
+    double W9[9], H[9], t[3];
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 9; ++a)
+#pragma unroll
+      for (int b = a; b < 9; ++b) { AtA[a * 9 + b] = sh.llp[k]; AtA[b * 9 + a] = sh.llp[k]; ++k; }
+    dsvd_ws<9, 9>(AtA, W9, U9, V9, sh.dlt[1], sh.dlt[2]);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) H[i] = V9[i * 9 + 8];
+    if (fabs(H[8]) >= 1e-300) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) H[i] /= H[8];
+      double h1 = sqrt(H[0] * H[0] + H[3] * H[3] + H[6] * H[6]);
+      double h2 = sqrt(H[1] * H[1] + H[4] * H[4] + H[7] * H[7]);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        H[i * 3] /= fmax(h1, DBL_EPSILON);
+        H[i * 3 + 1] /= fmax(h2, DBL_EPSILON);
+        t[i] = H[i * 3 + 2] * 2. / fmax(h1 + h2, DBL_EPSILON);
+      }
+      H[2] = H[3] * H[7] - H[6] * H[4];
+      H[5] = H[6] * H[1] - H[0] * H[7];
+      H[8] = H[0] * H[4] - H[3] * H[1];
+      double r[3];
+      rod_R2r(H, r);
+      rod_r2R(r, H, nullptr);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) t[i] += H[i * 3] * sh.t3[0] + H[i * 3 + 1] * sh.t3[1] + H[i * 3 + 2] * sh.t3[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) R[i * 3 + j] = H[i * 3] * sh.rt[j] + H[i * 3 + 1] * sh.rt[3 + j] + H[i * 3 + 2] * sh.rt[6 + j];
+      param[3] = t[0]; param[4] = t[1]; param[5] = t[2];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0);
+    }
+    rod_R2r(R, param);
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) sh.param[i] = param[i];
+}
+
+// One LM evaluation over the inliers: the reprojection error norm, and with withJ the normal
+// equations J^T J / J^T e into sh.jtj / sh.jte (lane 0 writes).  Every lane returns the norm.
+__device__ __attribute__((noinline)) double lm_eval(PnpShared& sh, const Cam K, const float* P3, const float* p2,
+                                                    int n, bool withJ) {
+  const int lane = wave_lane();
+  double p[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) p[i] = sh.param[i];
+  double R[9], dR[27];
+  rod_r2R(p, R, dR);
+  double a[28];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) a[k] = 0;
+  for (int i = lane; i < n; i += 64) {
+    const int j = i;
+    double M[3] = {(double)P3[3 * j], (double)P3[3 * j + 1], (double)P3[3 * j + 2]}, uv[2], J[12];
+    dproject(K, R, dR, p + 3, M, uv, withJ ? J : nullptr);
+    double e0 = uv[0] - (double)p2[2 * j], e1 = uv[1] - (double)p2[2 * j + 1];
+    a[27] += e0 * e0 + e1 * e1;
+    if (withJ) {
+      int k = 0;
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = r; c < 6; ++c) a[k++] += J[r] * J[c] + J[6 + r] * J[6 + c];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) a[21 + r] += J[r] * e0 + J[6 + r] * e1;
+    }
+  }
+  if (withJ) {
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+      const double t = wsum_d(a[k]);
+      if (lane == 0) {
+        if (k < 21) sh.jtj[k] = t;
+        else sh.jte[k - 21] = t;
+      }
+    }
+  }
+  return sqrt(wsum_d(a[27]));
+}
+
+// The LM step (lane 0): (J^T J with the (1 + lambda) diagonal) x = J^T e from the packed
+// sh.jtj / sh.jte, sh.param = sh.prev - x.
+__device__ __attribute__((noinline)) void lm_step(PnpShared& sh, double lambdaLg10) {
+  const double lambda = exp(lambdaLg10 * log(10.));
+  double A[36], x[6], g[6];
+  int k = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = r; c < 6; ++c) { A[r * 6 + c] = sh.jtj[k]; A[c * 6 + r] = sh.jtj[k]; ++k; }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    A[i * 6 + i] *= 1. + lambda;
+    g[i] = sh.jte[i];
+  }
+  if (!chol_solve6(A, g, x)) dsolve<6, 6>(A, g, x);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) sh.param[i] = sh.prev[i] - x[i];
+}
+
+// P3 / p2: the inliers' points, compacted (k_pnp_refine stages them in LDS)
+__device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const float* p2, int n, double* mn) {
   // ---- init (cvFindExtrinsicCameraParams2, useExtrinsicGuess = false)
   const int lane = wave_lane();
   double acc[28];
 #pragma unroll
   for (int k = 0; k < 28; ++k) acc[k] = 0;
   for (int i = lane; i < n; i += 64) {
-    int j = inl[i];
+    const int j = i;
     dundistort(K, (double)p2[2 * j], (double)p2[2 * j + 1], &mn[2 * i]);
     acc[0] += (double)P3[3 * j];
     acc[1] += (double)P3[3 * j + 1];
@@ -1034,7 +1183,7 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
   double Mc[3] = {acc[0] / n, acc[1] / n, acc[2] / n};
   double MM[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int i = lane; i < n; i += 64) {
-    int j = inl[i];
+    const int j = i;
     double d[3] = {(double)P3[3 * j] - Mc[0], (double)P3[3 * j + 1] - Mc[1], (double)P3[3 * j + 2] - Mc[2]};
 #pragma unroll
     for (int a = 0; a < 3; ++a)
@@ -1057,7 +1206,7 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
   double Rt[9], T[3];
   if (!planar) {
     for (int i = lane; i < n; i += 64) {
-      int j = inl[i];
+      const int j = i;
       double x = -mn[2 * i], y = -mn[2 * i + 1];
       double P[3] = {(double)P3[3 * j], (double)P3[3 * j + 1], (double)P3[3 * j + 2]};
       double r0[12] = {P[0], P[1], P[2], 1., 0, 0, 0, 0, x * P[0], x * P[1], x * P[2], x};
@@ -1081,9 +1230,15 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
       for (int i = 0; i < 9; ++i) Rt[i] = -Rt[i];
 #pragma unroll
     for (int i = 0; i < 3; ++i) T[i] = -(Rt[i * 3] * Mc[0] + Rt[i * 3 + 1] * Mc[1] + Rt[i * 3 + 2] * Mc[2]);
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) sh.rt[i] = Rt[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) sh.t3[i] = T[i];
+    }
     // homography DLT (A^T A, 9x9 upper triangle = 45 entries)
     for (int i = lane; i < n; i += 64) {
-      int j = inl[i];
+      const int j = i;
       double s0 = P3[3 * j], s1 = P3[3 * j + 1], s2 = P3[3 * j + 2];
       double X = Rt[0] * s0 + Rt[1] * s1 + Rt[2] * s2 + T[0];
       double Y = Rt[3] * s0 + Rt[4] * s1 + Rt[5] * s2 + T[1];
@@ -1098,155 +1253,36 @@ __device__ void lm_refine(PnpShared& sh, const Cam& K, const float* P3, const fl
     }
   }
 #pragma unroll
-  for (int k = 0; k < 78; ++k) LLp[k] = wsum_d(LLp[k]);
-  double param[6] = {0, 0, 0, 0, 0, 0};
-  double RRt[12];
-  if (!planar) dlt12_null(LLp, sh.dlt[1], sh.dlt[2], RRt);  // the whole wave
-  if (lane == 0) {
-    double R[9];
-    if (!planar) {
-      double RR[9] = {RRt[0], RRt[1], RRt[2], RRt[4], RRt[5], RRt[6], RRt[8], RRt[9], RRt[10]};
-      double tt[3] = {RRt[3], RRt[7], RRt[11]};
-      if (ddet3(RR) < 0) {
-#pragma unroll
-        for (int i = 0; i < 9; ++i) RR[i] = -RR[i];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) tt[i] = -tt[i];
-      }
-      double sc = 0;
-#pragma unroll
-      for (int i = 0; i < 9; ++i) sc += RR[i] * RR[i];
-      sc = sqrt(sc);
-      double Wr[3], Ur[9], Vr[9];
-      dsvd<3, 3>(RR, Wr, Ur, Vr);
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) R[i * 3 + j] = Ur[i * 3] * Vr[j * 3] + Ur[i * 3 + 1] * Vr[j * 3 + 1] + Ur[i * 3 + 2] * Vr[j * 3 + 2];
-      double nR = 0;
-#pragma unroll
-      for (int i = 0; i < 9; ++i) nR += R[i] * R[i];
-      nR = sqrt(nR);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) param[3 + i] = tt[i] * nR / sc;
-      rod_R2r(R, param);
-    } else {
-      double* AtA = sh.dlt[0];
-      double* U9 = sh.dlt[3];
-      double* V9 = sh.dlt[4];
-      double W9[9], H[9], t[3];
-      int k = 0;
-#pragma unroll
-      for (int a = 0; a < 9; ++a)
-#pragma unroll
-        for (int b = a; b < 9; ++b) { AtA[a * 9 + b] = LLp[k]; AtA[b * 9 + a] = LLp[k]; ++k; }
-      dsvd_ws<9, 9>(AtA, W9, U9, V9, sh.dlt[1], sh.dlt[2]);
-#pragma unroll
-      for (int i = 0; i < 9; ++i) H[i] = V9[i * 9 + 8];
-      if (fabs(H[8]) >= 1e-300) {
-#pragma unroll
-        for (int i = 0; i < 9; ++i) H[i] /= H[8];
-        double h1 = sqrt(H[0] * H[0] + H[3] * H[3] + H[6] * H[6]);
-        double h2 = sqrt(H[1] * H[1] + H[4] * H[4] + H[7] * H[7]);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          H[i * 3] /= fmax(h1, DBL_EPSILON);
-          H[i * 3 + 1] /= fmax(h2, DBL_EPSILON);
-          t[i] = H[i * 3 + 2] * 2. / fmax(h1 + h2, DBL_EPSILON);
-        }
-        H[2] = H[3] * H[7] - H[6] * H[4];
-        H[5] = H[6] * H[1] - H[0] * H[7];
-        H[8] = H[0] * H[4] - H[3] * H[1];
-        double r[3];
-        rod_R2r(H, r);
-        rod_r2R(r, H, nullptr);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) t[i] += H[i * 3] * T[0] + H[i * 3 + 1] * T[1] + H[i * 3 + 2] * T[2];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) R[i * 3 + j] = H[i * 3] * Rt[j] + H[i * 3 + 1] * Rt[3 + j] + H[i * 3 + 2] * Rt[6 + j];
-        param[3] = t[0]; param[4] = t[1]; param[5] = t[2];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0);
-      }
-      rod_R2r(R, param);
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) sh.param[i] = param[i];
+  for (int k = 0; k < 78; ++k) {
+    const double t = wsum_d(LLp[k]);
+    if (lane == 0) sh.llp[k] = t;  // in LDS: the SVD below runs beside no register copy of it
   }
   __syncthreads();
+  if (!planar) dlt12_null(sh.llp, sh.dlt[1], sh.dlt[2], sh.rrt);  // the whole wave (same sh.rrt on every lane)
+  if (lane == 0) dlt_pose(sh, planar);
+  __syncthreads();
   // ---- Levenberg-Marquardt (CvLevMarq semantics)
-  auto eval = [&](bool withJ, double* JtJ, double* JtErr) -> double {
-    double p[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) p[i] = sh.param[i];
-    double R[9], dR[27];
-    rod_r2R(p, R, dR);
-    double a[28];
-#pragma unroll
-    for (int k = 0; k < 28; ++k) a[k] = 0;
-    for (int i = lane; i < n; i += 64) {
-      int j = inl[i];
-      double M[3] = {(double)P3[3 * j], (double)P3[3 * j + 1], (double)P3[3 * j + 2]}, uv[2], J[12];
-      dproject(K, R, dR, p + 3, M, uv, withJ ? J : nullptr);
-      double e0 = uv[0] - (double)p2[2 * j], e1 = uv[1] - (double)p2[2 * j + 1];
-      a[27] += e0 * e0 + e1 * e1;
-      if (withJ) {
-        int k = 0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-          for (int c = r; c < 6; ++c) a[k++] += J[r] * J[c] + J[6 + r] * J[6 + c];
-#pragma unroll
-        for (int r = 0; r < 6; ++r) a[21 + r] += J[r] * e0 + J[6 + r] * e1;
-      }
-    }
-#pragma unroll
-    for (int k = withJ ? 0 : 27; k < 28; ++k) a[k] = wsum_d(a[k]);
-    if (withJ) {
-      int k = 0;
-#pragma unroll
-      for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int c = r; c < 6; ++c) { JtJ[r * 6 + c] = a[k]; JtJ[c * 6 + r] = a[k]; ++k; }
-#pragma unroll
-      for (int r = 0; r < 6; ++r) JtErr[r] = a[21 + r];
-    }
-    return sqrt(a[27]);
-  };
-  double JtJ[36], JtErr[6], prev[6];
+  double prev[6];
   double lambdaLg10 = -3, prevErrNorm = DBL_MAX;
-  auto step = [&]() {
-    if (lane == 0) {
-      double lambda = exp(lambdaLg10 * log(10.));
-      double A[36], x[6];
-#pragma unroll
-      for (int i = 0; i < 36; ++i) A[i] = JtJ[i];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) A[i * 6 + i] *= 1. + lambda;
-      if (!chol_solve6(A, JtErr, x)) dsolve<6, 6>(A, JtErr, x);
-#pragma unroll
-      for (int i = 0; i < 6; ++i) sh.param[i] = prev[i] - x[i];
-    }
-    __syncthreads();
-  };
   int iters = 0;
-#pragma unroll
   for (;;) {
-    double e0 = eval(true, JtJ, JtErr);
+    double e0 = lm_eval(sh, K, P3, p2, n, true);
 #pragma unroll
     for (int i = 0; i < 6; ++i) prev[i] = sh.param[i];
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) sh.prev[i] = prev[i];
+    }
     __syncthreads();
-    step();
+    if (lane == 0) lm_step(sh, lambdaLg10);
+    __syncthreads();
     if (iters == 0) prevErrNorm = e0;
     double errNorm;
-#pragma unroll
     for (;;) {
-      errNorm = eval(false, nullptr, nullptr);
+      errNorm = lm_eval(sh, K, P3, p2, n, false);
       if (errNorm > prevErrNorm && ++lambdaLg10 <= 16) {
-        step();
+        if (lane == 0) lm_step(sh, lambdaLg10);
+        __syncthreads();
         continue;
       }
       break;
@@ -1541,8 +1577,10 @@ __global__ __launch_bounds__(64, 2) void k_pnp_refine(const float* __restrict__ 
                                                    const double* __restrict__ model, double* __restrict__ rvec,
                                                    double* __restrict__ tvec, double* __restrict__ T,
                                                    int32_t* __restrict__ status, uint8_t* __restrict__ inliers,
-                                                   int32_t* __restrict__ inl_idx, double* __restrict__ mn_buf) {
+                                                   int32_t* __restrict__ inl_idx, double* __restrict__ mn_buf,
+                                                   float* __restrict__ pts) {
   __shared__ PnpShared sh;
+  __shared__ float s_pts[5 * kRefineLds];  // the inliers' P3 then p2, compacted, when they fit
   const int b = blockIdx.x, lane = threadIdx.x;
   const PnpState st = state[b];
   const int n = st.n;
@@ -1577,7 +1615,17 @@ __global__ __launch_bounds__(64, 2) void k_pnp_refine(const float* __restrict__ 
         if (inliers) inliers[(int64_t)b * cap + i] = (uint8_t)f;
       }
       unsigned long long m = __ballot(f);
-      if (f) inl[carry + __popcll(m & ((1ull << lane) - 1ull))] = i;
+      if (f) {
+        const int k = carry + __popcll(m & ((1ull << lane) - 1ull));
+        inl[k] = i;
+        if (k < kRefineLds) {
+          s_pts[3 * k] = P3[3 * i];
+          s_pts[3 * k + 1] = P3[3 * i + 1];
+          s_pts[3 * k + 2] = P3[3 * i + 2];
+          s_pts[3 * kRefineLds + 2 * k] = p2[2 * i];
+          s_pts[3 * kRefineLds + 2 * k + 1] = p2[2 * i + 1];
+        }
+      }
       carry += __popcll(m);
     }
     if (inliers)
@@ -1585,7 +1633,28 @@ __global__ __launch_bounds__(64, 2) void k_pnp_refine(const float* __restrict__ 
     if (lane == 0) sh.ninl = carry;
   }
   __syncthreads();
-  lm_refine(sh, K, P3, p2, inl, sh.ninl, mn_buf + (int64_t)b * cap * 2);
+  // the LM's evaluations read every inlier several times: from LDS (~100 cycles) instead of a
+  // dependent global gather per point (~1 us) -- or, past kRefineLds inliers, compacted in the
+  // global buffer pts (same values: the results do not depend on where they are read from)
+  const int ninl = sh.ninl;
+  const float* Pc = s_pts;
+  const float* Qc = s_pts + 3 * kRefineLds;
+  if (ninl > kRefineLds) {
+    float* gP = pts + (int64_t)b * cap * 5;
+    float* gQ = gP + 3 * cap;
+    for (int k = lane; k < ninl; k += 64) {
+      const int i = inl[k];
+      gP[3 * k] = P3[3 * i];
+      gP[3 * k + 1] = P3[3 * i + 1];
+      gP[3 * k + 2] = P3[3 * i + 2];
+      gQ[2 * k] = p2[2 * i];
+      gQ[2 * k + 1] = p2[2 * i + 1];
+    }
+    __syncthreads();
+    Pc = gP;
+    Qc = gQ;
+  }
+  lm_refine(sh, K, Pc, Qc, ninl, mn_buf + (int64_t)b * cap * 2);
   double out[6];
   for (int i = 0; i < 6; ++i) out[i] = sh.flag ? sh.param[i] : sh.best[i];
   if (lane == 0) {
@@ -1616,7 +1685,7 @@ int pose_init(fvo_ctx* ctx) {
       (rc = hipFuncSetAttribute((const void*)k_pnp_setup, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 144 * 64 * (int)sizeof(double)) == hipSuccess ? 0 : fvo_fail(ctx, "pnp: LDS attribute")) ||
       (rc = fvo_alloc(ctx, &ctx->pnp_good, it)) || (rc = fvo_alloc(ctx, (PnpState**)&ctx->pnp_state, B)) ||
-      (rc = fvo_alloc(ctx, &ctx->pnp_plan, 3 * (B + 1))))
+      (rc = fvo_alloc(ctx, &ctx->pnp_plan, 3 * (B + 1))) || (rc = fvo_alloc(ctx, &ctx->pnp_pts, 5 * n)))
     return rc;
   return 0;
 }
@@ -1674,7 +1743,7 @@ int pnp_run(fvo_ctx* ctx, const float* P3, const float* p2, const int32_t* npts,
       hyp(ctx->pnp_plan, dim3(gs), dim3(ga), dim3(gb), first, maxIters);
     }
     hipLaunchKernelGGL(k_pnp_refine, dim3(batch), dim3(64), 0, s, P3, p2, cap, c, thr2, maxIters, st,
-                       ctx->pnp_models, rvec, tvec, T, status, inliers, ctx->pnp_sub, ctx->pnp_hyp);
+                       ctx->pnp_models, rvec, tvec, T, status, inliers, ctx->pnp_sub, ctx->pnp_hyp, ctx->pnp_pts);
   });
   FVO_LAUNCH_CHECK(ctx);
   return 0;
