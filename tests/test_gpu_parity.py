@@ -168,9 +168,12 @@ def test_pnp_ransac_matches_oracle(oracle_mod):
     K, dist = synth.K0, synth.DIST_L
     cases = [(s, n, f, nz) for s, (n, f, nz) in enumerate([(300, 0.3, 0.3), (80, 0.5, 0.2), (1000, 0.1, 0.5),
                                                            (40, 0.0, 0.0), (12, 0.2, 0.1), (6, 0.0, 0.2),
-                                                           (500, 0.7, 0.3), (5, 0.0, 0.0)])]
+                                                           (500, 0.7, 0.3), (5, 0.0, 0.0),
+                                                           # > 1024 inliers: k_pnp_refine's global
+                                                           # compacted copy instead of its LDS stage
+                                                           (1500, 0.1, 0.3)])]
     B = len(cases)
-    ctx = _lib.Context(960, 600, max_batch=B)
+    ctx = _lib.Context(960, 600, max_batch=B, nfeatures=1000)  # kp_cap 2064: room for the 1500-point case
     cap = ctx.kp_cap
     P3 = np.zeros((B, cap, 3), np.float32)
     p2 = np.zeros((B, cap, 2), np.float32)

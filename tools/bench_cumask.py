@@ -4,7 +4,8 @@ stay free for the back stage's dispatches (tooling experiment: prints frames/s p
     python tools/bench_cumask.py [--masks none,lo16,stride16] [--steps 10]
 
 lo16 masks out CUs 0..15, stride16 every 16th CU (which of the two spreads the reserved CUs
-over the 8 XCDs depends on the driver's CU numbering, hence both)."""
+over the 8 XCDs depends on the driver's CU numbering, hence both); hiprio puts the back stage,
+fronthi the front stage on a high-priority stream."""
 import argparse
 import ctypes
 import json
@@ -21,6 +22,8 @@ sys.path.insert(0, ROOT)
 def masked_stream(dev, kind):
     if kind in ("none", "hiprio"):
         return torch.cuda.Stream(dev)
+    if kind == "fronthi":  # the front stage (the step's critical path) on a high-priority stream
+        return torch.cuda.Stream(dev, priority=-1)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     words = [0] * ((ncu + 31) // 32)
     for cu in range(ncu):
