@@ -1370,8 +1370,11 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
 // j, j + GLU, ... (all of them at GLU = 1, one each at GLU >= K) and forms their W^T dp (W from
 // ba_eval_lw at the linearisation point, as k_ba_lin) and, after the step, their cost at the
 // tentative poses; the group sums both over its lanes (xor butterfly), the block sums the cost
-// (fixed order) into one partial per block.  GLU = 1 at K <= 16 (short tracks: per-lane loops
-// are short and the blocks few), 32 at K = 20.
+// (fixed order) into one partial per block.  kUpdGluShort = 2 lanes at K <= 16 (BA 600p / K = 10
+// 1.80 -> 1.75 ms against 1 lane, 4: 1.76 ms), kUpdGluLong = 8 at K > 16 (up to 3 observations
+// each of a 20-frame track; BA 1080p / K = 20 4.53 -> 4.27 ms against 32 lanes, which sat mostly
+// idle on tracks of a few observations; 16: 4.43, 4: 4.26 ms).
+constexpr int kUpdGluShort = 2, kUpdGluLong = 8;
 template <int GLU>
 __global__ __launch_bounds__(kBlock) void k_ba_upd(BaIn in, void* ws, BaDims dm, BaCam cam) {
   constexpr int LPU = kBlock / GLU;
@@ -1549,7 +1552,7 @@ BaDims make_dims(const fvo_ctx* ctx) {
   d.NPART = d.NPART < 1 ? 1 : d.NPART > kLinParts ? kLinParts : d.NPART;
   if (d.NPART > d.NCH) d.NPART = d.NCH;
   d.NCU = (d.Lmax + kBlock - 1) / kBlock;
-  d.LPU = d.K <= 16 ? kBlock : kBlock / 32;  // k_ba_upd: landmarks per block (GLU = 1 / 32 lanes each)
+  d.LPU = kBlock / (d.K <= 16 ? kUpdGluShort : kUpdGluLong);  // k_ba_upd: landmarks per block
   d.NCUP = (d.Lmax + d.LPU - 1) / d.LPU;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
@@ -1658,8 +1661,8 @@ void ba_windows_launch(fvo_ctx* ctx, const BaIn& in, const BaCam& cam, const BaD
     if (d.NPART >= kGsumParts)
       hipLaunchKernelGGL(k_ba_gsum, dim3(nw, (d.NR * d.NR / 2 + 255) / 256), dim3(256), 0, s, ws, d);
     hipLaunchKernelGGL(k_ba_solve, dim3(nw), dim3(kSolveBlock), shs, s, ws, d);
-    if (d.K <= 16) hipLaunchKernelGGL(k_ba_upd<1>, dim3(nw, d.NCUP), dim3(kBlock), 0, s, in, ws, d, cam);
-    else hipLaunchKernelGGL(k_ba_upd<32>, dim3(nw, d.NCUP), dim3(kBlock), 0, s, in, ws, d, cam);
+    if (d.K <= 16) hipLaunchKernelGGL(k_ba_upd<kUpdGluShort>, dim3(nw, d.NCUP), dim3(kBlock), 0, s, in, ws, d, cam);
+    else hipLaunchKernelGGL(k_ba_upd<kUpdGluLong>, dim3(nw, d.NCUP), dim3(kBlock), 0, s, in, ws, d, cam);
     hipLaunchKernelGGL(k_ba_accept, dim3(nw), dim3(64), 0, s, ws, d);
   }
   hipLaunchKernelGGL(k_ba_final, dim3(nw), dim3(64), 0, s, in.Trel, ws, d, fe, Tout + 16 * (int64_t)w0,
