@@ -418,22 +418,29 @@ class Context:
         return cum, npo
 
     def copy_regions(self, pairs):
-        """Device-to-device copies ``dst.copy_(src)`` for every (dst, src) in pairs, batched
-        into fvo_copy_regions launches of up to FVO_MAX_REGIONS (same-dtype contiguous pairs;
-        any other pair is copied by torch).  No destination may overlap any source or other
-        destination (the library refuses it)."""
+        """Device-to-device copies ``dst.copy_(src)`` for every (dst, src) in pairs, in list
+        order, batched into fvo_copy_regions launches of up to FVO_MAX_REGIONS (same-dtype
+        contiguous pairs; any other pair is copied by torch after the batch before it has been
+        launched, so a torch copy never overtakes an earlier batched one).  No destination may
+        overlap any source or other destination of one batch (the library refuses it)."""
         batch = []
+
+        def flush():
+            for k in range(0, len(batch), FVO_MAX_REGIONS):
+                part = batch[k:k + FVO_MAX_REGIONS]
+                arr = (FvoRegion * len(part))(*[FvoRegion(dp, sp, nb) for dp, sp, nb in part])
+                self._check(self.L.fvo_copy_regions(self.h, len(part), ctypes.cast(arr, _P), _stream(self.device)))
+            batch.clear()
+
         for d, src in pairs:
             nb = d.numel() * d.element_size()
             if d.dtype != src.dtype or d.shape != src.shape or not (d.is_contiguous() and src.is_contiguous()):
+                flush()
                 d.copy_(src)
                 continue
             if nb:
                 batch.append((d.data_ptr(), src.data_ptr(), nb))
-        for k in range(0, len(batch), FVO_MAX_REGIONS):
-            part = batch[k:k + FVO_MAX_REGIONS]
-            arr = (FvoRegion * len(part))(*[FvoRegion(dp, sp, nb) for dp, sp, nb in part])
-            self._check(self.L.fvo_copy_regions(self.h, len(part), ctypes.cast(arr, _P), _stream(self.device)))
+        flush()
 
     def count_guard(self, counts, n, sets=1, q_counts=None, status=None, code=0, clamped_out=None):
         """fvo_count_guard: status[i] = code where any counts[s*n + i] / q_counts[s*n + i]

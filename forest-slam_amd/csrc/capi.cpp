@@ -87,6 +87,7 @@ static void release(fvo_ctx* c) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->ba_s2) (void)hipStreamDestroy(c->ba_s2);
+
   if (c->ba_fork) (void)hipEventDestroy(c->ba_fork);
   if (c->ba_join) (void)hipEventDestroy(c->ba_join);
 }
@@ -441,6 +442,9 @@ int fvo_debug_buffer(fvo_ctx* c, int which, void** ptr, int64_t* bytes) {
     case 6: *ptr = c->pnp_good; *bytes = B * c->pnp_max_iters * 4; return 0;
     case 7: *ptr = c->pnp_models; *bytes = B * c->pnp_max_iters * 6 * 8; return 0;
     case 8: *ptr = c->pnp_state; *bytes = B * 16; return 0;
+    case 9:  // SGBM control words: ticket, generation, hand-off timeouts, per-pair failure flags
+      if (!c->sg_ctl) return fvo_fail(c, "no SGBM workspace");
+      *ptr = c->sg_ctl; *bytes = (4 + B) * 4; return 0;
     default: return fvo_fail(c, "unknown debug buffer");
   }
 }

@@ -83,6 +83,8 @@ struct fvo_ctx {
   uint16_t* sg_M = nullptr;     // min over d of each V row, [B][HG4 + nstripes][width1][4]
   uint32_t* sg_ckpt = nullptr;  // [B][4-row blocks][nck][64 lanes][ckw] left->right path checkpoints
   int16_t* sg_raw = nullptr;    // [B][H][W] pre-median disparity
+  uint64_t* sg_hand = nullptr;  // [B][H][2][D/32][16] L-path hand-off granules (cost pass, column block to block)
+  uint32_t* sg_ctl = nullptr;   // [4 + B] ticket, generation, hand-off timeouts, per-pair failure flags
   // pose workspace
   double* pnp_hyp = nullptr;      // [B][cap][2] normalised inlier points (refinement)
   int32_t* pnp_sub = nullptr;     // [B][cap] inlier indices

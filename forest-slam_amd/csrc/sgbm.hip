@@ -195,6 +195,75 @@ __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q
 }
 
 
+// ------------------------------------------------------------------ row bands: C + left/right paths + WTA
+// A row of 16 lanes is one DPP row: neighbours by row_shr/row_shl:1, minima by quad xor 1/2,
+// row_half_mirror and row_mirror.
+constexpr int kRShr1 = 0x111;        // row_shr:1 -- value of lane i-1
+constexpr int kRShl1 = 0x101;        // row_shl:1 -- value of lane i+1
+constexpr int kRHalfMirror = 0x141;  // lane i <-> 7-i within each half row
+constexpr int kRMirror = 0x140;      // lane i <-> 15-i
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t rdpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+
+// Ring sizes of the row pass's LDS windows (powers of two): keys cover x2 over 2D + 4 SEG
+// columns, raw disparities wait D + 2 SEG columns for their check.
+__host__ __device__ constexpr int sg_pow2(int n) { return n <= 1 ? 1 : 2 * sg_pow2((n + 1) / 2); }
+__host__ __device__ constexpr int sg_ring_keys(int D) { return sg_pow2(2 * D + 32); }
+__host__ __device__ constexpr int sg_ring_raw(int D) { return sg_pow2(D + 16); }
+
+// One path step of a 16-lane row (PQ packed words per lane); returns the row minimum.
+template <int PQ>
+__device__ __forceinline__ uint32_t step16(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
+                                           uint32_t P2) {
+  // a row's lanes 0 / 15 have no left / right neighbour: the sentinel there
+  const uint32_t lo0 = dshift_or<kRShr1>(st[PQ - 1], q == 0 ? kSent << 16 : 0u);
+  const uint32_t hiN = dshift_or<kRShl1>(st[0], q == 15 ? kSent : 0u);
+  const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
+  u16x2 mn = splat(0xFFFF);
+  uint32_t oldk = 0;
+#pragma unroll
+  for (int k = 0; k < PQ; ++k) mn = vmin(mn, as_v(sgm_pair<PQ>(st, k, oldk, c[k], P1, mp2, mpv, lo0, hiN)));
+  uint32_t m = as_u(mn);
+  m = min(m & 0xFFFFu, m >> 16);
+  m = dmin<kQX1>(m);
+  m = dmin<kQX2>(m);
+  m = dmin<kRHalfMirror>(m);
+  m = dmin<kRMirror>(m);
+  return m;
+}
+
+template <int PQ>
+__device__ __forceinline__ void vadd(uint32_t* a, const uint32_t* b) {
+#pragma unroll
+  for (int k = 0; k < PQ; ++k) a[k] = as_u(as_v(a[k]) + as_v(b[k]));
+}
+
+// C of one column from the top-down path: V(y) = C + min(Vp[d], Vp[d-1] + P1, Vp[d+1] + P1,
+// min Vp + P2) - min Vp with Vp = V(y-1) of the same stripe's path (zero above its first
+// row), so C = V(y) - (that minimum) + min Vp -- the cost pass's u16 arithmetic undone
+// exactly (modular).  16 lanes per row as step16; m = min Vp (stored by the cost pass).
+template <int PQ>
+__device__ __forceinline__ void derive16(const uint32_t* vp, const uint32_t* v, uint32_t* c, uint32_t m, u16x2 P1,
+                                         uint32_t P2, int q) {
+  // a row's lanes 0 / 15 have no left / right neighbour: the sentinel there
+  const uint32_t lo0 = dshift_or<kRShr1>(vp[PQ - 1], q == 0 ? kSent << 16 : 0u);
+  const uint32_t hiN = dshift_or<kRShl1>(vp[0], q == 15 ? kSent : 0u);
+  const u16x2 mp2 = splat(m + P2), mpv = splat(m);
+#pragma unroll
+  for (int k = 0; k < PQ; ++k) {
+    const uint32_t cur = vp[k];
+    const uint32_t lo = k > 0 ? vp[k - 1] : lo0;
+    const uint32_t hi = k < PQ - 1 ? vp[k + 1] : hiN;
+    const u16x2 dm = as_v(__builtin_amdgcn_alignbit(cur, lo, 16));
+    const u16x2 dp = as_v(__builtin_amdgcn_alignbit(hi, cur, 16));
+    const u16x2 mm = vmin(vmin(dm, dp) + P1, vmin(as_v(cur), mp2));
+    c[k] = as_u(as_v(v[k]) - mm + mpv);
+  }
+}
+
 // ------------------------------------------------------------------ fused cost + vertical pass
 // One block (G*CB threads) per (CB columns, stripe, pair), G lanes per column.  Per new hsum
 // row (the row entering the 7-row window) the block stages the 3 image rows of its column
@@ -206,10 +275,144 @@ __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q
 // row's image bytes are loaded right after the current row is staged and taken before the
 // row's C / V stores (vmcnt retires in order: a wait for them behind the stores would also
 // wait for the stores).  Integer arithmetic as oracle/sgbm_ref.cpp (order-independent sums).
-template <int D, int CB, int G>
-__global__ __launch_bounds__(G * CB, 1) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
+// The left->right path (LP = true, the default schedule): the block also runs the L path of
+// its CB columns -- per group of 4 output rows, one wave (16 lanes per row, D/16 disparities
+// per lane) steps the 4 rows across the columns over C read back from a 4-row LDS ring, starting
+// from the state the block of the previous column range handed over for those rows, stores the
+// row pass's checkpoints and hands its own last state on (SgLink below).  The row pass then
+// needs only its right->left sweep: one V read per pair fewer.
+struct SgLink {
+  uint32_t* ckpt;           // [B][H][nck][16][CKW] L checkpoints (the row pass's, per row)
+  int nck, nk;              // checkpoint slots per row; column blocks per stripe
+  uint64_t* hand;           // [B][H][2][PQ16][16] hand-off granules {tag, word}, by column-block parity
+  uint32_t* ctl;            // [0] ticket, [1] generation, [2] timeouts, [4 + b] pair failed
+};
+
+typedef __attribute__((address_space(1))) unsigned long long sg_gu64;
+typedef __attribute__((address_space(1))) unsigned int sg_gu32;
+
+// The L path of a group of nrows (<= 4) output rows y0.. of one column block (LP schedule), run
+// by one wave while the block's other waves wait at a barrier (so at raised priority): lane = row
+// r (4) x disparity run q (16 lanes, D/32 words each); C from the block's LDS ring (row y0 + r in
+// slot s0 + r mod 4), the entering state from the previous column block's hand-off granules, the row pass's
+// checkpoints, the leaving state handed on.  Not inlined:
+// inlined into the cost pass's 7-way unrolled row loop its address arithmetic was hoisted and
+// kept the whole kernel above 128 VGPRs (156 VGPRs / 3 waves per SIMD, or 33 spills at 128).
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+
+// the granules of rows ya.. (nr rows) of column block kb - 1 from memory: one pass, no waiting
+template <int PQ16>
+__device__ __forceinline__ void sg_load_granules(const SgLink& lk, int b, int H, int kb, int ya, int nr, uint64_t* g) {
+  const int lane = (int)(threadIdx.x & 63), rr = lane >> 4, qq = lane & 15;
+  const int64_t hrow = ((int64_t)b * H + ya + min(rr, nr - 1)) * 2;
+  sg_gu64* hp = (sg_gu64*)lk.hand + ((hrow + ((kb - 1) & 1)) * PQ16) * 16 + qq;
+#pragma unroll
+  for (int k = 0; k < PQ16; ++k) g[k] = __hip_atomic_load(hp + k * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int D, int CB>
+__device__ __attribute__((noinline)) void sg_run_L(SgLink lk, lds_cu32* ring, int s0, int b, int H, int kb, int c0,
+                                                   int width1, uint32_t gen, int y0, int nrows, uint32_t P1s, int P2) {
+  // the arguments are wave-uniform: keep them (and the loop control) in SGPRs
+  auto uni = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
+  s0 = uni(s0), b = uni(b), H = uni(H), kb = uni(kb), c0 = uni(c0), width1 = uni(width1);
+  gen = (uint32_t)uni((int)gen), y0 = uni(y0), nrows = uni(nrows), P1s = (uint32_t)uni((int)P1s), P2 = uni(P2);
+  constexpr int PQ16 = D / 32;
+  constexpr int CKW = PQ16 + 1 <= 4 ? 4 : 8;
+  constexpr int RW = CB * D / 2 + 16;
+  __builtin_amdgcn_s_setprio(3);
+  const u16x2 P1 = splat(P1s);
+  const int lane = (int)(threadIdx.x & 63);
+  const int rr = lane >> 4, qq = lane & 15;
+  const int yr = y0 + min(rr, nrows - 1);  // lanes of missing rows repeat the last row (no stores)
+  const bool live = rr < nrows;
+  uint32_t lst[PQ16];
+  uint32_t lmin = 0;
+  const int64_t hrow = ((int64_t)b * H + yr) * 2;
+  if (kb == 0) {
+#pragma unroll
+    for (int g = 0; g < PQ16; ++g) lst[g] = 0;  // the path starts at x1 = 0 from the zero state
+  } else {
+    // granules {tag, word} of the previous column block (the data is its own flag: no fence,
+    // no ordering): re-read until every tag is (generation, kb - 1)
+    const uint32_t tag = (gen << 7) | (uint32_t)(kb - 1);
+    uint64_t gv[PQ16];
+    sg_load_granules<PQ16>(lk, b, H, kb, y0, nrows, gv);
+    uint64_t t0 = 0;
+    for (int it = 0;; ++it) {
+      bool ok = true;
+#pragma unroll
+      for (int g = 0; g < PQ16; ++g) {
+        lst[g] = (uint32_t)gv[g];
+        ok &= (uint32_t)(gv[g] >> 32) == tag;
+      }
+      if (__all(ok)) break;
+      // bounded wait: after 20 ms (or once the pair is marked failed upstream) give up, mark the
+      // pair failed (its disparities come out invalid) and count the timeout
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (it == 0) t0 = now;
+      const bool failed = __hip_atomic_load((sg_gu32*)lk.ctl + 4 + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+      if (failed || now - t0 > 2000000ull) {
+        if (lane == 0 && !failed) {
+          __hip_atomic_fetch_or((sg_gu32*)lk.ctl + 4 + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add((sg_gu32*)lk.ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int g = 0; g < PQ16; ++g) lst[g] = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      sg_load_granules<PQ16>(lk, b, H, kb, y0, nrows, gv);
+    }
+    // the state's minimum over d (the next step's minPrev)
+    uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+    for (int g = 0; g < PQ16; ++g) m = min(m, min(lst[g] & 0xFFFFu, lst[g] >> 16));
+    m = dmin<kQX1>(m);
+    m = dmin<kQX2>(m);
+    m = dmin<kRHalfMirror>(m);
+    lmin = dmin<kRMirror>(m);
+  }
+  const int nx = min(CB, width1 - c0);
+  // checkpoints after the columns x1 = W1 - 9 - 8 m (m >= 0): the row pass's segment m starts there
+  const int i0 = (((width1 - 9 - c0) % 8) + 8) % 8;
+  uint32_t* ckrow = lk.ckpt + (((int64_t)b * H + yr) * lk.nck * 16 + qq) * CKW;
+  lds_cu32* rbase = ring + ((s0 + rr) & 3) * RW + qq * PQ16;  // row y0 + r sits in ring slot s0 + r
+  uint32_t c[PQ16];
+#pragma unroll
+  for (int g = 0; g < PQ16; ++g) c[g] = rbase[g];
+#pragma unroll 1
+  for (int i = 0; i < nx; ++i) {
+    uint32_t cn[PQ16];  // the next column's C, read one step ahead
+    const int in = min(i + 1, CB - 1);
+#pragma unroll
+    for (int g = 0; g < PQ16; ++g) cn[g] = rbase[in * (D / 2) + g];
+    lmin = step16<PQ16>(lst, c, qq, P1, lmin, P2);
+    if (((i - i0) & 7) == 0 && c0 + i <= width1 - 9 && live) {
+      const int slot = (width1 - 9 - (c0 + i)) >> 3;
+      uint32_t v[CKW];
+#pragma unroll
+      for (int g = 0; g < CKW; ++g) v[g] = g < PQ16 ? lst[g] : g == PQ16 ? lmin : 0u;
+      sg_gu32* cp = (sg_gu32*)(ckrow + (int64_t)slot * 16 * CKW);  // global, not flat, stores
+#pragma unroll
+      for (int g = 0; g < CKW; ++g) cp[g] = v[g];
+    }
+#pragma unroll
+    for (int g = 0; g < PQ16; ++g) c[g] = cn[g];
+  }
+  if (kb < lk.nk - 1 && live) {
+    const uint64_t tag = (uint64_t)((gen << 7) | (uint32_t)kb) << 32;
+    sg_gu64* hp = (sg_gu64*)lk.hand + ((hrow + (kb & 1)) * PQ16) * 16 + qq;
+#pragma unroll
+    for (int g = 0; g < PQ16; ++g) __hip_atomic_store(hp + g * 16, tag | lst[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <int D, int CB, int G, bool LP>
+__global__ __launch_bounds__(G * CB, LP ? 4 : 1) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
                                                     int64_t stride, int pitch, SgParams p, uint16_t* __restrict__ Vvol,
-                                                    uint16_t* __restrict__ Mvol) {
+                                                    uint16_t* __restrict__ Mvol, SgLink lk) {
   constexpr int DQ = D / G, PQ = DQ / 2, NV2 = DQ / 4;
   constexpr int NT = G * CB;                // threads: G lanes per column
   constexpr int kCX = CB + 6;               // pixel-cost columns (7-wide box apron)
@@ -217,15 +420,38 @@ __global__ __launch_bounds__(G * CB, 1) void k_sg_costvert(const uint8_t* __rest
   constexpr int NLI = kCX + 4, NRI = NRC + 4;  // staged pixels per image row (core + 2 each side)
   constexpr int NIMG = 3 * (NLI + NRI);     // staged bytes per hsum row
   constexpr int PER = (NIMG + NT - 1) / NT;  // staged bytes per thread
+  constexpr int PQ16 = D / 32;              // L path: packed words per lane (16 lanes per row)
+  constexpr int CKW = PQ16 + 1 <= 4 ? 4 : 8;
+  // C ring of the L path: 4 rows x CB columns x D/2 words, the row stride = 16 mod 32 words so
+  // the 4 rows' lanes (3 words apart within a row) hit disjoint banks
+  constexpr int RW = LP ? CB * D / 2 + 16 : 1;
   __shared__ uint8_t sImg[3][NLI + NRI];
   __shared__ uint32_t sCh[kCX + 2 + NRC + 2];                       // (Sobel, intensity), L then R
   __shared__ uint32_t sW[3][kCX + NRC];                            // u, BT min, BT max, L then R
   __shared__ __attribute__((aligned(16))) uint16_t sPC[kCX][D];    // pixel cost
+  __shared__ uint32_t sRing[LP ? 4 : 1][RW];
+  __shared__ int sUnit;
   const int tid = threadIdx.x, lane = tid & 63, q = lane % G;
   const int col = (tid >> 6) * (64 / G) + lane / G;  // 0..CB-1
-  const XcdBlock xb = xcd_block();  // neighbouring column blocks (shared image rows) on one XCD
-  const int c0 = xb.x * CB;
-  const int s = xb.y, b = xb.z;
+  int c0, s, b, kb;
+  if constexpr (LP) {
+    // units (column block k, pair b, stripe s) in ticket order, k major: the block that hands
+    // this one its L states took its ticket nchains tickets earlier, so it is running or done
+    // whatever the dispatch order (no deadlock), and usually far enough ahead that nobody waits
+    if (tid == 0) sUnit = (int)atomicAdd(lk.ctl, 1u);
+    __syncthreads();
+    const int nch = (int)gridDim.x / lk.nk;
+    const int t = sUnit;
+    kb = t / nch;
+    const int ch = t - kb * nch;
+    b = ch / p.nstripes;
+    s = ch - b * p.nstripes;
+    c0 = kb * CB;
+  } else {
+    const XcdBlock xb = xcd_block();  // neighbouring column blocks (shared image rows) on one XCD
+    c0 = xb.x * CB;
+    s = xb.y, b = xb.z, kb = xb.x;
+  }
   const int H = p.H, W = p.W;
   const int start = max(min(s * p.ss - p.ov, H), 0);
   const int end = min((s + 1) * p.ss, H);
@@ -364,6 +590,7 @@ __global__ __launch_bounds__(G * CB, 1) void k_sg_costvert(const uint8_t* __rest
   const int x1 = c0 + col;
   const int64_t plane = (int64_t)p.width1 * D;
   const int64_t colofs = (int64_t)b * (p.HG4 + p.nstripes) * 4 * plane + (int64_t)x1 * 4 * D + q * DQ;
+  const uint32_t gen = LP ? lk.ctl[1] : 0u;
   // V step + stores of output row y
   auto vrow = [&](int y) {
     minPrev = hstepG<PQ, G>(st, crun, q, P1, minPrev, p.P2);
@@ -382,6 +609,24 @@ __global__ __launch_bounds__(G * CB, 1) void k_sg_costvert(const uint8_t* __rest
       }
       // min over d of this V row (the next row's minPrev): the row pass's inversion needs it
       if (q == 0) Mvol[(colofs - q * DQ + yo) / D] = (uint16_t)minPrev;
+    }
+    if constexpr (LP) {
+      if (out_row) {
+        // groups of 4 rows at a phase of their own per column block (kb & 3), so the blocks
+        // sharing a CU -- which otherwise run in lockstep -- do not all wait for their L waves at once
+        const int yi = y - first_out + (kb & 3);
+        uint32_t* rp = &sRing[yi & 3][col * (D / 2) + q * PQ];
+#pragma unroll
+        for (int k = 0; k < PQ; ++k) rp[k] = crun[k];
+        if ((yi & 3) == 3 || y == end - 1) {  // a complete group (or the stripe's last rows)
+          __syncthreads();
+          const int y0 = max(first_out, y - (yi & 3));
+          if ((tid >> 6) == ((yi >> 2) & 3))
+            sg_run_L<D, CB>(lk, (lds_cu32*)&sRing[0][0], (y0 - first_out + (kb & 3)) & 3, b, H, kb, c0, p.width1, gen, y0,
+                            y - y0 + 1, (uint32_t)p.P1, p.P2);
+          __syncthreads();  // the ring is rewritten from the next row on
+        }
+      }
     }
   };
   vrow(start);
@@ -412,75 +657,6 @@ __global__ __launch_bounds__(G * CB, 1) void k_sg_costvert(const uint8_t* __rest
   }
 }
 
-// ------------------------------------------------------------------ row bands: C + left/right paths + WTA
-// A row of 16 lanes is one DPP row: neighbours by row_shr/row_shl:1, minima by quad xor 1/2,
-// row_half_mirror and row_mirror.
-constexpr int kRShr1 = 0x111;        // row_shr:1 -- value of lane i-1
-constexpr int kRShl1 = 0x101;        // row_shl:1 -- value of lane i+1
-constexpr int kRHalfMirror = 0x141;  // lane i <-> 7-i within each half row
-constexpr int kRMirror = 0x140;      // lane i <-> 15-i
-
-template <int CTRL>
-__device__ __forceinline__ uint32_t rdpp(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
-}
-
-// Ring sizes of the row pass's LDS windows (powers of two): keys cover x2 over 2D + 4 SEG
-// columns, raw disparities wait D + 2 SEG columns for their check.
-__host__ __device__ constexpr int sg_pow2(int n) { return n <= 1 ? 1 : 2 * sg_pow2((n + 1) / 2); }
-__host__ __device__ constexpr int sg_ring_keys(int D) { return sg_pow2(2 * D + 32); }
-__host__ __device__ constexpr int sg_ring_raw(int D) { return sg_pow2(D + 16); }
-
-// One path step of a 16-lane row (PQ packed words per lane); returns the row minimum.
-template <int PQ>
-__device__ __forceinline__ uint32_t step16(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
-                                           uint32_t P2) {
-  // a row's lanes 0 / 15 have no left / right neighbour: the sentinel there
-  const uint32_t lo0 = dshift_or<kRShr1>(st[PQ - 1], q == 0 ? kSent << 16 : 0u);
-  const uint32_t hiN = dshift_or<kRShl1>(st[0], q == 15 ? kSent : 0u);
-  const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
-  u16x2 mn = splat(0xFFFF);
-  uint32_t oldk = 0;
-#pragma unroll
-  for (int k = 0; k < PQ; ++k) mn = vmin(mn, as_v(sgm_pair<PQ>(st, k, oldk, c[k], P1, mp2, mpv, lo0, hiN)));
-  uint32_t m = as_u(mn);
-  m = min(m & 0xFFFFu, m >> 16);
-  m = dmin<kQX1>(m);
-  m = dmin<kQX2>(m);
-  m = dmin<kRHalfMirror>(m);
-  m = dmin<kRMirror>(m);
-  return m;
-}
-
-template <int PQ>
-__device__ __forceinline__ void vadd(uint32_t* a, const uint32_t* b) {
-#pragma unroll
-  for (int k = 0; k < PQ; ++k) a[k] = as_u(as_v(a[k]) + as_v(b[k]));
-}
-
-// C of one column from the top-down path: V(y) = C + min(Vp[d], Vp[d-1] + P1, Vp[d+1] + P1,
-// min Vp + P2) - min Vp with Vp = V(y-1) of the same stripe's path (zero above its first
-// row), so C = V(y) - (that minimum) + min Vp -- the cost pass's u16 arithmetic undone
-// exactly (modular).  16 lanes per row as step16; m = min Vp (stored by the cost pass).
-template <int PQ>
-__device__ __forceinline__ void derive16(const uint32_t* vp, const uint32_t* v, uint32_t* c, uint32_t m, u16x2 P1,
-                                         uint32_t P2, int q) {
-  // a row's lanes 0 / 15 have no left / right neighbour: the sentinel there
-  const uint32_t lo0 = dshift_or<kRShr1>(vp[PQ - 1], q == 0 ? kSent << 16 : 0u);
-  const uint32_t hiN = dshift_or<kRShl1>(vp[0], q == 15 ? kSent : 0u);
-  const u16x2 mp2 = splat(m + P2), mpv = splat(m);
-#pragma unroll
-  for (int k = 0; k < PQ; ++k) {
-    const uint32_t cur = vp[k];
-    const uint32_t lo = k > 0 ? vp[k - 1] : lo0;
-    const uint32_t hi = k < PQ - 1 ? vp[k + 1] : hiN;
-    const u16x2 dm = as_v(__builtin_amdgcn_alignbit(cur, lo, 16));
-    const u16x2 dp = as_v(__builtin_amdgcn_alignbit(hi, cur, 16));
-    const u16x2 mm = vmin(vmin(dm, dp) + P1, vmin(as_v(cur), mp2));
-    c[k] = as_u(as_v(v[k]) - mm + mpv);
-  }
-}
-
 // Wave per 4 rows (one block), 16 lanes per row, D/16 disparities per lane.  Sweep 1 walks
 // the row left->right over C (prefetched PF columns ahead) running the L path and storing
 // its state (+ minimum) every SEG columns -- at x = W1-1-SEG*(s+1), the left neighbour of sweep
@@ -491,7 +667,13 @@ __device__ __forceinline__ void derive16(const uint32_t* vp, const uint32_t* v, 
 // by an LDS atomicMin -- the serial rule "replace iff disp2cost > cost" of sgbm_ref.cpp (the
 // smallest cost wins, among equal costs the largest x1, the first one the scan visits).  The
 // pseudo left-right check then runs on the LDS row and writes the row-major raw disparity.
-template <int D>
+// SW: kSwBoth = both sweeps (checkpoints per 4-row block: [B][row blocks][nck][64 lanes][CKW]);
+// kSwRight = sweep 2 only, over the per-row checkpoints ([B][H][nck][16 lanes][CKW]) the L-path
+// cost pass stored.  (r5, measured and not kept: sweep 1 as a launch of its own, kSwLeft, per chunk
+// of pairs on a second stream beside the next chunk's cost pass -- bit-exact, 8.1-8.4 vs 8.1-8.2 ms:
+// the cost pass slowed by what sweep 1 cost.)
+constexpr int kSwBoth = 0, kSwRight = 1, kSwLeft = 2;
+template <int D, int SW>
 __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t* __restrict__ Vvol,
                                                                  const uint16_t* __restrict__ Mvol, SgParams p,
                                                                  uint32_t* __restrict__ ckpt, int nck,
@@ -500,9 +682,10 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
   constexpr int CKW = PQ + 1 <= 4 ? 4 : 8;
   constexpr int XS = 2 * D;  // u32 words per column of a 4-row group
   constexpr int RK = sg_ring_keys(D), RS = sg_ring_raw(D);
-  __shared__ uint32_t s_key[4][RK];  // right-view keys of the live x2 window (ring, by x2)
-  __shared__ __attribute__((aligned(16))) uint16_t s_S[4][D];  // one column's S of each row (WTA neighbours)
-  __shared__ int16_t s_raw[4][RS];   // raw disparities awaiting their check (ring, by x1)
+  constexpr bool S1 = SW != kSwRight, S2 = SW != kSwLeft;
+  __shared__ uint32_t s_key[4][S2 ? RK : 1];  // right-view keys of the live x2 window (ring, by x2)
+  __shared__ __attribute__((aligned(16))) uint16_t s_S[4][S2 ? D : 2];  // one column's S of each row (WTA neighbours)
+  __shared__ int16_t s_raw[4][S2 ? RS : 2];   // raw disparities awaiting their check (ring, by x1)
   const int lane = threadIdx.x, q = lane & 15, r = lane >> 4;
   // consecutive row groups on one XCD: a group's first row reads the previous group's last
   // V row, which that group's wave streams at about the same time (an L2 hit)
@@ -515,11 +698,13 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
   uint32_t* key = s_key[r];
   int16_t* sraw = s_raw[r];
   const int INVALID = (p.minD - 1) * 16;
-  for (int k = q; k < RK; k += 16) key[k] = 0xFFFFFFFFu;
   int16_t* out = raw + ((int64_t)b * H + yy) * W;
-  if (rowok)  // columns left of the first x1 (and right of the last) never get a disparity
-    for (int x = q; x < W; x += 16)
-      if (x < p.minX1 || x >= p.minX1 + W1) out[x] = (int16_t)INVALID;
+  if constexpr (S2) {
+    for (int k = q; k < RK; k += 16) key[k] = 0xFFFFFFFFu;
+    if (rowok)  // columns left of the first x1 (and right of the last) never get a disparity
+      for (int x = q; x < W; x += 16)
+        if (x < p.minX1 || x >= p.minX1 + W1) out[x] = (int16_t)INVALID;
+  }
   // pseudo left-right check of pixel x1 (its right-view keys are final once the sweep has
   // passed x1 - D: every x2 it reads lies within D of x1 + minX1 - minD)
   auto disp2 = [&](int x2) -> int {
@@ -546,7 +731,12 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
   // lanes with no pixel to check store into this lane's words of the dummy checkpoint slot, so
   // every segment issues the same global stores: with a conditional store the compiler's vmcnt
   // bookkeeping falls back to draining every load in flight at the next segment
-  int16_t* const sink = reinterpret_cast<int16_t*>(ckpt + ((((int64_t)b * gridDim.x + blk) * nck + nck - 1) * 64 + lane) * (PQ + 1 <= 4 ? 4 : 8));
+  // (S1 layout: [B][row blocks][nck][64 lanes][CKW]; per-row layout: [B][H][nck][16 lanes][CKW])
+  auto ckptr = [&](int slot) -> uint32_t* {
+    return SW == kSwBoth ? ckpt + ((((int64_t)b * gridDim.x + blk) * nck + slot) * 64 + lane) * CKW
+              : ckpt + ((((int64_t)b * H + yy) * nck + slot) * 16 + q) * CKW;
+  };
+  int16_t* const sink = reinterpret_cast<int16_t*>(ckptr(nck - 1));
   int next_chk = W1 - 1;  // highest pixel not yet checked
   // V of this row and of the previous row of the same stripe's path: inside the stripe the
   // row above, at its first output row (s > 0) the overlap row the cost pass kept in group
@@ -581,7 +771,6 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
   const int pgrp = ptop ? p.HG4 + stripe : yp >> 2, psub = ptop ? 0 : yp & 3;
   const uint32_t voffM = pzero ? 0x80000000u : (uint32_t)(((int64_t)pgrp * W1 * 4 + psub) * 2);
   const u16x2 P1 = splat(p.P1);
-  const int64_t ckbase = ((int64_t)b * gridDim.x + blk) * nck;
   // column offsets are wave-uniform (readfirstlane keeps them in SGPRs: a VGPR soffset would
   // make the compiler wrap each load in a waterfall loop)
   auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
@@ -600,6 +789,7 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
   // so the scheduler overlaps one column's serial min-reduction with the next column's work.
   // V and the previous row PD columns ahead (a ring of PD column buffers)
   static_assert(PF == SEG && SEG % PD == 0, "ring slots line up across blocks");
+  if constexpr (S1) {
   uint32_t st[PQ], vb[PD][PQ], pb[PD][PQ], mb[PD];
   uint32_t minPrev = 0;
   const int xs = ((W1 - 1) & (SEG - 1)) - (SEG - 1);
@@ -631,7 +821,7 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
     }
     const int rem = W1 - 1 - SEG - (x0 + SEG - 1);
     const int slot = rem >= 0 ? rem / SEG : nck - 1;
-    uint32_t* cp = ckpt + ((ckbase + slot) * 64 + lane) * CKW;
+    uint32_t* cp = ckptr(slot);
     uint32_t v[CKW];
 #pragma unroll
     for (int kk = 0; kk < CKW; ++kk) v[kk] = kk < PQ ? st[kk] : kk == PQ ? minPrev : 0u;
@@ -642,6 +832,8 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
 #pragma unroll 1
   for (int x0 = xs + SEG; x0 < W1; x0 += SEG) block1(x0, std::false_type{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the checkpoints, re-read below by the lanes that stored them
+  }
+  if constexpr (!S2) return;
 
   // ---- sweep 2: segments s of reflected columns x' = SEG*s + i (x1 = W1-1-x'), right to left
   const int nseg = (W1 + SEG - 1) / SEG;
@@ -656,7 +848,7 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
   uint32_t Vn[SEG][PQ], Pn[SEG][PQ], Mn[SEG], ckn[CKW];
   auto ldck = [&](int sg) {
     const int slot = SEG * (sg + 1) > W1 - 1 ? nck - 1 : sg;
-    const uint32_t* cp = ckpt + ((ckbase + slot) * 64 + lane) * CKW;
+    const uint32_t* cp = ckptr(slot);
 #pragma unroll
     for (int kk = 0; kk < CKW; kk += 4) {
       const uint4 w4 = *reinterpret_cast<const uint4*>(cp + kk);
@@ -821,7 +1013,9 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
 }
 
 // ------------------------------------------------------------------ median 3x3
-__global__ void k_sg_median(const int16_t* __restrict__ raw, int16_t* __restrict__ out, int W, int H) {
+// fail (may be null): pairs whose L-path hand-off timed out come out invalid everywhere
+__global__ void k_sg_median(const int16_t* __restrict__ raw, int16_t* __restrict__ out, int W, int H,
+                            const uint32_t* __restrict__ fail, int16_t invalid) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, b = blockIdx.z;
   if (x >= W) return;
   const int16_t* s = raw + (int64_t)b * W * H;
@@ -840,15 +1034,35 @@ __global__ void k_sg_median(const int16_t* __restrict__ raw, int16_t* __restrict
   SG_S(0, 3) SG_S(5, 8) SG_S(4, 7) SG_S(3, 6) SG_S(1, 4) SG_S(2, 5) SG_S(4, 7) SG_S(4, 2) SG_S(6, 4)
   SG_S(4, 2)
 #undef SG_S
-  out[((int64_t)b * H + y) * W + x] = (int16_t)v[4];
+  out[((int64_t)b * H + y) * W + x] = (fail && fail[b]) ? invalid : (int16_t)v[4];
 }
 
-// Launch-shape knobs of the cost pass (read per launch; every variant is bit-identical and
-// parity-tested): FVO_SG_G lanes per column (4 or 8), FVO_SG_CB columns per block (G=4: 32/64;
-// G=8: 16/32).
+// Per call of the L-path schedule: ticket counter reset, generation advanced (never 0, < 2^25:
+// tags are generation << 7 | column block), failure flags of the batch's pairs cleared.
+__global__ void k_sg_prep(uint32_t* ctl, int nb) {
+  const int t = threadIdx.x;
+  if (t == 0) {
+    ctl[0] = 0;
+    const uint32_t g = ctl[1] + 1;
+    ctl[1] = g >= (1u << 25) ? 1u : g;
+  }
+  for (int b = t; b < nb; b += blockDim.x) ctl[4 + b] = 0;
+}
+
+// Schedules and launch shapes (read per launch; every variant is bit-identical and
+// parity-tested), FVO_SG_MODE:
+//   (default)  one cost pass, one row pass running both sweeps, with FVO_SG_G lanes per column
+//              (4 or 8) and FVO_SG_CB columns per block (G=4: 32/64; G=8: 16/32)
+//   lpath      the L path in the cost pass, handed from column block to column block: one V read
+//              per pair fewer (<= 300 MB/pair) but slower -- DESIGN.md §4.2 r5
 int env_int(const char* name, int def) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : def;
+}
+enum SgMode { kSgClassic, kSgLPath };
+SgMode sg_mode() {
+  const char* v = getenv("FVO_SG_MODE");
+  return v && std::string(v) == "lpath" ? kSgLPath : kSgClassic;
 }
 
 SgParams make_params(const fvo_config& c) {
@@ -873,28 +1087,47 @@ SgParams make_params(const fvo_config& c) {
   return p;
 }
 
-// Checkpoints of the left->right path per (pair, 4-row block): at x = W1-9-8s, s < nck.
+// Checkpoints of the left->right path (per 4-row block or per row): at x = W1-9-8s, s < nck.
 int sg_nck(const SgParams& p) { return p.width1 / 8 + 2; }  // + a dummy slot
 int sg_ckw(int D) { return D / 32 + 1 <= 4 ? 4 : 8; }
 int sg_nblk(const SgParams& p) { return (p.H + 3) / 4; }
+constexpr int kSgCB = 32;  // columns per cost block of the L-path schedule
+int sg_nk(const SgParams& p) { return (p.width1 + kSgCB - 1) / kSgCB; }
 
 template <int D>
 void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_t* R, int nb, int64_t stride,
                  int pitch, int16_t* disp, hipStream_t s) {
-  const int g = env_int("FVO_SG_G", 8), cb = env_int("FVO_SG_CB", g == 8 ? 32 : 64);
   uint16_t* V = ctx->sg_V;
   uint16_t* M = ctx->sg_M;
-  const dim3 gcv((p.width1 + cb - 1) / cb, p.nstripes, nb);
-  FVO_TIMED(ctx, KN_SG_VERT, s, {
-    if (g == 8 && cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 8>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, V, M);
-    else if (g == 8) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 16, 8>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, V, M);
-    else if (cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 4>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, V, M);
-    else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 64, 4>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, V, M);
-  });
-  FVO_TIMED(ctx, KN_SG_ROWS, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_rows<D>), dim3(sg_nblk(p), nb), dim3(64), 0, s,
-                                                   V, M, p, ctx->sg_ckpt, sg_nck(p), ctx->sg_raw));
+  const int nck = sg_nck(p);
+  const int16_t invalid = (int16_t)((p.minD - 1) * 16);
+  const SgMode mode = sg_mode();
+  if (mode == kSgClassic) {
+    const int g = env_int("FVO_SG_G", 8), cb = env_int("FVO_SG_CB", g == 8 ? 32 : 64);
+    const dim3 gcv((p.width1 + cb - 1) / cb, p.nstripes, nb);
+    const SgLink lk{};
+    FVO_TIMED(ctx, KN_SG_VERT, s, {
+      if (g == 8 && cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 8, false>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, V, M, lk);
+      else if (g == 8) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 16, 8, false>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, V, M, lk);
+      else if (cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 4, false>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, V, M, lk);
+      else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 64, 4, false>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, V, M, lk);
+    });
+    FVO_TIMED(ctx, KN_SG_ROWS, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_rows<D, kSwBoth>), dim3(sg_nblk(p), nb), dim3(64), 0, s,
+                                                     V, M, p, ctx->sg_ckpt, nck, ctx->sg_raw));
+    FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.W + 255) / 256, p.H, nb), dim3(256), 0, s,
+                                                       ctx->sg_raw, disp, p.W, p.H, nullptr, invalid));
+    return;
+  }
+  const int nk = sg_nk(p);
+  const SgLink lk{ctx->sg_ckpt, nck, nk, ctx->sg_hand, ctx->sg_ctl};
+  hipLaunchKernelGGL(k_sg_prep, dim3(1), dim3(256), 0, s, ctx->sg_ctl, nb);
+  FVO_TIMED(ctx, KN_SG_VERT, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, kSgCB, 8, true>),
+                                                   dim3(nk * p.nstripes * nb), dim3(8 * kSgCB), 0, s, L, R, stride, pitch,
+                                                   p, V, M, lk));
+  FVO_TIMED(ctx, KN_SG_ROWS, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_rows<D, kSwRight>), dim3(sg_nblk(p), nb), dim3(64), 0, s,
+                                                   V, M, p, ctx->sg_ckpt, nck, ctx->sg_raw));
   FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.W + 255) / 256, p.H, nb), dim3(256), 0, s,
-                                                     ctx->sg_raw, disp, p.W, p.H));
+                                                     ctx->sg_raw, disp, p.W, p.H, ctx->sg_ctl + 4, invalid));
 }
 
 }  // namespace
@@ -924,12 +1157,20 @@ int sgbm_init(fvo_ctx* ctx) {
   // stripes' overlap rows); sg_ckpt: the left->right path checkpoints; sg_raw: pre-median
   // disparity [B][H][W]
   const int64_t vol = (int64_t)(p.HG4 + p.nstripes) * 4 * plane;
+  // (the per-block layout of the classic schedule is the larger one: 64 lanes per 4 rows)
   const int64_t ckp = (int64_t)sg_nblk(p) * sg_nck(p) * 64 * sg_ckw(p.D);
+  // sg_hand: the L path's hand-off granules [B][H][2][D/32][16] u64; sg_ctl: ticket, generation,
+  // timeout count, per-pair failure flags.  Both zeroed once (tags of a zeroed granule never match)
+  const int64_t hand = (int64_t)p.H * 2 * (p.D / 32) * 16;
+  if (sg_nk(p) >= 128) return fvo_fail(ctx, "SGBM: image too wide (width - numDisparities > 4064)");
   // sg_M: min over d of every stored V row, [B][HG4 + nstripes][width1][4] u16
   if ((rc = fvo_alloc(ctx, &ctx->sg_V, B * vol)) || (rc = fvo_alloc(ctx, &ctx->sg_M, B * vol / p.D)) ||
       (rc = fvo_alloc(ctx, &ctx->sg_ckpt, B * ckp)) ||
-      (rc = fvo_alloc(ctx, &ctx->sg_raw, B * p.H * p.W)))
+      (rc = fvo_alloc(ctx, &ctx->sg_raw, B * p.H * p.W)) || (rc = fvo_alloc(ctx, &ctx->sg_hand, B * hand)) ||
+      (rc = fvo_alloc(ctx, &ctx->sg_ctl, 4 + B)))
     return rc;
+  FVO_HIP(ctx, hipMemset(ctx->sg_hand, 0, B * hand * sizeof(uint64_t)));
+  FVO_HIP(ctx, hipMemset(ctx->sg_ctl, 0, (4 + B) * sizeof(uint32_t)));
   return 0;
 }
 

@@ -49,11 +49,22 @@ def warmup_pairs(n_pairs: int, rank: int, world: int, halo: int) -> int:
     return frame_shard(n_pairs, rank, world)[0] - frame_shard(n_pairs, rank, world, halo)[0]
 
 
+def _world_rank(group=None) -> tuple[int, int]:
+    """(world size, rank) of ``group``; (1, 0) when no process group exists (one process:
+    ``bench.py --shard frames --gpus 1`` starts none)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1, 0
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
 def gather_relative_poses(T_local: torch.Tensor, status_local: torch.Tensor, n_pairs: int,
                           group=None) -> tuple[np.ndarray, np.ndarray]:
     """All-gather every rank's relative transforms (f64 [n_r,4,4]) and statuses into the
-    full per-pair arrays (rank order == frame order)."""
-    world = dist.get_world_size(group)
+    full per-pair arrays (rank order == frame order).  Without a process group the local
+    arrays are the whole sequence and are returned as they are."""
+    world, _ = _world_rank(group)
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
+        return T_local.cpu().numpy(), status_local.cpu().numpy()
     # gloo (CPU tests, or GPU ranks sharing one card) all-gathers host tensors
     dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else T_local.device
     T_local, status_local = T_local.to(dev), status_local.to(dev)
@@ -88,7 +99,7 @@ def run_sequence_sharded(make_frontend, L_all: torch.Tensor, R_all: torch.Tensor
     (default: every image is held, n_pairs = len(L_all) - 1)."""
     from . import eval as ev
     from .vo import _check_overflow
-    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    world, rank = _world_rank(group)
     if n_pairs is None:
         if first_image:
             raise ValueError("n_pairs is required when L_all starts past image 0")

@@ -129,7 +129,7 @@ class StereoFrontEnd:
         if self.ba_window:
             Kw = self.ba_window
             self.hkp[Kw - 2].copy_(kp[0])
-            self.hnkp[Kw - 2:Kw - 1].copy_(cnt[0:1])
+            self.hnkp[Kw - 2:Kw - 1].copy_(cnt[0:1].clamp(min=0))  # clamped like count_guard's output
             self.valid_from = Kw - 2
         self.has_prev = True
         # prime's kernels and copies (ORB, last_*) are queued on the caller's stream; the next

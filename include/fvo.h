@@ -266,12 +266,6 @@ int fvo_map_transform(fvo_ctx* ctx, const float* points, int32_t point_stride, c
                       int64_t cap, const double* T, int32_t* map_count, int64_t map_cap, double* map_xyz64,
                       float* map_xyz32, fvo_stream stream);
 
-/* Open3D PointCloud::VoxelDownSample(voxel_size) of n_points fp64 xyz points (device [n][3]):
- * vmin = min_bound - voxel/2, voxel index floor((p - vmin)/voxel), per voxel the fp64 sum of
- * its points in input order divided by the count.  Output: out [<= n][3] fp64 ordered by
- * voxel index (x, then y, then z — Open3D's hash-map order is unspecified), *n_out (device).
- * workspace: device scratch of fvo_voxel_workspace_bytes(n_points) bytes (caller-owned).
- * status (device, may be NULL): 0 ok, 1 = a voxel index outside [0, 2^21) (result invalid). */
 /* Pose chains of n_seq sequences advanced over one batch of n frames each (any stage; no
  * workspace) — stereo_slam.py:292-306 on the device, for the map of every posed frame:
  * for s < n_seq, i < n in order, a frame is posed when status[s*n + i] >= 0 (pose valid, or
@@ -307,6 +301,12 @@ int fvo_copy_regions(fvo_ctx* ctx, int32_t count, const fvo_region* regions, fvo
 int fvo_count_guard(fvo_ctx* ctx, const int32_t* counts, const int32_t* q_counts, int32_t n, int32_t sets,
                     int32_t* status, int32_t code, int32_t* counts_clamped, fvo_stream stream);
 
+/* Open3D PointCloud::VoxelDownSample(voxel_size) of n_points fp64 xyz points (device [n][3]):
+ * vmin = min_bound - voxel/2, voxel index floor((p - vmin)/voxel), per voxel the fp64 sum of
+ * its points in input order divided by the count.  Output: out [<= n][3] fp64 ordered by
+ * voxel index (x, then y, then z — Open3D's hash-map order is unspecified), *n_out (device).
+ * workspace: device scratch of fvo_voxel_workspace_bytes(n_points) bytes (caller-owned).
+ * status (device, may be NULL): 0 ok, 1 = a voxel index outside [0, 2^21) (result invalid). */
 int64_t fvo_voxel_workspace_bytes(int64_t n_points);
 int fvo_voxel_down_sample(fvo_ctx* ctx, const double* points, int64_t n_points, double voxel_size, void* workspace,
                           int64_t workspace_bytes, double* out, int32_t* n_out, int32_t* status, fvo_stream stream);
@@ -331,7 +331,8 @@ int fvo_timing_read(fvo_ctx* ctx, double* ms, int32_t* launches);
  * call (0 pyramid, 1 blurred pyramid, 2 FAST score map, 3/4/5 per-level counts before /
  * after the two retainBest passes, 6/7 PnP RANSAC per-iteration inlier counts / hypotheses of the
  * last fvo_pnp_ransac, 8 its per-frame RANSAC state: int32 best count, iteration bound, best
- * iteration, points).  For stage-by-stage parity tests only. */
+ * iteration, points, 9 the SGBM control words: u32 ticket, generation, L-path hand-off timeouts
+ * (must stay 0), reserved, then one failure flag per pair).  For stage-by-stage parity tests only. */
 int fvo_debug_buffer(fvo_ctx* ctx, int which, void** ptr, int64_t* bytes);
 
 #ifdef __cplusplus

@@ -69,3 +69,33 @@ def test_gather_poses_two_ranks_gloo():
         assert kf == [0.0, 1.0] and nl == [2, 3]
         # chaining the gathered poses equals the single-process chain exactly
         assert np.array_equal(ev.chain(T, S != -1), ev.chain(allT, S != -1))
+
+
+class _FakeFrontEnd:
+    """CPU stand-in for vo.StereoFrontEnd: pair i -> a translation of i (image values carry i)."""
+    B, ba_window = 4, 3
+
+    def prime(self, L, R):
+        self.prev = float(L[0, 0])
+
+    def step(self, L, R):
+        n = L.shape[0]
+        T = torch.eye(4, dtype=torch.float64).repeat(n, 1, 1)
+        T[:, 0, 3] = L[:, 0, 0].double()
+        self.T = T
+        return T, torch.ones(n, dtype=torch.int32)
+
+
+def test_run_sequence_sharded_without_process_group():
+    """bench.py --shard frames --gpus 1 starts no process group: the sharded run is the whole
+    sequence on one rank (it raised 'Default process group has not been initialized')."""
+    import torch.distributed as dist
+    from forest_slam_amd import dist as fd
+    from forest_slam_amd import eval as ev
+    assert not dist.is_initialized()
+    n_img = 11
+    imgs = torch.arange(n_img, dtype=torch.uint8)[:, None, None].expand(n_img, 2, 2).contiguous()
+    rows, T, S = fd.run_sequence_sharded(_FakeFrontEnd, imgs, imgs)
+    assert T.shape == (n_img - 1, 4, 4) and (S == 1).all()
+    assert np.array_equal(T[:, 0, 3], np.arange(1, n_img, dtype=np.float64))
+    assert np.array_equal(rows[:, 1], ev.chain(T, S != -1)[:, 0, 3])

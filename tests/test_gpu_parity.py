@@ -125,18 +125,27 @@ def test_bf_match_bit_exact(oracle_mod, frames):
         assert np.array_equal(m[i, :nm[i]], want)
 
 
+def sgbm_ctl(ctx):
+    """SGBM control words (debug buffer 9): ticket, generation, L-path hand-off timeouts, ...,
+    per-pair failure flags."""
+    return ctx.debug_buffer(9).view(torch.int32).numpy()
+
+
 def test_sgbm_bit_exact(oracle_mod, frames):
     from forest_slam_amd import _lib
     ctx = _lib.Context(960, 600, max_batch=2)
     L = np.stack([frames[0][0], frames[1][0]])
     R = np.stack([frames[0][1], frames[1][1]])
-    d = ctx.sgbm(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda())
-    torch.cuda.synchronize()
-    d = d.cpu().numpy()
-    for i in range(2):
-        want = oracle_mod.sgbm(L[i], R[i])
-        bad = np.argwhere(d[i] != want)
-        assert len(bad) == 0, f"pair {i}: {len(bad)} px differ, first {bad[:5]}"
+    for rep in range(2):  # a second call (lpath: the hand-off granules of the first carry an older tag)
+        d = ctx.sgbm(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda())
+        torch.cuda.synchronize()
+        d = d.cpu().numpy()
+        for i in range(2):
+            want = oracle_mod.sgbm(L[i], R[i])
+            bad = np.argwhere(d[i] != want)
+            assert len(bad) == 0, f"call {rep} pair {i}: {len(bad)} px differ, first {bad[:5]}"
+        ctl = sgbm_ctl(ctx)
+        assert ctl[2] == 0 and not ctl[4:6].any()  # no L-path hand-off timed out (lpath schedule)
 
 
 def test_sgbm_small_geometry(oracle_mod):
@@ -300,11 +309,14 @@ def sgbm_ref(oracle_mod, frames):
     return [oracle_mod.sgbm(L, R) for L, R in frames]
 
 
-@pytest.mark.parametrize("g,cb", [(4, 64), (4, 32), (8, 32), (8, 16)])
-def test_sgbm_variants_bit_exact(frames, sgbm_ref, monkeypatch, g, cb):
-    """Every SGBM launch variant (lanes per column and columns per block of the V pass) is
-    bit-identical to the oracle."""
+@pytest.mark.parametrize("mode,g,cb", [("classic", 4, 64), ("classic", 4, 32), ("classic", 8, 32), ("classic", 8, 16),
+                                       ("lpath", 8, 32)])
+def test_sgbm_variants_bit_exact(frames, sgbm_ref, monkeypatch, mode, g, cb):
+    """Every SGBM schedule and launch variant is bit-identical to the oracle: the default schedule
+    (one row pass running both sweeps) with each cost-pass shape (lanes per column, columns per
+    block), and the L path run inside the cost pass with its column-block hand-off (lpath)."""
     from forest_slam_amd import _lib
+    monkeypatch.setenv("FVO_SG_MODE", mode)
     monkeypatch.setenv("FVO_SG_G", str(g))
     monkeypatch.setenv("FVO_SG_CB", str(cb))
     ctx = _lib.Context(960, 600, max_batch=len(frames))
@@ -335,6 +347,7 @@ def test_sgbm_ragged_geometries_bit_exact(oracle_mod, W, H, nd):
         want = oracle_mod.sgbm(img, R, num_disp=nd)
         bad = np.argwhere(d[i].cpu().numpy() != want)
         assert len(bad) == 0, f"{W}x{H}/{nd} image {i}: {len(bad)} px differ, first {bad[:5]}"
+    assert sgbm_ctl(ctx)[2] == 0  # no L-path hand-off timed out
 
 
 def test_orb_rejects_edge_threshold_below_half_patch():
