@@ -118,12 +118,17 @@ __device__ __forceinline__ void load_run(const uint16_t* base, uint32_t* out) {
   }
 }
 
+template <int PQ>
+__device__ __forceinline__ uint32_t step16(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
+                                           uint32_t P2);
+
 // One step of a path over a lane's run with G lanes per column (G = 4: quad; G = 8: half
-// row, neighbours by DPP row shifts, minimum by two quad steps + row_half_mirror); returns
-// the group-wide minimum.
+// row, neighbours by DPP row shifts, minimum by two quad steps + row_half_mirror; G = 16: a
+// DPP row, step16); returns the group-wide minimum.
 template <int PQ, int G>
 __device__ __forceinline__ uint32_t hstepG(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
                                            uint32_t P2) {
+  if constexpr (G == 16) return step16<PQ>(st, c, q, P1, minPrev, P2);
   uint32_t prevLast, nextFirst;
   if (G == 4) {
     prevLast = qperm<kQPrev>(st[PQ - 1]);
@@ -410,24 +415,25 @@ __device__ __attribute__((noinline)) void sg_run_L(SgLink lk, lds_cu32* ring, in
 }
 
 template <int D, int CB, int G, bool LP>
-__global__ __launch_bounds__(G * CB, LP ? 4 : 1) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
+__global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
                                                     int64_t stride, int pitch, SgParams p, uint16_t* __restrict__ Vvol,
                                                     uint16_t* __restrict__ Mvol, SgLink lk) {
-  constexpr int DQ = D / G, PQ = DQ / 2, NV2 = DQ / 4;
+  constexpr int DQ = D / G, PQ = DQ / 2, NV2 = DQ / 4;  // NV2 = 0: a run of 6 (G = 16) moves as words
   constexpr int NT = G * CB;                // threads: G lanes per column
   constexpr int kCX = CB + 6;               // pixel-cost columns (7-wide box apron)
   constexpr int NRC = kCX + D - 1;          // right-image core pixels
   constexpr int NLI = kCX + 4, NRI = NRC + 4;  // staged pixels per image row (core + 2 each side)
-  constexpr int NIMG = 3 * (NLI + NRI);     // staged bytes per hsum row
+  constexpr int NIMG = NLI + NRI;           // staged bytes per image row
   constexpr int PER = (NIMG + NT - 1) / NT;  // staged bytes per thread
   constexpr int PQ16 = D / 32;              // L path: packed words per lane (16 lanes per row)
   constexpr int CKW = PQ16 + 1 <= 4 ? 4 : 8;
   // C ring of the L path: 4 rows x CB columns x D/2 words, the row stride = 16 mod 32 words so
   // the 4 rows' lanes (3 words apart within a row) hit disjoint banks
   constexpr int RW = LP ? CB * D / 2 + 16 : 1;
-  __shared__ uint8_t sImg[3][NLI + NRI];
+  __shared__ uint8_t sImg[4][NLI + NRI];                            // image rows (ring by row & 3), L then R
   __shared__ uint32_t sCh[kCX + 2 + NRC + 2];                       // (Sobel, intensity), L then R
-  __shared__ uint32_t sW[3][kCX + NRC];                            // u, BT min, BT max, L then R
+  __shared__ uint32_t sU[6][kCX];                                  // left BT words per channel (splat)
+  __shared__ uint32_t sV[6][NRC];                                  // right BT words per channel (pixel pairs)
   __shared__ __attribute__((aligned(16))) uint16_t sPC[kCX][D];    // pixel cost
   __shared__ uint32_t sRing[LP ? 4 : 1][RW];
   __shared__ int sUnit;
@@ -467,110 +473,171 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : 1) void k_sg_costvert(const uint8_
   const int ft = p.ftzero;
   auto clip = [ft](int v) { return min(max(v, -ft), ft) + ft; };
 
-  // image bytes of hsum row r (rows r-1, r, r+1, clamped): thread-private prefetch slots
+  // ---- image rows: a 4-slot LDS ring (slot = image row & 3) of the block's core columns (+2 each
+  // side) of both images; hsum row r reads rows r-1, r, r+1 (clamped), so each new hsum row stages
+  // one new image row, loaded one hsum row ahead into a register (one byte per thread)
+  const uint8_t* colsrc[PER];  // this thread's bytes of a staged row (clamped columns)
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int jb = min(tid + NT * k, NIMG - 1);
+    colsrc[k] = jb < NLI ? Lb + min(max(xl0 - 2 + jb, 0), W - 1) : Rb + min(max(xr0 - 2 + (jb - NLI), 0), W - 1);
+  }
   uint32_t pre[PER];
-  auto fetch = [&](int r) {
-    const int rows[3] = {r > 0 ? r - 1 : r, r, r < H - 1 ? r + 1 : r};
+  int pre_row = -1;  // image row held in `pre` (-1: none)
+  auto put_row = [&](int row) {
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int i = min(tid + NT * k, NIMG - 1);
-      const int rr = i / (NLI + NRI), j = i % (NLI + NRI);
-      const uint8_t* src = j < NLI ? Lb + min(max(xl0 - 2 + j, 0), W - 1) : Rb + min(max(xr0 - 2 + (j - NLI), 0), W - 1);
-      pre[k] = src[(int64_t)rows[rr] * pitch];
-    }
+    for (int k = 0; k < PER; ++k)
+      if (tid + NT * k < NIMG) sImg[row & 3][tid + NT * k] = (uint8_t)pre[k];
   };
-  // hsum row from the staged bytes -> acc (this lane's column and disparity run)
-  auto hs_row = [&](uint32_t* acc, int next) {
+  auto load_row = [&](int row) {
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int i = tid + NT * k;
-      if (i < NIMG) (&sImg[0][0])[i] = (uint8_t)pre[k];
+    for (int k = 0; k < PER; ++k) pre[k] = colsrc[k][(int64_t)row * pitch];
+  };
+  // ---- per-thread pixel-cost tasks (8 disparities of one column each), fixed for the block:
+  // left word index kl, right pair index of the first disparity pair, output offset
+  constexpr int NDB = D / 32;
+  constexpr int NSLOT = ((kCX + 7) / 8) * NDB * 32;
+  constexpr int NTASK = (NSLOT + NT - 1) / NT;
+  int tk_kl[NTASK], tk_jr[NTASK], tk_out[NTASK];
+#pragma unroll
+  for (int m = 0; m < NTASK; ++m) {
+    const int t = tid + NT * m;
+    const int g = t >> 5, w = t & 31;
+    const int i = (g / NDB) * 8 + (w >> 2), d0 = ((g % NDB) * 4 + (w & 3)) * 8;
+    const int x1c = min(max(c0 - 3 + i, 0), p.width1 - 1);
+    tk_kl[m] = x1c + p.minX1 - xl0;
+    tk_jr[m] = tk_kl[m] + (D - 1) - d0;  // right pixel of disparity d0 (pairs: d0 + 2j at tk_jr - 2j)
+    tk_out[m] = (t < NSLOT && i < kCX) ? i * D + d0 : -1;
+  }
+  // hsum row r from the ring -> acc (this lane's column and disparity run); `next` = the hsum
+  // row after it (-1: none), whose new image row is loaded here
+  auto hs_row = [&](uint32_t* acc, int r, int next) {
+    if (pre_row >= 0) put_row(pre_row);
+    pre_row = -1;
+    if (next >= 0 && next + 1 <= H - 1) {
+      load_row(next + 1);
+      pre_row = next + 1;
     }
-    if (next >= 0) fetch(next);
     __syncthreads();
     // channel words at core-1 .. core+1 of both images; borders (x < 1, x >= W-1) read ftzero
-    for (int j = tid; j < (nl + 2) + (nr + 2); j += NT) {
-      const bool left = j < nl + 2;
-      const int k = left ? j : j - (nl + 2);
-      const int x = (left ? xl0 : xr0) - 1 + k;
-      const uint8_t* r0 = &sImg[0][left ? 0 : NLI];
-      const uint8_t* r1 = &sImg[1][left ? 0 : NLI];
-      const uint8_t* r2 = &sImg[2][left ? 0 : NLI];
-      const int jj = k + 1;
-      uint32_t wv = (uint32_t)clip(0) * 0x10001u;
-      if (x >= 1 && x < W - 1) {
-        const int sb = (r1[jj + 1] - r1[jj - 1]) * 2 + r0[jj + 1] - r0[jj - 1] + r2[jj + 1] - r2[jj - 1];
-        wv = (uint32_t)clip(sb) | ((uint32_t)r1[jj] << 16);
+    {
+      const uint8_t* r0 = sImg[(r > 0 ? r - 1 : r) & 3];
+      const uint8_t* r1 = sImg[r & 3];
+      const uint8_t* r2 = sImg[(r < H - 1 ? r + 1 : r) & 3];
+      for (int j = tid; j < (nl + 2) + (nr + 2); j += NT) {
+        const bool left = j < nl + 2;
+        const int k = left ? j : j - (nl + 2);
+        const int x = (left ? xl0 : xr0) - 1 + k;
+        const int jj = k + 1 + (left ? 0 : NLI);
+        uint32_t wv = (uint32_t)clip(0) * 0x10001u;
+        if (x >= 1 && x < W - 1) {
+          const int sb = (r1[jj + 1] - r1[jj - 1]) * 2 + r0[jj + 1] - r0[jj - 1] + r2[jj + 1] - r2[jj - 1];
+          wv = (uint32_t)clip(sb) | ((uint32_t)r1[jj] << 16);
+        }
+        sCh[left ? k : (kCX + 2) + k] = wv;
       }
-      sCh[left ? k : (kCX + 2) + k] = wv;
     }
     __syncthreads();
-    // BT words: u, min(u, (u+ul)/2, (u+ur)/2), max(...); at x = 0 / W-1 the half is u itself
+    // BT words per channel c (lo half: x-Sobel, hi: intensity): value, min(u, (u+ul)/2, (u+ur)/2),
+    // max(...) (at x = 0 / W-1 the half is u itself).  Left pixels as splat words (both halves
+    // the pixel's), right pixels as pairs (pixel k, pixel k-1): a pixel-cost word then holds
+    // disparities (d, d+1) of one column, both from one packed operation
+    auto btw = [&](const uint32_t* ch, int k, int x, u16x2& u, u16x2& mn, u16x2& mx) {
+      u = as_v(ch[k + 1]);
+      u16x2 hl = (u + as_v(ch[k])) >> 1, hr = (u + as_v(ch[k + 2])) >> 1;
+      if (x == 0) hl = u;
+      if (x == W - 1) hr = u;
+      mn = vmin(vmin(hl, hr), u);
+      mx = __builtin_elementwise_max(__builtin_elementwise_max(hl, hr), u);
+    };
     for (int j = tid; j < nl + nr; j += NT) {
       const bool left = j < nl;
       const int k = left ? j : j - nl;
       const int x = left ? xl0 + k : xr0 + k;
       const uint32_t* ch = left ? sCh : sCh + (kCX + 2);
-      const u16x2 u = as_v(ch[k + 1]);
-      u16x2 hl = (u + as_v(ch[k])) >> 1, hr = (u + as_v(ch[k + 2])) >> 1;
-      if (x == 0) hl = u;
-      if (x == W - 1) hr = u;
-      const int o = left ? k : kCX + k;
-      sW[0][o] = as_u(u);
-      sW[1][o] = as_u(vmin(vmin(hl, hr), u));
-      sW[2][o] = as_u(__builtin_elementwise_max(__builtin_elementwise_max(hl, hr), u));
+      u16x2 u, mn, mx;
+      btw(ch, k, x, u, mn, mx);
+      if (left) {
+        const u16x2 w3[3] = {u, mn, mx};
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int e = 0; e < 3; ++e) sU[3 * c + e][k] = as_u(splat(c ? as_u(w3[e]) >> 16 : as_u(w3[e])));
+      } else if (k > 0) {
+        u16x2 up, mnp, mxp;  // the right pixel k - 1
+        btw(ch, k - 1, x - 1, up, mnp, mxp);
+        const uint32_t a3[3] = {as_u(u), as_u(mn), as_u(mx)}, b3[3] = {as_u(up), as_u(mnp), as_u(mxp)};
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+          sV[e][k] = (a3[e] & 0xFFFFu) | (b3[e] << 16);             // x-Sobel (k, k-1)
+          sV[3 + e][k] = (a3[e] >> 16) | (b3[e] & 0xFFFF0000u);     // intensity (k, k-1)
+        }
+      }
     }
     __syncthreads();
-    // pixel costs of the kCX (clamped) columns x D disparities, 8 disparities per task
-    constexpr int NDB = D / 32;
-    constexpr int NSLOT = ((kCX + 7) / 8) * NDB * 32;
-    for (int t = tid; t < NSLOT; t += NT) {
-      const int g = t >> 5, w = t & 31;
-      const int i = (g / NDB) * 8 + (w >> 2), d0 = ((g % NDB) * 4 + (w & 3)) * 8;
-      if (i >= kCX) continue;
-      const int x1c = min(max(c0 - 3 + i, 0), p.width1 - 1);
-      const int kl = x1c + p.minX1 - xl0;
-      const u16x2 u = as_v(sW[0][kl]), u0 = as_v(sW[1][kl]), u1 = as_v(sW[2][kl]);
+    // pixel costs of the kCX (clamped) columns x D disparities, 8 disparities per task, two per
+    // packed operation: cost = BT(x-Sobel) + (BT(intensity) >> 2)
+#pragma unroll
+    for (int m = 0; m < NTASK; ++m) {
+      if (tk_out[m] < 0) continue;
+      const int kl = tk_kl[m];
+      u16x2 uu[6];
+#pragma unroll
+      for (int e = 0; e < 6; ++e) uu[e] = as_v(sU[e][kl]);
       uint32_t out[4];
 #pragma unroll
-      for (int h = 0; h < 8; ++h) {
-        const int kr = kCX + kl + (D - 1) - (d0 + h);
-        const u16x2 v = as_v(sW[0][kr]), v0 = as_v(sW[1][kr]), v1 = as_v(sW[2][kr]);
-        const u16x2 cA = __builtin_elementwise_max(__builtin_elementwise_sub_sat(u, v1), __builtin_elementwise_sub_sat(v0, u));
-        const u16x2 cB = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, u1), __builtin_elementwise_sub_sat(u0, v));
-        const uint32_t m = as_u(vmin(cA, cB));
-        const uint32_t cst = (m & 0xFFFFu) + (m >> 18);
-        if (h & 1) out[h >> 1] |= cst << 16; else out[h >> 1] = cst;
+      for (int h = 0; h < 4; ++h) {
+        const int jr = tk_jr[m] - 2 * h;
+        u16x2 mc[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const u16x2 v = as_v(sV[3 * c][jr]), v0 = as_v(sV[3 * c + 1][jr]), v1 = as_v(sV[3 * c + 2][jr]);
+          const u16x2 u = uu[3 * c], u0 = uu[3 * c + 1], u1 = uu[3 * c + 2];
+          const u16x2 cA = __builtin_elementwise_max(__builtin_elementwise_sub_sat(u, v1), __builtin_elementwise_sub_sat(v0, u));
+          const u16x2 cB = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, u1), __builtin_elementwise_sub_sat(u0, v));
+          mc[c] = vmin(cA, cB);
+        }
+        out[h] = as_u(mc[0] + (mc[1] >> 2));
       }
-      *reinterpret_cast<uint4*>(&sPC[i][d0]) = make_uint4(out[0], out[1], out[2], out[3]);
+      *reinterpret_cast<uint4*>(&sPC[0][0] + tk_out[m]) = make_uint4(out[0], out[1], out[2], out[3]);
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PQ; ++k) acc[k] = 0;
 #pragma unroll
     for (int t = 0; t < 7; ++t) {
-      const uint2* src = reinterpret_cast<const uint2*>(&sPC[col + t][q * DQ]);
+      if constexpr (DQ % 4 == 0) {
+        const uint2* src = reinterpret_cast<const uint2*>(&sPC[col + t][q * DQ]);
 #pragma unroll
-      for (int k = 0; k < NV2; ++k) {
-        const uint2 w2 = src[k];
-        acc[2 * k] = as_u(as_v(acc[2 * k]) + as_v(w2.x));
-        acc[2 * k + 1] = as_u(as_v(acc[2 * k + 1]) + as_v(w2.y));
+        for (int k = 0; k < NV2; ++k) {
+          const uint2 w2 = src[k];
+          acc[2 * k] = as_u(as_v(acc[2 * k]) + as_v(w2.x));
+          acc[2 * k + 1] = as_u(as_v(acc[2 * k + 1]) + as_v(w2.y));
+        }
+      } else {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&sPC[col + t][q * DQ]);
+#pragma unroll
+        for (int k = 0; k < PQ; ++k) acc[k] = as_u(as_v(acc[k]) + as_v(src[k]));
       }
     }
-    // no trailing barrier: the next row's first LDS write (sImg) comes after every thread
-    // has passed this row's later barriers, i.e. finished reading sImg / sCh / sW / sPC
+    // no trailing barrier: the next row's first LDS write (its image row, in a ring slot no
+    // phase of this row reads) comes before its first barrier, and every later write after it
   };
 
   // window: win[k] = hsum(clamp(start - 3 + k)), k = 0..6, for the output row start
   uint32_t win[7][PQ], crun[PQ], st[PQ];
-  fetch(start);
-  hs_row(win[6], start + 1 <= H - 1 ? start + 1 : -1);
+  // the first hsum row's image rows (start - 1, start, start + 1, clamped) straight into the ring
+  for (int row = max(start - 1, 0); row <= min(start + 1, H - 1); ++row) {
+    load_row(row);
+    put_row(row);
+  }
+  hs_row(win[6], start, start + 1 <= H - 1 ? start + 1 : -1);
   for (int r = start + 1; r <= start + 3; ++r) {
 #pragma unroll
     for (int k = 0; k < 6; ++k)
 #pragma unroll
       for (int j = 0; j < PQ; ++j) win[k][j] = win[k + 1][j];
-    if (r <= H - 1) hs_row(win[6], r + 1 <= H - 1 ? r + 1 : -1);
+    if (r <= H - 1) hs_row(win[6], r, r + 1 <= H - 1 ? r + 1 : -1);
   }
   // win[3..6] = hs(start..start+3 clamped); rows above start clamp to start
 #pragma unroll
@@ -601,11 +668,17 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : 1) void k_sg_costvert(const uint8_
     const bool out_row = y >= first_out, top_row = s > 0 && y == first_out - 1;
     if ((out_row || top_row) && x1 < p.width1) {
       const int64_t yo = out_row ? (int64_t)(y >> 2) * 4 * plane + (y & 3) * D : (int64_t)(p.HG4 + s) * 4 * plane;
-      uint2* vp = reinterpret_cast<uint2*>(Vvol + colofs + yo);
+      if constexpr (DQ % 4 == 0) {
+        uint2* vp = reinterpret_cast<uint2*>(Vvol + colofs + yo);
 #pragma unroll
-      for (int i = 0; i < NV2; ++i) {
-        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        __builtin_nontemporal_store(u32x2{st[2 * i], st[2 * i + 1]}, reinterpret_cast<u32x2*>(vp + i));
+        for (int i = 0; i < NV2; ++i) {
+          typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+          __builtin_nontemporal_store(u32x2{st[2 * i], st[2 * i + 1]}, reinterpret_cast<u32x2*>(vp + i));
+        }
+      } else {
+        uint32_t* vp = reinterpret_cast<uint32_t*>(Vvol + colofs + yo);
+#pragma unroll
+        for (int i = 0; i < PQ; ++i) __builtin_nontemporal_store(st[i], vp + i);
       }
       // min over d of this V row (the next row's minPrev): the row pass's inversion needs it
       if (q == 0) Mvol[(colofs - q * DQ + yo) / D] = (uint16_t)minPrev;
@@ -642,7 +715,7 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : 1) void k_sg_costvert(const uint8_
       if (y >= end) break;
       uint32_t nw[PQ];
       if (y + 3 <= H - 1) {
-        hs_row(nw, y + 4 <= H - 1 ? y + 4 : -1);
+        hs_row(nw, y + 3, y + 4 <= H - 1 ? y + 4 : -1);
       } else {
 #pragma unroll
         for (int j = 0; j < PQ; ++j) nw[j] = win[(ph + 6) % 7][j];
@@ -1052,7 +1125,7 @@ __global__ void k_sg_prep(uint32_t* ctl, int nb) {
 // Schedules and launch shapes (read per launch; every variant is bit-identical and
 // parity-tested), FVO_SG_MODE:
 //   (default)  one cost pass, one row pass running both sweeps, with FVO_SG_G lanes per column
-//              (4 or 8) and FVO_SG_CB columns per block (G=4: 32/64; G=8: 16/32)
+//              (4, 8 or 16) and FVO_SG_CB columns per block (G=4: 32/64; G=8: 16/32; G=16: 32)
 //   lpath      the L path in the cost pass, handed from column block to column block: one V read
 //              per pair fewer (<= 300 MB/pair) but slower -- DESIGN.md §4.2 r5
 int env_int(const char* name, int def) {
@@ -1103,15 +1176,20 @@ void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_
   const int16_t invalid = (int16_t)((p.minD - 1) * 16);
   const SgMode mode = sg_mode();
   if (mode == kSgClassic) {
-    const int g = env_int("FVO_SG_G", 8), cb = env_int("FVO_SG_CB", g == 8 ? 32 : 64);
+    // (G, CB) of the cost pass: the grid follows the kernel actually launched, so an unsupported
+    // FVO_SG_CB falls back to that G's default shape instead of leaving columns uncomputed
+    const int g = env_int("FVO_SG_G", 8), cbr = env_int("FVO_SG_CB", g == 4 ? 64 : 32);
+    typedef void (*CostKernel)(const uint8_t*, const uint8_t*, int64_t, int, SgParams, uint16_t*, uint16_t*, SgLink);
+    CostKernel kern;
+    int gg, cb;
+    if (g == 16) kern = k_sg_costvert<D, 32, 16, false>, gg = 16, cb = 32;
+    else if (g == 4 && cbr == 32) kern = k_sg_costvert<D, 32, 4, false>, gg = 4, cb = 32;
+    else if (g == 4) kern = k_sg_costvert<D, 64, 4, false>, gg = 4, cb = 64;
+    else if (cbr == 16) kern = k_sg_costvert<D, 16, 8, false>, gg = 8, cb = 16;
+    else kern = k_sg_costvert<D, 32, 8, false>, gg = 8, cb = 32;
     const dim3 gcv((p.width1 + cb - 1) / cb, p.nstripes, nb);
     const SgLink lk{};
-    FVO_TIMED(ctx, KN_SG_VERT, s, {
-      if (g == 8 && cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 8, false>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, V, M, lk);
-      else if (g == 8) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 16, 8, false>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, V, M, lk);
-      else if (cb == 32) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 32, 4, false>), gcv, dim3(128), 0, s, L, R, stride, pitch, p, V, M, lk);
-      else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, 64, 4, false>), gcv, dim3(256), 0, s, L, R, stride, pitch, p, V, M, lk);
-    });
+    FVO_TIMED(ctx, KN_SG_VERT, s, hipLaunchKernelGGL(kern, gcv, dim3(gg * cb), 0, s, L, R, stride, pitch, p, V, M, lk));
     FVO_TIMED(ctx, KN_SG_ROWS, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_rows<D, kSwBoth>), dim3(sg_nblk(p), nb), dim3(64), 0, s,
                                                      V, M, p, ctx->sg_ckpt, nck, ctx->sg_raw));
     FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.W + 255) / 256, p.H, nb), dim3(256), 0, s,

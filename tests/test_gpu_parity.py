@@ -310,7 +310,7 @@ def sgbm_ref(oracle_mod, frames):
 
 
 @pytest.mark.parametrize("mode,g,cb", [("classic", 4, 64), ("classic", 4, 32), ("classic", 8, 32), ("classic", 8, 16),
-                                       ("lpath", 8, 32)])
+                                       ("classic", 16, 32), ("lpath", 8, 32)])
 def test_sgbm_variants_bit_exact(frames, sgbm_ref, monkeypatch, mode, g, cb):
     """Every SGBM schedule and launch variant is bit-identical to the oracle: the default schedule
     (one row pass running both sweeps) with each cost-pass shape (lanes per column, columns per
