@@ -260,6 +260,23 @@ def pmc_valu(shape: str):
                         for r in rows if r["kernel"].startswith(hot)}}
 
 
+def exchange_fields(world: int, rank0_only: bool, send_bytes: int, stream_ms, collective_ms, host_ms, steps) -> dict:
+    """The JSON line's multi-rank exchange record: what each rank sends and
+    receives per step and how long the side stream spends on it (send copies + collectives +
+    map placement, HIP events on SequenceRank.stream; `collective_ms` the collectives' share) and
+    the host time of the exchange call, rank 0's means over the timed steps."""
+    if world == 1:
+        return {"mode": "off (one rank: no exchange)", "send_bytes_per_rank_per_step": 0,
+                "recv_bytes_per_rank_per_step": 0, "stream_ms_per_step": None, "collective_ms_per_step": None,
+                "host_ms_per_step": None, "steps_timed": 0}
+    return {"mode": ("gather to rank 0, map on rank 0 only" if rank0_only
+                     else "all-gather, every rank places the whole map"),
+            "send_bytes_per_rank_per_step": send_bytes, "recv_bytes_per_rank_per_step": send_bytes * world,
+            "stream_ms_per_step": None if stream_ms is None else round(stream_ms, 4),
+            "collective_ms_per_step": None if collective_ms is None else round(collective_ms, 4),
+            "host_ms_per_step": None if host_ms is None else round(host_ms, 4), "steps_timed": steps}
+
+
 def _free_port() -> int:
     import socket
     with socket.socket() as sk:
@@ -343,13 +360,19 @@ def main_dry_run(args):
     gloo ranks on the CPU, a 1 ms host "step" + one all-reduce per step, the same barrier /
     max-over-ranks timing and the same rank / world fields in the JSON line; value is null."""
     rk = Ranks(args, cpu=True)
+    from forest_slam_amd import dist as fdist
+    B, cap = args.batch, 2 * args.nfeatures + 64  # fvo_kp_capacity's default for nfeatures
+    send = [torch.zeros((B, 4, 4), dtype=torch.float64), torch.zeros((B,), dtype=torch.int32),
+            torch.zeros((B, cap, 3), dtype=torch.float32), torch.zeros((B,), dtype=torch.int32)]
+    host_s = []
     rk.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         time.sleep(0.001)
         if rk.dist:
-            x = torch.ones(1)
-            rk.dist.all_reduce(x)
+            t1 = time.perf_counter()
+            fdist.exchange_frame_map(*send, dst=0 if args.map_rank0 else None)  # the bench's exchange, host tensors
+            host_s.append(time.perf_counter() - t1)
     rk.barrier()
     elapsed = rk.max_elapsed(time.perf_counter() - t0)
     if rk.rank == 0:
@@ -358,6 +381,9 @@ def main_dry_run(args):
                "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 3), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": None, "data": "dry run: no GPU, no VO work",
                "config": {"workload": "dry run (launcher / process-group check)", "parallelism": f"x{rk.world}"}}
+        eb = fdist.exchange_bytes(B, cap)
+        out["exchange"] = exchange_fields(rk.world, args.map_rank0, eb, None, None,
+                                          sum(host_s) / len(host_s) * 1e3 if host_s else None, len(host_s))
         out.update(rk.fields())
         print(json.dumps(out), flush=True)
     rk.close()
@@ -452,6 +478,8 @@ def main():
     ap.add_argument("--shard", choices=("sequences", "frames"), default="sequences",
                     help="sequences: one sequence per GPU, B frames per GPU per step (weak scaling, the default); "
                          "frames: ONE sequence of steps x B frames split by frame pairs over the GPUs (strong scaling)")
+    ap.add_argument("--map-rank0", type=int, default=0,
+                    help="multi-rank map on rank 0 only (gather) instead of on every rank (all-gather, the default)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group check without a GPU (gloo ranks on the CPU, no VO work)")
     args = ap.parse_args()
@@ -492,7 +520,7 @@ def main():
     # points3D and the multi-sequence map built from it on the device (dist.GlobalMap), on a
     # side stream behind the step
     steps_total = max(args.warmup, 1) + 2 + args.steps
-    rank_step = fdist.SequenceRank(fe, map_capacity=steps_total * world * B * fe.cap)
+    rank_step = fdist.SequenceRank(fe, map_capacity=steps_total * world * B * fe.cap, map_rank0_only=bool(args.map_rank0))
     nstep = [0]
 
     def eager_step():
@@ -525,6 +553,7 @@ def main():
     # stream overlapped its launches share the GPU with the main stream's kernels, so the
     # in-order launch time of the breakdown pass is reported beside it
     fe.ctx.timing_enable([dom])
+    rank_step.timing(True)
     rk.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -536,13 +565,18 @@ def main():
     dom_t = fe.ctx.timing_read()
     fe.ctx.timing_enable([])
     elapsed = rk.max_elapsed(elapsed)
+    xs = rank_step.exchange_stats()
+    rank_step.timing(False)
+    exchange = exchange_fields(world, bool(args.map_rank0), xs["send_bytes_per_rank_per_step"] if xs else 0,
+                               xs.get("stream_ms_per_step") if xs else None, xs.get("collective_ms_per_step") if xs else None,
+                               xs.get("host_ms_per_step") if xs else None, xs["steps_timed"] if xs else 0)
 
     global_map = None
     if rank_step.gmap is not None:
         gm = rank_step.gmap.flush()
         torch.cuda.synchronize()
         global_map = {"points": len(gm), "sequences": world, "steps_placed": rank_step.gmap.steps,
-                      "what": f"every posed frame's points3D of every rank, all-gathered over {rk.backend} each "
+                      "what": f"every posed frame's points3D of every rank, {exchange['mode']} over {rk.backend} each "
                               "step and placed on the device with each sequence's chained poses (dist.GlobalMap: "
                               "fvo_chain_poses + fvo_map_transform)"}
     frames = world * B * args.steps
@@ -639,6 +673,7 @@ def main():
             "pmc_shape": shape,
             "ate": ate,
             "global_map": global_map,
+            "exchange": exchange,
             "stages_ms_per_step": stage_ms,
             "workspace_gb": round(fe.ctx.workspace_bytes / 1e9, 2),
         }

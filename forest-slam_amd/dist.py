@@ -133,25 +133,39 @@ def run_sequence_sharded(make_frontend, L_all: torch.Tensor, R_all: torch.Tensor
 
 
 def exchange_frame_map(T_step: torch.Tensor, st_step: torch.Tensor, P3: torch.Tensor, n_points: torch.Tensor,
-                       group=None):
+                       group=None, dst: int | None = None):
     """The per-step map exchange of the multi-sequence run: every rank's
     relative poses of the step (f64 [B,4,4], BA-refined with local BA), their statuses (i32 [B])
     and every frame's points3D (the back-projected, depth-filtered points PnP consumed: f32
-    [B,cap,3] + i32 [B] counts, stereo_slam.py:274-289) are all-gathered (RCCL over xGMI).
-    Fixed shapes and device-side counts: no host synchronisation, the collectives queue on the
-    current stream.  Returns (T [world,B,4,4], st [world,B], P3 [world,B,cap,3], n [world,B])
-    on the inputs' device.  Under the gloo backend (CPU tests, or GPU ranks sharing one card)
-    the tensors go through host copies."""
+    [B,cap,3] + i32 [B] counts, stereo_slam.py:274-289) are all-gathered (RCCL over xGMI), or,
+    with ``dst`` set, gathered to that rank only (the map placed on one rank: the others send and
+    receive nothing back; they get None).  Fixed shapes and device-side counts: no host
+    synchronisation, the collectives queue on the current stream.  Returns (T [world,B,4,4],
+    st [world,B], P3 [world,B,cap,3], n [world,B]) on the inputs' device.  Under the gloo
+    backend (CPU tests, or GPU ranks sharing one card) the tensors go through host copies."""
     world = dist.get_world_size(group)
     host = dist.get_backend(group) == "gloo" and T_step.is_cuda
     dev = T_step.device
     ins = [t.contiguous().cpu() if host else t.contiguous() for t in (T_step, st_step, P3, n_points)]
+    me = dist.get_rank(group)
     outs = []
     for t in ins:
-        o = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather(list(o.unbind(0)), t, group=group)
-        outs.append(o.to(dev) if host else o)
-    return tuple(outs)
+        if dst is None or me == dst:
+            o = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+            if dst is None:
+                dist.all_gather(list(o.unbind(0)), t, group=group)
+            else:
+                dist.gather(t, list(o.unbind(0)), dst=dst, group=group)
+            outs.append(o.to(dev) if host else o)
+        else:
+            dist.gather(t, None, dst=dst, group=group)
+    return tuple(outs) if outs else None
+
+
+def exchange_bytes(B: int, cap: int) -> int:
+    """Bytes one rank contributes to a step's map exchange: T f64 [B,4,4] + status i32 [B] +
+    points3D f32 [B,cap,3] + counts i32 [B]."""
+    return B * (16 * 8 + 4 + cap * 3 * 4 + 4)
 
 
 class GlobalMap:
@@ -188,17 +202,24 @@ class GlobalMap:
 class SequenceRank:
     """One rank of the sequence-per-GPU run: ``step`` = the front end's step over the rank's
     next frames, then, when the exchange is on (a process group of more than one rank, or
-    ``exchange=True``), the exchange of the step's relative poses, statuses and points3D with
-    every rank (``exchange_frame_map``) and, with ``map_capacity`` > 0, their placement in the
-    multi-sequence map (``GlobalMap``; ``self.gmap``).
+    ``exchange=True``), the exchange of the step's relative poses, statuses and points3D
+    (``exchange_frame_map``) and, with ``map_capacity`` > 0, their placement in the
+    multi-sequence map (``GlobalMap``; ``self.gmap``).  ``map_rank0_only``: the map lives on rank
+    0 only -- the step data are gathered there instead of all-gathered (the other ranks send
+    their 12 MB per step and receive nothing), and only rank 0 places them.
 
     The exchange and the map run on their own stream behind the step's kernels: the host does
     not wait for them (nor for the step), and the next step's back stage only waits for the
     copy of this step's poses and points into the send buffers.  Returns (T, status, gathered)
-    with gathered = None or the (T, st, P3, n) all-gather result, valid on ``self.stream``
-    (synchronise it, or the device, before reading it on the host)."""
+    with gathered = None or the (T, st, P3, n) result, valid on ``self.stream`` (synchronise
+    it, or the device, before reading it on the host).
 
-    def __init__(self, frontend, group=None, map_capacity: int = 0, exchange: bool | None = None):
+    ``timing(True)`` brackets each step's side-stream work with HIP events (send-buffer copies,
+    collectives, placement; ``exchange_stats`` reads them) and times the host call of the
+    exchange (the gloo path copies through the host and blocks there)."""
+
+    def __init__(self, frontend, group=None, map_capacity: int = 0, exchange: bool | None = None,
+                 map_rank0_only: bool = False):
         self.fe = frontend
         self.group = group
         if exchange is None:
@@ -206,17 +227,49 @@ class SequenceRank:
         self.exchange = bool(exchange)
         self.gmap = None
         self.copied = None
+        self.rank0_only = bool(map_rank0_only)
+        self.timed = False
+        self._ev, self._host_s = [], []
         if self.exchange:
             dev, B, cap = frontend.dev, frontend.B, frontend.cap
             self.world = dist.get_world_size(group)
+            self.rank = dist.get_rank(group)
             self.stream = torch.cuda.Stream(dev)
             e = lambda shape, dt: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
             self.sT, self.sS = e((B, 4, 4), torch.float64), e((B,), torch.int32)
             self.sP, self.sN = e((B, cap, 3), torch.float32), e((B,), torch.int32)
-            if map_capacity > 0:
+            self.send_bytes = exchange_bytes(B, cap)
+            if map_capacity > 0 and (self.rank == 0 or not self.rank0_only):
                 self.gmap = GlobalMap(self.world, map_capacity, dev, ctx=frontend.ctx)
 
+    def timing(self, on: bool):
+        """Start (on) or stop recording the per-step exchange timing; starting clears it."""
+        self.timed = bool(on)
+        if on:
+            self._ev, self._host_s = [], []
+
+    def exchange_stats(self) -> dict | None:
+        """Per-step means over the timed steps (synchronises the exchange stream): bytes this
+        rank sends and receives, the side stream's time from the send copies to the end of the
+        placement, the collectives' share of it, and the host time of the exchange call."""
+        if not self.exchange:
+            return None
+        recv = self.send_bytes * self.world if (not self.rank0_only or self.rank == 0) else 0
+        out = {"mode": ("gather to rank 0, map on rank 0 only" if self.rank0_only
+                        else "all-gather, every rank places the whole map"),
+               "send_bytes_per_rank_per_step": self.send_bytes, "recv_bytes_per_rank_per_step": recv,
+               "steps_timed": len(self._ev)}
+        if self._ev:
+            self.stream.synchronize()
+            tot = [a.elapsed_time(d) for a, b, c, d in self._ev]
+            col = [b.elapsed_time(c) for a, b, c, d in self._ev]
+            out.update({"stream_ms_per_step": round(sum(tot) / len(tot), 4),
+                        "collective_ms_per_step": round(sum(col) / len(col), 4),
+                        "host_ms_per_step": round(sum(self._host_s) / len(self._host_s) * 1e3, 4)})
+        return out
+
     def step(self, L: torch.Tensor, R: torch.Tensor):
+        import time
         fe = self.fe
         dev = fe.dev
         main = torch.cuda.current_stream(dev)
@@ -228,6 +281,9 @@ class SequenceRank:
         n = L.shape[0]
         self.stream.wait_stream(main)
         with torch.cuda.stream(self.stream):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if self.timed else None
+            if ev:
+                ev[0].record()
             # fixed-size send buffers: frames past n are padding (status -2: not posed, 0 points)
             self.sT[:n].copy_(T)
             self.sS[:n].copy_(st)
@@ -237,9 +293,20 @@ class SequenceRank:
                 self.sS[n:].fill_(-2)
                 self.sN[n:].zero_()
             self.copied = self.stream.record_event()
-            gathered = exchange_frame_map(self.sT, self.sS, self.sP, self.sN, self.group)
-            if self.gmap is not None:
+            if ev:
+                ev[1].record()
+            t0 = time.perf_counter()
+            gathered = exchange_frame_map(self.sT, self.sS, self.sP, self.sN, self.group,
+                                          dst=0 if self.rank0_only else None)
+            host_s = time.perf_counter() - t0
+            if ev:
+                ev[2].record()
+            if self.gmap is not None and gathered is not None:
                 self.gmap.place(gathered)
+            if ev:
+                ev[3].record()
+                self._ev.append(tuple(ev))
+                self._host_s.append(host_s)
         return T, st, gathered
 
 

@@ -29,6 +29,21 @@ def test_gpus_2_starts_two_ranks():
     assert r.returncode == 0, r.stderr[-2000:]
     j = _line(r)
     assert j["n_gpus"] == 2 and j["world_size_seen"] == 2 and j["backend"] == "gloo" and j["steps"] == 3
+    # the exchange record (the bench's per-step map exchange, run here on host
+    # tensors of the bench shapes: B = 64 frames, cap = 2 * 1000 + 64 keypoints)
+    x = j["exchange"]
+    send = 64 * (16 * 8 + 4 + (2 * 1000 + 64) * 3 * 4 + 4)
+    assert x["mode"].startswith("all-gather") and x["send_bytes_per_rank_per_step"] == send
+    assert x["recv_bytes_per_rank_per_step"] == 2 * send and x["steps_timed"] == 3 and x["host_ms_per_step"] > 0
+    assert "stream_ms_per_step" in x and "collective_ms_per_step" in x
+
+
+def test_gpus_2_map_on_rank0_gathers():
+    r = _run(["--gpus", "2", "--steps", "2", "--warmup", "0", "--dry-run", "--map-rank0", "1"],
+             {"FVO_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    x = _line(r)["exchange"]
+    assert x["mode"].startswith("gather to rank 0") and x["steps_timed"] == 2
 
 
 def test_gpus_1_is_one_process():
@@ -36,6 +51,7 @@ def test_gpus_1_is_one_process():
     assert r.returncode == 0, r.stderr[-2000:]
     j = _line(r)
     assert j["n_gpus"] == 1 and j["world_size_seen"] == 1
+    assert j["exchange"]["mode"].startswith("off") and j["exchange"]["send_bytes_per_rank_per_step"] == 0
 
 
 def test_rank_count_other_than_gpus_is_refused():

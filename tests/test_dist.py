@@ -35,8 +35,13 @@ def _worker(rank, world, port, n_pairs, out):
                                            torch.full((4,), rank - 1, dtype=torch.int32),
                                            torch.full((4, 16, 3), 10.0 + rank, dtype=torch.float32),
                                            torch.tensor([rank + 5, 1, 2, 3], dtype=torch.int32))
+    g0 = fd.exchange_frame_map(torch.full((4, 4, 4), float(rank), dtype=torch.float64),
+                               torch.full((4,), rank - 1, dtype=torch.int32),
+                               torch.full((4, 16, 3), 10.0 + rank, dtype=torch.float32),
+                               torch.tensor([rank + 5, 1, 2, 3], dtype=torch.int32), dst=0)  # map on rank 0 only
+    g0 = None if g0 is None else (g0[0][:, 0, 0, 0].tolist(), g0[2][:, 0, 0, 0].tolist(), g0[3][:, 0].tolist())
     out[rank] = (T, S, [p[0, 0].item() for p in poses], [l.shape[0] for l in lms],
-                 (Tw[:, 0, 0, 0].tolist(), Pw[:, 0, 0, 0].tolist(), Nw[:, 0].tolist(), Sw[:, 3].tolist()))
+                 (Tw[:, 0, 0, 0].tolist(), Pw[:, 0, 0, 0].tolist(), Nw[:, 0].tolist(), Sw[:, 3].tolist()), g0)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -62,8 +67,9 @@ def test_gather_poses_two_ranks_gloo():
     allT = np.tile(np.eye(4), (n_pairs, 1, 1))
     allT[:, :3, 3] = rng.normal(0, 0.1, (n_pairs, 3))
     for r in range(2):
-        T, S, kf, nl, wm = out[r]
+        T, S, kf, nl, wm, g0 = out[r]
         assert wm == ([0.0, 1.0], [10.0, 11.0], [5, 6], [-1, 0])
+        assert g0 == (([0.0, 1.0], [10.0, 11.0], [5, 6]) if r == 0 else None)  # gathered to rank 0 only
         assert np.array_equal(T, allT)
         assert S[3] == -1 and (S[np.arange(n_pairs) != 3] == 1).all()
         assert kf == [0.0, 1.0] and nl == [2, 3]

@@ -83,7 +83,7 @@ def _free_port():
     return p
 
 
-def _rank_worker(rank, world, port, out):
+def _rank_worker(rank, world, port, out, rank0_only=False):
     import sys
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
@@ -94,23 +94,33 @@ def _rank_worker(rank, world, port, out):
     torch.cuda.set_device(0)  # both ranks share the one card of the box
     seq, L, R = _frames(40 + rank, 7, start=60 * rank)
     fe = _fe(seq, 3, ba_window=3)
-    sr = fd.SequenceRank(fe, map_capacity=40000)
-    assert sr.exchange and sr.gmap is not None
+    sr = fd.SequenceRank(fe, map_capacity=40000, map_rank0_only=rank0_only)
+    assert sr.exchange and (sr.gmap is not None) == (rank == 0 or not rank0_only)
+    sr.timing(True)
     local = fd.GlobalMap(1, 40000, "cuda:0", ctx=fe.ctx)  # this rank's own map, built without the exchange
     fe.prime(L[0], R[0])
     res = []
     for s in (1, 4):
-        T, st, (Tg, Sg, Pg, Ng) = sr.step(L[s:s + 3], R[s:s + 3])
+        T, st, gathered = sr.step(L[s:s + 3], R[s:s + 3])
         torch.cuda.synchronize()
+        if gathered is None:  # map on rank 0 only: the other ranks send and get nothing back
+            assert rank0_only and rank != 0
+            gathered = tuple(torch.zeros(1) for _ in range(4))
+        Tg, Sg, Pg, Ng = gathered
         mine = (T.clone()[None], st.clone()[None], fe.P3[:3].clone()[None], fe.npts[:3].clone()[None])
         local.place(mine)
         torch.cuda.synchronize()
         res.append(dict(T=mine[0][0].cpu().numpy(), st=mine[1][0].cpu().numpy(), P=mine[2][0].cpu().numpy(),
                         N=mine[3][0].cpu().numpy(), Tg=Tg.cpu().numpy(), Sg=Sg.cpu().numpy(), Pg=Pg.cpu().numpy(),
                         Ng=Ng.cpu().numpy()))
-    g, lo = sr.gmap.flush(), local.flush()
+    xs = sr.exchange_stats()
+    assert xs["steps_timed"] == 2 and xs["stream_ms_per_step"] > 0 and xs["host_ms_per_step"] > 0
+    assert xs["recv_bytes_per_rank_per_step"] == (0 if rank0_only and rank else 2 * xs["send_bytes_per_rank_per_step"])
+    lo = local.flush()
+    g = sr.gmap.flush() if sr.gmap is not None else None
     torch.cuda.synchronize()
-    out[rank] = dict(steps=res, gmap=g.cloud64(), gmap32=g.cloud32(), local=lo.cloud64(), local32=lo.cloud32())
+    out[rank] = dict(steps=res, gmap=g.cloud64() if g else None, gmap32=g.cloud32() if g else None,
+                     local=lo.cloud64(), local32=lo.cloud32())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -172,6 +182,25 @@ def test_two_ranks_exchange_frame_maps():
     for r in range(2):
         ref = np.concatenate(_map_ref(out[r]["steps"]))
         assert np.array_equal(out[r]["local"], ref)
+
+
+def test_two_ranks_map_on_rank0_only():
+    """SequenceRank(map_rank0_only=True) gathers the step data to rank 0 only
+    (the other rank gets nothing back and keeps no map); rank 0's map equals the union of both
+    ranks' own maps, as in the all-gather mode."""
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rank_worker, args=(2, _free_port(), out, True), nprocs=2, join=True)
+    assert out[1]["gmap"] is None
+    segs, pos = [], [0, 0]
+    for step in range(2):
+        for r in range(2):
+            st = out[r]["steps"][step]
+            c = int(st["N"][st["st"] >= 0].sum())
+            segs.append(out[r]["local"][pos[r]:pos[r] + c])
+            pos[r] += c
+    assert np.array_equal(out[0]["gmap"], np.concatenate(segs))
 
 
 def test_sequence_rank_step_does_not_wait_for_the_gpu():
