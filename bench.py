@@ -94,18 +94,32 @@ def host_cpus() -> dict:
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
+def _ba_window_job(args):
+    """One local-BA window of the CPU baseline (process-pool worker: oracle/ba_ref.py holds the
+    GIL, so the windows run in separate processes)."""
+    root, kps, matches, stereo, rel, K, baseline = args
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import ba_ref  # test/baseline infrastructure only
+    t0 = time.perf_counter()
+    ba_ref.ba_window(kps, matches, stereo, rel, K, baseline, iters=10)
+    return time.perf_counter() - t0
+
+
 def cpu_baseline(n_frames: int, nfeatures: int, W: int, H: int, ba_window: int) -> dict:
     """Scalar C++ restatement of the reference CPU path (oracle/) timed on a bounded sample:
     per frame the reference's full per-iteration work -- 4 ORB extractions (prev/cur x L/R),
-    2 BF cross-check matchings, SGBM-3way, back-projection, PnP -- on 1 host thread and with
-    frames spread over `cores` threads (the C calls release the GIL), as SURVEY.md §8(d)
-    asks; `value` is the multi-core rate.  BASELINE.md §2's separate local-BA column: the
-    NumPy float64 BA specification (oracle/ba_ref.py) timed on K-frame windows of the same
-    frames (one window per frame, as the GPU path runs), 1 thread and over the pool."""
+    2 BF cross-check matchings, SGBM-3way, back-projection, PnP -- on 1 host thread (stage by
+    stage: `stages_ms_per_frame`) and with frames spread over `cores` threads (the C calls
+    release the GIL), as SURVEY.md §8(d) asks; `value` is the multi-core rate.  BASELINE.md §2's
+    separate local-BA column: the NumPy float64 BA specification (oracle/ba_ref.py) on K-frame
+    windows of the same frames (one window per frame, as the GPU path runs), 1 process and a
+    pool of `cores` processes (measured, r5: ba_ref holds the GIL, so threads cannot run it in
+    parallel)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test/baseline infrastructure only
     import ba_ref
-    from concurrent.futures import ThreadPoolExecutor
+    from concurrent.futures import ProcessPoolExecutor, ThreadPoolExecutor
+    import multiprocessing as mproc
     from forest_slam_amd import synth
     cores, why = cpu_threads()
     n_mt = max(n_frames, cores * 2, ba_window + 4)
@@ -121,9 +135,35 @@ def cpu_baseline(n_frames: int, nfeatures: int, W: int, H: int, ba_window: int) 
         oracle.bf_match(dR0, dR1)
         return out
 
+    def staged(i, acc):
+        """one() stage by stage (same calls, stereo_slam.py:232-306 order), times into acc."""
+        (pL, pR), (cL, cR) = imgs[i], imgs[i + 1]
+        t = time.perf_counter
+        t0 = t()
+        kp0, d0 = oracle.orb_detect_compute(pL, nfeatures)
+        kp1, d1 = oracle.orb_detect_compute(cL, nfeatures)
+        _, dR0 = oracle.orb_detect_compute(pR, nfeatures)
+        _, dR1 = oracle.orb_detect_compute(cR, nfeatures)
+        t1 = t()
+        m = oracle.bf_match(d0, d1) if len(d0) and len(d1) else np.zeros((0, 3), np.int32)
+        oracle.bf_match(dR0, dR1)
+        t2 = t()
+        disp16 = oracle.sgbm(pL, pR)
+        t3 = t()
+        P3, p2, _ = oracle.backproject(oracle.disparity_map(disp16), kp0[:, :2].astype(np.float32)[m[:, 0]],
+                                       kp1[:, :2].astype(np.float32)[m[:, 1]], seq.K, synth.BASELINE)
+        t4 = t()
+        if len(P3) >= 6:
+            oracle.solve_pnp_ransac(P3, p2, seq.K, synth.DIST_L)
+        t5 = t()
+        for k, v in (("orb_x4", t1 - t0), ("bf_x2", t2 - t1), ("sgbm", t3 - t2), ("backproject", t4 - t3),
+                     ("pnp_ransac", t5 - t4)):
+            acc[k] = acc.get(k, 0.0) + v
+
+    acc = {}
     t0 = time.perf_counter()
     for i in range(n_frames):
-        one(i)
+        staged(i, acc)
     dt1 = time.perf_counter() - t0
     with ThreadPoolExecutor(max_workers=cores) as ex:
         t0 = time.perf_counter()
@@ -131,34 +171,42 @@ def cpu_baseline(n_frames: int, nfeatures: int, W: int, H: int, ba_window: int) 
         dtm = time.perf_counter() - t0
     res = {"value": n_mt / dtm, "unit": "frames/s", "cores": cores, "cores_from": why, "kind": "port",
            "value_1core": n_frames / dt1, "host_cpus": host_cpus(),
+           "stages_ms_per_frame": {k: round(v / n_frames * 1e3, 2) for k, v in acc.items()},
            "sample": f"{W}x{H} synthetic stereo frames, nfeatures={nfeatures}: 4 ORB + 2 BF-xcheck + "
                      f"SGBM-3way + back-projection + PnP-RANSAC per frame, oracle/ scalar C++; {n_mt} frames "
-                     f"over {cores} threads in {dtm:.1f} s; {n_frames} frames on 1 thread in {dt1:.1f} s"}
+                     f"over {cores} threads in {dtm:.1f} s; {n_frames} frames on 1 thread in {dt1:.1f} s "
+                     f"(stage by stage)"}
     if ba_window:
         kps = [p["kp0"] for p in pairs] + [pairs[-1]["kp1"]]
         stereo = [ba_ref.stereo_points(kps[j], pairs[j]["disp16"], seq.K, synth.BASELINE) for j in range(n_mt)]
         rel = [p["T"] if p["T"] is not None else np.eye(4) for p in pairs]
         ends = list(range(ba_window - 1, n_mt))
 
-        def win(e):
+        def job(e):
             s = e - ba_window + 1
-            return ba_ref.ba_window(kps[s:e + 1], [p["matches"] for p in pairs[s:e]], stereo[s:e], rel[s:e], seq.K,
-                                    synth.BASELINE, iters=10)
+            return (ROOT, kps[s:e + 1], [p["matches"] for p in pairs[s:e]], stereo[s:e], rel[s:e], seq.K,
+                    synth.BASELINE)
 
-        # ba_ref is NumPy on small arrays and holds the GIL, so threads do not scale it (measured:
-        # 8 threads slower than 1): timed on 1 thread; the per-core rate x cores is the bound a
-        # process-parallel CPU run could reach, and that optimistic figure is the one combined
-        n1 = min(2, len(ends))
+        n1 = min(4, len(ends))
         t0 = time.perf_counter()
         for e in ends[:n1]:
-            win(e)
+            _ba_window_job(job(e))
         b1 = time.perf_counter() - t0
-        ba_fps1 = n1 / b1
-        ba_fps = ba_fps1 * cores
-        res["local_ba"] = {"value": round(ba_fps, 3), "value_1core": round(ba_fps1, 4), "unit": "windows/s (= frames/s)",
-                           "window": ba_window, "what": "oracle/ba_ref.py (NumPy fp64 LM, 10 iterations) per window; "
-                                                       "value = 1-thread rate x cores (GIL-bound, not run threaded)",
-                           "sample": f"{n1} windows of {ba_window} frames on 1 thread in {b1:.1f} s"}
+        # the pool: every window once more, `cores` worker processes (spawned: the parent holds
+        # the GPU runtime), timed from the first submission to the last result after a warm-up map
+        # that starts the workers
+        jobs = [job(e) for e in ends]
+        with ProcessPoolExecutor(max_workers=cores, mp_context=mproc.get_context("spawn")) as ex:
+            list(ex.map(_ba_window_job, jobs[:cores]))
+            t0 = time.perf_counter()
+            list(ex.map(_ba_window_job, jobs))
+            bm = time.perf_counter() - t0
+        ba_fps = len(jobs) / bm
+        res["local_ba"] = {"value": round(ba_fps, 3), "value_1core": round(n1 / b1, 4), "unit": "windows/s (= frames/s)",
+                           "window": ba_window, "what": "oracle/ba_ref.py (NumPy fp64 LM, 10 iterations) per window, "
+                                                       f"measured over a pool of {cores} processes",
+                           "sample": f"{len(jobs)} windows of {ba_window} frames over {cores} processes in {bm:.1f} s; "
+                                     f"{n1} windows on 1 process in {b1:.1f} s"}
         res["value_with_ba"] = round(1.0 / (1.0 / res["value"] + 1.0 / ba_fps), 3)
     return res
 
@@ -470,7 +518,7 @@ def main():
     ap.add_argument("--height", type=int, default=600)
     ap.add_argument("--ate-frames", type=int, default=200, help="frames of the ATE run (0 = skip)")
     ap.add_argument("--ba-window", type=int, default=10, help="local BA window K (0 = PnP only)")
-    ap.add_argument("--cpu-frames", type=int, default=2, help="CPU baseline 1-thread sample (0 = skip)")
+    ap.add_argument("--cpu-frames", type=int, default=6, help="CPU baseline 1-thread sample, frames (0 = skip)")
     ap.add_argument("--cpu-ate", type=int, default=1, help="ATE of the CPU reference path on the ATE frames")
     ap.add_argument("--overlap-sgbm", type=int, default=1, help="SGBM of step k+1 on a side stream during step k")
     ap.add_argument("--ba-max-landmarks", type=int, default=0, help="per-window landmark cap (0 = library default)")
@@ -629,6 +677,23 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_frames > 0:
         cpu = cpu_baseline(args.cpu_frames, args.nfeatures, W, H, args.ba_window)
+        # per-frame stage times beside the GPU's (in-order breakdown pass / B; ORB: the CPU path
+        # extracts 4 images per frame as the reference does, the GPU path 2)
+        g = {k: v / B for k, v in stage_ms.items()}
+        gpu_stage = {"orb": sum(v for k, v in g.items() if k.startswith("orb_")),
+                     "bf": g.get("bf_argmin", 0.0) + g.get("bf_finish", 0.0),
+                     "sgbm": sum(v for k, v in g.items() if k.startswith("sgbm_")),
+                     "backproject": g.get("backproject", 0.0), "pnp_ransac": g.get("pnp_ransac", 0.0),
+                     "local_ba": g.get("ba_solve", 0.0) + g.get("ba_build", 0.0) + g.get("ba_stereo", 0.0)}
+        cs = cpu["stages_ms_per_frame"]
+        cpu["stage_compare_ms_per_frame"] = {
+            "orb": {"cpu_1thread": cs["orb_x4"], "gpu": round(gpu_stage["orb"], 4)},
+            "bf": {"cpu_1thread": cs["bf_x2"], "gpu": round(gpu_stage["bf"], 4)},
+            "sgbm": {"cpu_1thread": cs["sgbm"], "gpu": round(gpu_stage["sgbm"], 4)},
+            "backproject": {"cpu_1thread": cs["backproject"], "gpu": round(gpu_stage["backproject"], 4)},
+            "pnp_ransac": {"cpu_1thread": cs["pnp_ransac"], "gpu": round(gpu_stage["pnp_ransac"], 4)},
+            "local_ba": {"cpu_1process": round(1e3 / cpu["local_ba"]["value_1core"], 2) if "local_ba" in cpu else None,
+                         "gpu": round(gpu_stage["local_ba"], 4)}}
 
     cfg_name = ("configs[1]" if (W, H, args.nfeatures) == (960, 600, 1000) else
                 "configs[4] (1080p, 2000 kp, BA window 20)" if (W, H) == (1920, 1080) else "custom")

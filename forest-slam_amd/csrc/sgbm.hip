@@ -735,7 +735,7 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void
 // its state (+ minimum) every SEG columns -- at x = W1-1-SEG*(s+1), the left neighbour of sweep
 // 2's segment s.  Sweep 2 walks segments of SEG columns right->left (double-buffered C and V
 // loads one segment ahead): L recomputed forward over the segment from its checkpoint, then
-// the R path, S = L + R + V, first-minimum WTA as one u32 min of (S << 7 | d) across the
+// the R path, S = L + R + V, first-minimum WTA as one u32 min of (S << 8 | d) across the
 // row's lanes, integer sub-pixel, and the right-view key (cost << 16 | 0xFFFF - x1) lowered
 // by an LDS atomicMin -- the serial rule "replace iff disp2cost > cost" of sgbm_ref.cpp (the
 // smallest cost wins, among equal costs the largest x1, the first one the scan visits).  The
@@ -943,23 +943,28 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
   // one segment; FULL (every segment but the last): 8 valid columns and a checkpoint, so the
   // body has no per-column conditions
   // WTA of column i of a segment from its S words: first minimum over d as one u32 min of
-  // (S << 7 | d) across the row's lanes, then S[d-1] << 16 | S[d+1] from the lanes that hold
+  // (S << 8 | d) across the row's lanes, then S[d-1] << 16 | S[d+1] from the lanes that hold
   // them (OR across the row); every lane of the row ends with both, lane q keeps column q's
   auto ihi_of = [&](int sg) { return min(SEG - 1, W1 - 1 - SEG * sg); };  // valid i: x' < W1
   uint32_t wk = 0, wn = 0;
   auto wta = [&](int i, const uint32_t* Sw) {
-    uint32_t kmin = 0xFFFFFFFFu;
+    // keys (S << 8 | j) with j the disparity's index in this lane's run, built by byte permutes
+    // (S's two bytes above a byte of the constant (j, j + 1) pair word), min3-folded, then the
+    // lane's first disparity q * DQ added to the index byte (j + q * DQ < D <= 128: no carry)
+    uint32_t kmin = 0;
 #pragma unroll
     for (int kk = 0; kk < PQ; ++kk) {
-      const uint32_t d0 = (uint32_t)(q * DQ + 2 * kk);
-      kmin = min(kmin, ((Sw[kk] & 0xFFFFu) << 7) | d0);
-      kmin = min(kmin, ((Sw[kk] >> 16) << 7) | (d0 + 1));
+      const uint32_t jj = (uint32_t)(2 * kk) | ((uint32_t)(2 * kk + 1) << 8);
+      const uint32_t klo = __builtin_amdgcn_perm(Sw[kk], jj, 0x0c050400u);  // S[2kk] << 8 | 2kk
+      const uint32_t khi = __builtin_amdgcn_perm(Sw[kk], jj, 0x0c070601u);  // S[2kk+1] << 8 | 2kk+1
+      kmin = kk == 0 ? min(klo, khi) : min(kmin, min(klo, khi));
     }
+    kmin += (uint32_t)(q * DQ);
     kmin = dmin<kQX1>(kmin);
     kmin = dmin<kQX2>(kmin);
     kmin = dmin<kRHalfMirror>(kmin);
     kmin = dmin<kRMirror>(kmin);
-    const int d = (int)(kmin & 127u);
+    const int d = (int)(kmin & 0xFFu);
     // S[d-1] << 16 | S[d+1] (only read when 0 < d < D-1): the row's S words through a one-column
     // LDS slot (a wave's LDS accesses execute in order: no barrier, and the next column's store
     // comes after these loads)
@@ -1053,7 +1058,7 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
         const int x1 = W1 - 1 - (SEG * sg + q);
         if (colv) key[(x1 + p.minX1 - p.minD - (D - 1)) & (RK - 1)] = 0xFFFFFFFFu;
         if (colv) {
-          const int best = (int)(wk >> 7), d = (int)(wk & 127u);
+          const int best = (int)(wk >> 8), d = (int)(wk & 0xFFu);
           const int sm1 = (int)(wn >> 16), sp1 = (int)(wn & 0xFFFFu);
           const int x2 = x1 + p.minX1 - d - p.minD;
           if (x2 >= 0 && x2 < W && best < 0x7FFF)  // disp2cost starts at SHRT_MAX
