@@ -171,8 +171,42 @@ constexpr int kTW = 64, kTH = 32;
 constexpr int kRecKeep = 0, kRecPre = 8 * kTH, kRecSc = kRecPre + 2 * kTH;  // byte offsets in a record
 constexpr int kTRec = kRecSc + kTH * kTW / 2;  // + <= 1024 kept scores
 
-constexpr int kFW = kTW + 2, kFH = kTH + 2;     // FAST region (NMS halo)
-constexpr int kIW = kTW + 8, kIH = kTH + 8;     // image patch (FAST radius 3 + halo)
+constexpr int kFW = kTW + 2, kFH = kTH + 2;  // FAST region (NMS halo)
+constexpr int kPG = (kFW + 3) / 4;           // 4-pixel groups of a FAST region row
+// image patch: staged column j holds x0 - 5 + j, so FAST position c (x = x0 - 1 + c) sits at
+// column c + kIC and a group of 4 positions (c = 4g..4g+3) is the aligned dword g + 1
+constexpr int kIC = 4, kIW = kTW + 12, kIH = kTH + 8;
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+// bytes 0, 2 / 1, 3 of a dword as two u16 lanes
+__device__ __forceinline__ u16x2 bytes02(uint32_t v) { return as_u16x2(__builtin_amdgcn_perm(0u, v, 0x0c020c00u)); }
+__device__ __forceinline__ u16x2 bytes13(uint32_t v) { return as_u16x2(__builtin_amdgcn_perm(0u, v, 0x0c030c01u)); }
+
+// FAST prefilter on two pixels (u16 lanes): at least two of the four cardinal circle pixels
+// brighter than v + t, or at least two darker than v - t.  With s_k = sat(p_k - (v + t))
+// (nonzero = brighter), "two of a, b, c, d nonzero" = max(min(a,b), min(c,d),
+// min(max(a,b), max(c,d))) != 0: saturating subtracts and min/max only, all packed.
+__device__ __forceinline__ u16x2 two_of_four(u16x2 a, u16x2 b, u16x2 c, u16x2 d) {
+  const u16x2 lab = __builtin_elementwise_min(a, b), hab = __builtin_elementwise_max(a, b);
+  const u16x2 lcd = __builtin_elementwise_min(c, d), hcd = __builtin_elementwise_max(c, d);
+  return __builtin_elementwise_max(__builtin_elementwise_max(lab, lcd), __builtin_elementwise_min(hab, hcd));
+}
+__device__ __forceinline__ uint32_t fast_pre2(u16x2 v, u16x2 p0, u16x2 p4, u16x2 p8, u16x2 p12, u16x2 t) {
+  const u16x2 vt = v + t, vm = __builtin_elementwise_sub_sat(v, t);
+  auto br = [&](u16x2 p) { return __builtin_elementwise_sub_sat(p, vt); };
+  auto dk = [&](u16x2 p) { return __builtin_elementwise_sub_sat(vm, p); };
+  return as_u32(__builtin_elementwise_max(two_of_four(br(p0), br(p4), br(p8), br(p12)),
+                                          two_of_four(dk(p0), dk(p4), dk(p8), dk(p12))));
+}
+
+// a run of >= 9 set bits on the 16-circle (bit k = circle pixel k): doubling windows
+__device__ __forceinline__ bool has9(unsigned m) {
+  const unsigned mm = m | (m << 16);
+  const unsigned c2 = mm & (mm >> 1), c4 = c2 & (c2 >> 2), c8 = c4 & (c4 >> 4), c9 = c8 & (c8 >> 1);
+  return (c9 & 0xFFFFu) != 0;
+}
 
 __device__ __forceinline__ int tile_level(const OrbDev& G, int t) {
   int l = 0;
@@ -189,7 +223,9 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   __shared__ __attribute__((aligned(16))) uint8_t s_img[kIH][kIW];
   __shared__ __attribute__((aligned(16))) uint8_t s_sc[kFH][kFW];
   __shared__ uint16_t s_list[kFH * kFW];
-  __shared__ uint16_t s_pre[kFH * kFW];
+  __shared__ uint16_t s_pre[kFH * kPG * 4];
+  __shared__ uint32_t s_m[kTH][2];  // keep bits of a tile row (64 px), as two dwords
+  __shared__ int s_rp[kTH];
   __shared__ int s_n, s_npre;
   // XCD-aware tile order (xcd_block): tiles whose staged aprons share cache lines meet in
   // one L2 instead of being fetched by two XCDs
@@ -201,13 +237,12 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   const int x0 = tx * kTW, y0 = ty * kTH;
   const int w = G.w[l], h = G.h[l];
   const uint8_t* im = pyr + b * total + G.off[l];
-  if (x0 >= 4 && x0 + kTW + 8 <= w && y0 >= 4 && y0 + kTH + 4 <= h) {
+  if (x0 >= 8 && x0 + kTW + 12 <= w && y0 >= 4 && y0 + kTH + 4 <= h) {
     // interior tile: the staged rows and the aligned dwords around them lie inside the level
-    // row (4 px of slack on the right), so a row's 72 bytes come from 19 aligned dwords,
-    // byte-aligned by v_alignbyte
+    // row, so a row's 76 bytes come from 20 aligned dwords, byte-aligned by v_alignbyte
     for (int i = threadIdx.x; i < kIH * (kIW / 4); i += 256) {
       const int r = i / (kIW / 4), k = i % (kIW / 4);
-      const uint8_t* p = im + (int64_t)(y0 - 4 + r) * w + x0 - 4 + 4 * k;
+      const uint8_t* p = im + (int64_t)(y0 - 4 + r) * w + x0 - 1 - kIC + 4 * k;
       const uint32_t* a = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
       const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
       *reinterpret_cast<uint32_t*>(&s_img[r][4 * k]) = __builtin_amdgcn_alignbyte(a[1], a[0], sh);
@@ -215,35 +250,55 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   } else {
     for (int i = threadIdx.x; i < kIH * kIW; i += 256) {
       const int r = i / kIW, c = i % kIW;
-      const int y = min(max(y0 - 4 + r, 0), h - 1), x = min(max(x0 - 4 + c, 0), w - 1);
+      const int y = min(max(y0 - 4 + r, 0), h - 1), x = min(max(x0 - 1 - kIC + c, 0), w - 1);
       s_img[r][c] = im[(int64_t)y * w + x];
     }
   }
   for (int i = threadIdx.x; i < kFH * kFW / 4; i += 256) reinterpret_cast<uint32_t*>(&s_sc[0][0])[i] = 0;
+  if (threadIdx.x < 2 * kTH) (&s_m[0][0])[threadIdx.x] = 0u;
   if (threadIdx.x == 0) { s_n = 0; s_npre = 0; }
   __syncthreads();
   // FAST-9 on the tile + halo in two compacted stages.  (1) A 9-arc of the 16-circle always
   // holds at least two of the four cardinal pixels (0, 4, 8, 12), so a position with fewer
   // than two cardinals brighter than v+t and fewer than two darker than v-t cannot be a
-  // corner; the rest go to a pre-list.  (2) The full 16-pixel test on the pre-list; corners
-  // go to the list.  Same corners as testing every position.
-  for (int i0 = 0; i0 < kFH * kFW; i0 += 256) {  // uniform trip count: ballots see whole waves
+  // corner; the rest go to a pre-list.  This stage runs on 4 positions per lane: the centre
+  // and cardinal bytes of the group are 5 dword reads, tested as u16 pairs (saturating
+  // subtracts).  (2) The full 16-pixel test on the pre-list; corners go to the list.  Same
+  // corners as testing every position.
+  const u16x2 tt = {(unsigned short)thr, (unsigned short)thr};
+  for (int i0 = 0; i0 < kFH * kPG; i0 += 256) {  // uniform trip count: ballots see whole waves
     const int i = i0 + threadIdx.x;
-    const int r = i / kFW, c = i % kFW;
-    const int y = y0 - 1 + r, x = x0 - 1 + c;
-    bool maybe = false;
-    if (i < kFH * kFW && x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
-      const int v = s_img[r + 3][c + 3];
-      const int p0 = s_img[r][c + 3], p4 = s_img[r + 3][c + 6], p8 = s_img[r + 6][c + 3], p12 = s_img[r + 3][c];
-      const int nb = (p0 > v + thr) + (p4 > v + thr) + (p8 > v + thr) + (p12 > v + thr);
-      const int nd = (p0 < v - thr) + (p4 < v - thr) + (p8 < v - thr) + (p12 < v - thr);
-      maybe = nb >= 2 || nd >= 2;
+    const int r = i / kPG, g = i % kPG;
+    const int y = y0 - 1 + r, xg = x0 - 1 + 4 * g;
+    unsigned f = 0;
+    if (i < kFH * kPG && y >= 3 && y < h - 3) {
+      const uint32_t* rc = reinterpret_cast<const uint32_t*>(&s_img[r + 3][0]);
+      const uint32_t dv = rc[g + 1];
+      const uint32_t d0 = reinterpret_cast<const uint32_t*>(&s_img[r + 6][0])[g + 1];  // circle 0: dy +3
+      const uint32_t d8 = reinterpret_cast<const uint32_t*>(&s_img[r][0])[g + 1];      // circle 8: dy -3
+      const uint32_t d4 = __builtin_amdgcn_alignbyte(rc[g + 2], dv, 3);                 // circle 4: dx +3
+      const uint32_t d12 = __builtin_amdgcn_alignbyte(dv, rc[g], 1);                    // circle 12: dx -3
+      const uint32_t e = fast_pre2(bytes02(dv), bytes02(d0), bytes02(d4), bytes02(d8), bytes02(d12), tt);
+      const uint32_t o = fast_pre2(bytes13(dv), bytes13(d0), bytes13(d4), bytes13(d8), bytes13(d12), tt);
+      f = (unsigned)((e & 0xFFFFu) != 0) | (unsigned)((o & 0xFFFFu) != 0) << 1 | (unsigned)((e >> 16) != 0) << 2 |
+          (unsigned)((o >> 16) != 0) << 3;
+      // positions inside the region and 3 px from the level's sides
+      const int lo = max(3 - xg, 0), hi = min(min(w - 3 - xg, kFW - 4 * g), 4);
+      f &= hi > lo ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
     }
-    const unsigned long long m = __ballot(maybe);
+    const unsigned long long m0 = __ballot(f & 1u), m1 = __ballot(f & 2u), m2 = __ballot(f & 4u),
+                             m3 = __ballot(f & 8u);
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int pos = __popcll(m0 & below) + __popcll(m1 & below) + __popcll(m2 & below) + __popcll(m3 & below);
     int base = 0;
-    if ((threadIdx.x & 63) == 0 && m) base = atomicAdd(&s_npre, __popcll(m));
-    base = __shfl(base, 0, 64);
-    if (maybe) s_pre[base + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1ull))] = (uint16_t)i;
+    const int tot = __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+    if (lane == 0 && tot) base = atomicAdd(&s_npre, tot);
+    pos += __shfl(base, 0, 64);
+    const int ib = r * kFW + 4 * g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((f >> j) & 1u) s_pre[pos++] = (uint16_t)(ib + j);
   }
   __syncthreads();
   const int npre = s_npre;
@@ -254,21 +309,24 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
     if (j < npre) {
       i = s_pre[j];
       const int r = i / kFW, c = i % kFW;
-      const int v = s_img[r + 3][c + 3];
-      unsigned bright = 0, dark = 0;
+      const int v = s_img[r + 3][c + kIC];
+      // circle pixels k and k + 8 share a dword (u16 lanes); the sign bit of (v + t) - p
+      // (bright) / p - (v - t) (dark) is shifted to bit k of its lane and merged into the mask
+      const u16x2 vt = {(unsigned short)(v + thr), (unsigned short)(v + thr)};
+      const u16x2 vm = {(unsigned short)(v - thr), (unsigned short)(v - thr)};
+      uint32_t ab = 0, ad = 0;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int p = s_img[r + 3 + c_cdy[k]][c + 3 + c_cdx[k]];
-        bright |= (unsigned)(p > v + thr) << k;
-        dark |= (unsigned)(p < v - thr) << k;
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t pk = (uint32_t)s_img[r + 3 + c_cdy[k]][c + kIC + c_cdx[k]] |
+                            (uint32_t)s_img[r + 3 + c_cdy[k + 8]][c + kIC + c_cdx[k + 8]] << 16;
+        const u16x2 sh = {(unsigned short)(15 - k), (unsigned short)(15 - k)};
+        const uint32_t K = 0x10001u << k;
+        ab |= as_u32((vt - as_u16x2(pk)) >> sh) & K;
+        ad |= as_u32((as_u16x2(pk) - vm) >> sh) & K;
       }
-      auto has9 = [](unsigned mm0) {
-        unsigned mm = mm0 | (mm0 << 16);
-        unsigned cc = mm;
-#pragma unroll
-        for (int jj = 1; jj <= 8; ++jj) cc &= mm >> jj;
-        return (cc & 0xFFFFu) != 0;
-      };
+      // lanes -> 16-bit masks: bits 0..7 from the low lane, 8..15 from the high lane
+      const unsigned bright = __builtin_amdgcn_perm(0u, ab, 0x0c0c0200u);
+      const unsigned dark = __builtin_amdgcn_perm(0u, ad, 0x0c0c0200u);
       corner = has9(bright) || has9(dark);
     }
     const unsigned long long m = __ballot(corner);
@@ -283,12 +341,12 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   for (int j = threadIdx.x; j < nc; j += 256) {
     const int i = s_list[j];
     const int r = i / kFW, c = i % kFW;
-    const int v = s_img[r + 3][c + 3];
+    const int v = s_img[r + 3][c + kIC];
     // the minimum / maximum of d = v - p over every 9-arc of the circle by doubling windows
     // (2, 4, 8, then + 1): 128 min/max instead of 2 x 16 x 9 -- exact, order-free
     int d[16], n2[16], x2[16], n4[16], x4[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) d[k] = v - (int)s_img[r + 3 + c_cdy[k]][c + 3 + c_cdx[k]];
+    for (int k = 0; k < 16; ++k) d[k] = v - (int)s_img[r + 3 + c_cdy[k]][c + kIC + c_cdx[k]];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       n2[k] = min(d[k], d[(k + 1) & 15]);
@@ -310,49 +368,56 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
     s_sc[r][c] = (uint8_t)(max(a0, b0) - 1);
   }
   __syncthreads();
-  // NMS + border filter of the tile; one wave row = 64 pixels = one keep word
-  const int c = threadIdx.x & 63;
-  const int x = x0 + c;
-  __shared__ unsigned long long s_m[kTH];
-  __shared__ int s_rp[kTH];
-  for (int rr = threadIdx.x >> 6; rr < kTH; rr += 4) {
-    const int y = y0 + rr;
-    bool k = false;
-    int sv = 0;
-    if (y < h && x < w) {  // y < h is uniform per wave
-      sv = s_sc[rr + 1][c + 1];
-      k = sv && x >= edge && x < w - edge && y >= edge && y < h - edge && sv > s_sc[rr][c] && sv > s_sc[rr][c + 1] &&
-          sv > s_sc[rr][c + 2] && sv > s_sc[rr + 1][c] && sv > s_sc[rr + 1][c + 2] && sv > s_sc[rr + 2][c] &&
-          sv > s_sc[rr + 2][c + 1] && sv > s_sc[rr + 2][c + 2];
+  if (SCOREMAP) {  // debug hook: the score of every tile pixel (0 = no corner)
+    const int c = threadIdx.x & 63, x = x0 + c;
+    for (int rr = threadIdx.x >> 6; rr < kTH; rr += 4) {
+      const int y = y0 + rr;
+      if (y < h && x < w) score[b * total + G.off[l] + (int64_t)y * w + x] = s_sc[rr + 1][c + 1];
     }
-    if (SCOREMAP) {
-      if (y < h && x < w) score[b * total + G.off[l] + (int64_t)y * w + x] = (uint8_t)sv;
-      continue;
-    }
-    const unsigned long long m = __ballot(k);
-    if (c == 0) s_m[rr] = m;  // rows past the level's end keep nothing
+    return;
   }
-  if (SCOREMAP) return;
+  // strict 3x3 NMS + border filter, on the corners only (every other pixel scores 0): a kept
+  // corner sets its bit in its row's keep word and is marked in the list
+  for (int j = threadIdx.x; j < nc; j += 256) {
+    const int i = s_list[j];
+    const int r = i / kFW, c = i % kFW;
+    const int x = x0 - 1 + c, y = y0 - 1 + r;
+    if (r < 1 || r > kTH || c < 1 || c > kTW || x >= w - edge || y >= h - edge || x < edge || y < edge) continue;
+    const int sv = s_sc[r][c];
+    const bool k = sv && sv > s_sc[r - 1][c - 1] && sv > s_sc[r - 1][c] && sv > s_sc[r - 1][c + 1] && sv > s_sc[r][c - 1] &&
+                   sv > s_sc[r][c + 1] && sv > s_sc[r + 1][c - 1] && sv > s_sc[r + 1][c] && sv > s_sc[r + 1][c + 1];
+    if (k) {
+      atomicOr(&s_m[r - 1][(c - 1) >> 5], 1u << ((c - 1) & 31));
+      s_list[j] = (uint16_t)(i | 0x8000);
+    }
+  }
   __syncthreads();
   // tile-local prefix of the rows' keep counts (rows past the level's end hold none)
   if (threadIdx.x < 64) {
-    const int v = threadIdx.x < kTH ? __popcll(s_m[threadIdx.x]) : 0;
+    const int c = threadIdx.x;
+    const int v = c < kTH ? __popc(s_m[c][0]) + __popc(s_m[c][1]) : 0;
     int inc = v;
 #pragma unroll
     for (int o = 1; o < 32; o <<= 1) {
       const int u = __shfl_up(inc, o, 64);
       if (c >= o) inc += u;
     }
-    if (threadIdx.x < kTH) s_rp[threadIdx.x] = inc - v;
+    if (c < kTH) s_rp[c] = inc - v;
   }
   __syncthreads();
   uint8_t* rec = trec + ((int64_t)b * ntiles + t) * kTRec;
-  if (threadIdx.x < kTH) reinterpret_cast<unsigned long long*>(rec + kRecKeep)[threadIdx.x] = s_m[threadIdx.x];
+  if (threadIdx.x < kTH)
+    reinterpret_cast<unsigned long long*>(rec + kRecKeep)[threadIdx.x] =
+        (unsigned long long)s_m[threadIdx.x][0] | (unsigned long long)s_m[threadIdx.x][1] << 32;
   else if (threadIdx.x < 2 * kTH)
     reinterpret_cast<uint16_t*>(rec + kRecPre)[threadIdx.x - kTH] = (uint16_t)s_rp[threadIdx.x - kTH];
-  for (int rr = threadIdx.x >> 6; rr < kTH; rr += 4) {
-    const unsigned long long m = s_m[rr];
-    if ((m >> c) & 1ull) rec[kRecSc + s_rp[rr] + __popcll(m & ((1ull << c) - 1ull))] = s_sc[rr + 1][c + 1];
+  for (int j = threadIdx.x; j < nc; j += 256) {
+    const int e = s_list[j];
+    if (!(e & 0x8000)) continue;
+    const int i = e & 0x7FFF;
+    const int r = i / kFW, c = i % kFW;
+    const unsigned long long m = (unsigned long long)s_m[r - 1][0] | (unsigned long long)s_m[r - 1][1] << 32;
+    rec[kRecSc + s_rp[r - 1] + __popcll(m & ((1ull << (c - 1)) - 1ull))] = s_sc[r][c];
   }
 }
 
