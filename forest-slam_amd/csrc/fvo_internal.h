@@ -63,7 +63,6 @@ struct fvo_ctx {
   uint8_t* blur = nullptr;    // [B][total_px] debug only (orb_blur_debug), allocated on first use
   int orb_last_batch = 0;     // images of the last ORB call
   uint8_t* score = nullptr;   // [B][total_px]
-  int32_t* rowoff = nullptr;  // [B][total_rows]
   uint32_t* cand = nullptr;   // [B][cand_total] packed (score<<24 | y<<12 | x)
   uint64_t* hel = nullptr;    // [B][cand_total] (harris float bits << 32 | packed)
   int32_t* ncand = nullptr;   // [B][L]

@@ -45,6 +45,9 @@ __constant__ int c_umax[20];
 __constant__ signed char c_pattern[256 * 4];
 
 constexpr int kSelThreads = 512;
+// LDS capacity of the selection kernels (candidates per (image, level)); larger levels select
+// in global memory.  select 1: u32 candidates, select 2: u64 Harris records.
+constexpr int kSelCap1 = 10000, kSelCap2 = 4096;
 
 __device__ __forceinline__ int level_of_row(const OrbDev& G, int r) {
   int l = 0;
@@ -421,89 +424,6 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   }
 }
 
-// ordered (row-major) compaction of the kept pixels: one wave per row; the scores come from
-// the tile records k_fast_nms wrote
-__global__ __launch_bounds__(64) void k_keep_compact(const OrbDev G, const uint8_t* __restrict__ trec,
-                                                     const int32_t* __restrict__ rowoff, uint32_t* __restrict__ cand,
-                                                     int64_t cand_total, int edge, int ntiles) {
-  const int r = blockIdx.x, b = blockIdx.y;
-  const int l = level_of_row(G, r);
-  const int y = r - G.row0[l];
-  const int h = G.h[l];
-  if (y < edge || y >= h - edge) return;
-  const int lane = threadIdx.x, ntx = G.ntx[l];
-  // this row's records: tile (y / kTH, lane) of the level; the row's keep word and prefix in it
-  const uint8_t* myrec = trec + ((int64_t)b * ntiles + G.tile0[l] + (y / kTH) * ntx + min(lane, ntx - 1)) * kTRec;
-  const unsigned long long word =
-      lane < ntx ? reinterpret_cast<const unsigned long long*>(myrec + kRecKeep)[y % kTH] : 0ull;
-  const int cnt = __popcll(word);
-  int inc = cnt;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int v = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += v;
-  }
-  const int pre_lane = inc - cnt;
-  const int rpre = word ? reinterpret_cast<const uint16_t*>(myrec + kRecPre)[y % kTH] : 0;
-  const int base = rowoff[(int64_t)b * G.total_rows + r];
-  uint32_t* out = cand + b * cand_total + G.cand_off[l];
-  for (int j = 0; j < ntx; ++j) {
-    const unsigned long long wj = __shfl(word, j, 64);
-    if (!wj) continue;  // uniform
-    const int pj = __shfl(pre_lane, j, 64);
-    const int rj = __shfl(rpre, j, 64);
-    if ((wj >> lane) & 1ull) {
-      const int x = 64 * j + lane;
-      const int rank = __popcll(wj & ((1ull << lane) - 1ull));
-      const uint8_t* rec = trec + ((int64_t)b * ntiles + G.tile0[l] + (y / kTH) * ntx + j) * kTRec;
-      out[base + pj + rank] = ((uint32_t)rec[kRecSc + rj + rank] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
-    }
-  }
-}
-
-// per level: each row's keep count (popcounts of its keep words in the level's tile records),
-// exclusive scan -> row offsets, total -> ncand
-__global__ void k_row_scan(const OrbDev G, const uint8_t* __restrict__ trec, int32_t* __restrict__ rowoff,
-                           int32_t* __restrict__ ncand, int total_rows, int nlevels, int ntiles) {
-  int l = blockIdx.x, b = blockIdx.y;
-  int r0 = G.row0[l], h = G.h[l];
-  const int ntx = G.ntx[l];
-  const uint8_t* lrec = trec + ((int64_t)b * ntiles + G.tile0[l]) * kTRec;
-  auto rc = [&](int y) {
-    const uint8_t* rr = lrec + (int64_t)(y / kTH) * ntx * kTRec + kRecKeep + 8 * (y % kTH);
-    int n = 0;
-    for (int j = 0; j < ntx; ++j) n += __popcll(*reinterpret_cast<const unsigned long long*>(rr + (int64_t)j * kTRec));
-    return n;
-  };
-  int32_t* ro = rowoff + (int64_t)b * total_rows + r0;
-  __shared__ int s_w[16];
-  __shared__ int s_carry;
-  if (threadIdx.x == 0) s_carry = 0;
-  __syncthreads();
-  for (int base = 0; base < h; base += blockDim.x) {
-    int i = base + threadIdx.x;
-    int v = i < h ? rc(i) : 0;
-    int inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      int t = __shfl_up(inc, o, 64);
-      if (wave_lane() >= o) inc += t;
-    }
-    if (wave_lane() == 63) s_w[threadIdx.x >> 6] = inc;
-    __syncthreads();
-    int wpre = 0, tot = 0;
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
-      if (k < (int)(threadIdx.x >> 6)) wpre += s_w[k];
-      tot += s_w[k];
-    }
-    if (i < h) ro[i] = s_carry + wpre + inc - v;
-    __syncthreads();
-    if (threadIdx.x == 0) s_carry += tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) ncand[b * nlevels + l] = s_carry;
-}
-
 // ------------------------------------------------------------------ retainBest
 // Element views: key() is the KeyPoint.response the comparator looks at.
 struct ElemFast {
@@ -522,31 +442,44 @@ struct SelShared {
   int lo, hi, cut;
 };
 
-// Block-wide two-flag exclusive scan; returns prefixes, updates per-flag running carries
-// (uniform), tot[] = chunk totals.
-__device__ __forceinline__ void scan2(SelShared& sh, int f0, int f1, int& p0, int& p1) {
+// Block-wide exclusive scan of two per-thread counts (< 2^NB); returns the prefixes (including the
+// running carries) and advances the carries (uniform afterwards).
+template <int NB = 6>
+__device__ __forceinline__ void scan2(SelShared& sh, int v0, int v1, int& p0, int& p1) {
   const int lane = wave_lane(), wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  unsigned long long m0 = __ballot(f0), m1 = __ballot(f1);
-  unsigned long long below = (1ull << lane) - 1ull;
-  int w0 = __popcll(m0 & below), w1 = __popcll(m1 & below);
-  if (lane == 0) { sh.wsum[0][wid] = __popcll(m0); sh.wsum[1][wid] = __popcll(m1); }
+  // wave exclusive prefixes and totals of counts in [0, 2^NB), bit-sliced: one ballot per bit
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int e0 = 0, e1 = 0, s0 = 0, s1 = 0;
+#pragma unroll
+  for (int bt = 0; bt < NB; ++bt) {
+    const unsigned long long m0 = __ballot((v0 >> bt) & 1), m1 = __ballot((v1 >> bt) & 1);
+    e0 += __popcll(m0 & below) << bt;
+    e1 += __popcll(m1 & below) << bt;
+    s0 += __popcll(m0) << bt;
+    s1 += __popcll(m1) << bt;
+  }
+  if (lane == 0) { sh.wsum[0][wid] = s0; sh.wsum[1][wid] = s1; }
   __syncthreads();
   int a0 = 0, a1 = 0, t0 = 0, t1 = 0;
   for (int i = 0; i < nw; ++i) {
-    int v0 = sh.wsum[0][i], v1 = sh.wsum[1][i];
-    if (i < wid) { a0 += v0; a1 += v1; }
-    t0 += v0; t1 += v1;
+    const int w0 = sh.wsum[0][i], w1 = sh.wsum[1][i];
+    if (i < wid) { a0 += w0; a1 += w1; }
+    t0 += w0; t1 += w1;
   }
-  p0 = sh.carry[0] + a0 + w0;
-  p1 = sh.carry[1] + a1 + w1;
+  p0 = sh.carry[0] + a0 + e0;
+  p1 = sh.carry[1] + a1 + e1;
   __syncthreads();
   if (threadIdx.x == 0) { sh.carry[0] += t0; sh.carry[1] += t1; }
   __syncthreads();
 }
 
-__device__ __forceinline__ int block_count(SelShared& sh, int f) {
-  unsigned long long m = __ballot(f);
-  if (wave_lane() == 0) sh.wsum[0][threadIdx.x >> 6] = __popcll(m);
+// block sum of per-thread counts in [0, 2^NB)
+template <int NB>
+__device__ __forceinline__ int block_sum(SelShared& sh, int v) {
+  int x = 0;
+#pragma unroll
+  for (int bt = 0; bt < NB; ++bt) x += __popcll(__ballot((v >> bt) & 1)) << bt;
+  if (wave_lane() == 0) sh.wsum[0][threadIdx.x >> 6] = x;
   __syncthreads();
   int t = 0;
   for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh.wsum[0][i];
@@ -554,25 +487,42 @@ __device__ __forceinline__ int block_count(SelShared& sh, int f) {
   return t;
 }
 
+// Elements per thread of one scan pass (bits of a u32 flag word): a range of up to
+// kSelThreads * kSelPer positions costs one block scan, not one per kSelThreads.
+constexpr int kSelPer = 32;
+
 // Compact positions i in [first,last) with predicate A (ascending into SA) and B
-// (ascending into SB).  Returns counts.
-template <class E, class PA, class PB>
-__device__ void compact2(SelShared& sh, const typename E::T* a, int first, int last, int* SA, int* SB, PA pa, PB pb,
+// (ascending into SB).  Returns counts.  Each thread takes a run of consecutive positions,
+// so thread order = position order and one exclusive scan of the per-thread counts places
+// every position.
+template <class E, class I, class PA, class PB>
+__device__ void compact2(SelShared& sh, const typename E::T* a, int first, int last, I* SA, I* SB, PA pa, PB pb,
                          int& nA, int& nB) {
   if (threadIdx.x == 0) { sh.carry[0] = 0; sh.carry[1] = 0; }
   __syncthreads();
-  for (int base = first; base < last; base += blockDim.x) {
-    int i = base + threadIdx.x;
-    int fa = 0, fb = 0;
-    if (i < last) {
-      float k = E::key(a[i]);
-      fa = pa(k);
-      fb = pb(k);
+  for (int base = first; base < last; base += (int)blockDim.x * kSelPer) {
+    const int len = min(last - base, (int)blockDim.x * kSelPer);
+    const int per = (len + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int i0 = base + (int)threadIdx.x * per, i1 = min(i0 + per, base + len);
+    uint32_t ma = 0, mb = 0;
+    for (int i = i0; i < i1; ++i) {
+      const float k = E::key(a[i]);
+      ma |= (uint32_t)pa(k) << (i - i0);
+      mb |= (uint32_t)pb(k) << (i - i0);
     }
     int p0, p1;
-    scan2(sh, fa, fb, p0, p1);
-    if (fa) SA[p0] = i;
-    if (fb) SB[p1] = i;
+    if (per == 1) scan2<1>(sh, (int)ma, (int)mb, p0, p1);  // uniform: flags, one ballot each
+    else scan2<6>(sh, __popc(ma), __popc(mb), p0, p1);
+    while (ma) {
+      const int j = __builtin_ctz(ma);
+      ma &= ma - 1u;
+      SA[p0++] = (I)(i0 + j);
+    }
+    while (mb) {
+      const int j = __builtin_ctz(mb);
+      mb &= mb - 1u;
+      SB[p1++] = (I)(i0 + j);
+    }
   }
   nA = sh.carry[0];
   nB = sh.carry[1];
@@ -581,15 +531,19 @@ __device__ void compact2(SelShared& sh, const typename E::T* a, int first, int l
 
 // Pair the k-th A position (ascending) with the k-th B position from the right while
 // A_k < B_k; swap each pair.  This is exactly the set of swaps a sequential Hoare scan
-// (libstdc++ __unguarded_partition / bidirectional __partition) performs.  Returns k*.
-template <class E>
-__device__ int pair_swap(SelShared& sh, typename E::T* a, const int* SA, int nA, const int* SB, int nB) {
-  int m = min(nA, nB);
+// (libstdc++ __unguarded_partition / bidirectional __partition) performs.  Returns k*
+// (the predicate is monotone in k -- A_k rises, B_{nB-1-k} falls -- so k* is its count).
+template <class E, class I>
+__device__ int pair_swap(SelShared& sh, typename E::T* a, const I* SA, int nA, const I* SB, int nB) {
+  const int m = min(nA, nB);
   int c = 0;
-  for (int base = 0; base < m; base += blockDim.x) {
-    int k = base + threadIdx.x;
-    int f = k < m && SA[k] < SB[nB - 1 - k];
-    c += block_count(sh, f);
+  for (int base = 0; base < m; base += (int)blockDim.x * kSelPer) {
+    const int len = min(m - base, (int)blockDim.x * kSelPer);
+    const int per = (len + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int k0 = base + (int)threadIdx.x * per, k1 = min(k0 + per, base + len);
+    int f = 0;
+    for (int k = k0; k < k1; ++k) f += (int)SA[k] < (int)SB[nB - 1 - k];
+    c += per == 1 ? block_sum<1>(sh, f) : block_sum<6>(sh, f);
   }
   for (int k = threadIdx.x; k < c; k += blockDim.x) {
     int i = SA[k], j = SB[nB - 1 - k];
@@ -680,8 +634,8 @@ __device__ __forceinline__ int ilog2(int n) { return 31 - __clz(n); }
 
 // KeyPointsFilter::retainBest(a[0..n), keep) executed by one workgroup.  Returns the
 // surviving count; a[] is left in OpenCV's element order.
-template <class E>
-__device__ int select_block(SelShared& sh, typename E::T* a, int n, int keep, int* SA, int* SB) {
+template <class E, class I>
+__device__ int select_block(SelShared& sh, typename E::T* a, int n, int keep, I* SA, I* SB) {
   if (keep < 0 || n <= keep) return n;
   if (keep == 0) return 0;
   const int nth = keep - 1;
@@ -702,8 +656,8 @@ __device__ int select_block(SelShared& sh, typename E::T* a, int n, int keep, in
     __syncthreads();
     const float P = E::key(a[lo]);
     int nL, nR;
-    compact2<E>(sh, a, lo + 1, hi, SA, SB, [P](float k) { return k <= P; }, [P](float k) { return k >= P; }, nL, nR);
-    int ks = pair_swap<E>(sh, a, SA, nL, SB, nR);
+    compact2<E, I>(sh, a, lo + 1, hi, SA, SB, [P](float k) { return k <= P; }, [P](float k) { return k >= P; }, nL, nR);
+    int ks = pair_swap<E, I>(sh, a, SA, nL, SB, nR);
     int Lk = ks < nL ? SA[ks] : hi;
     int Rk = ks > 0 ? SB[nR - ks] : hi;
     int cut = min(Lk, Rk);
@@ -715,24 +669,104 @@ __device__ int select_block(SelShared& sh, typename E::T* a, int n, int keep, in
   }
   const float amb = E::key(a[nth]);
   int nF, nG;
-  compact2<E>(sh, a, keep, n, SA, SB, [amb](float k) { return !(k >= amb); }, [amb](float k) { return k >= amb; },
-              nF, nG);
-  pair_swap<E>(sh, a, SA, nF, SB, nG);
+  compact2<E, I>(sh, a, keep, n, SA, SB, [amb](float k) { return !(k >= amb); }, [amb](float k) { return k >= amb; },
+                 nF, nG);
+  pair_swap<E, I>(sh, a, SA, nF, SB, nG);
   return keep + nG;
 }
 
-template <class E>
-__global__ __launch_bounds__(kSelThreads) void k_select(const OrbDev G, typename E::T* __restrict__ arr,
-                                                        const int32_t* __restrict__ nin, int32_t* __restrict__ nout,
+// Ordered (row-major) compaction of level l's kept pixels from the tile records k_fast_nms
+// wrote: (row, tile) keep words in row-major order, a thread per run of up to kCmpPer
+// consecutive words (all loads in flight at once), one block scan of the runs' counts, each
+// word's pixels written at its offset -- (score << 24 | y << 12 | x), the order cv::FAST lists
+// keypoints in.  Candidates go to the global array and, while they fit, to the LDS copy.
+// Returns the count.
+constexpr int kCmpPer = 16;
+template <int CAP>
+__device__ int compact_level(SelShared& sh, const OrbDev& G, const uint8_t* __restrict__ trec, int ntiles, int edge,
+                             int l, int b, uint32_t* __restrict__ out, uint32_t* s_out) {
+  const int h = G.h[l], ntx = G.ntx[l];
+  const int ya = edge, yb = h - edge;  // the NMS border filter keeps nothing outside
+  const int npairs = yb > ya ? (yb - ya) * ntx : 0;
+  const uint8_t* lrec = trec + ((int64_t)b * ntiles + G.tile0[l]) * kTRec;
+  if (threadIdx.x == 0) { sh.carry[0] = 0; sh.carry[1] = 0; }
+  __syncthreads();
+  for (int base = 0; base < npairs; base += (int)blockDim.x * kCmpPer) {
+    const int len = min(npairs - base, (int)blockDim.x * kCmpPer);
+    const int per = (len + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int q0 = base + (int)threadIdx.x * per, q1 = min(q0 + per, base + len);
+    const int y0 = ya + q0 / ntx, tx0 = q0 - (y0 - ya) * ntx;
+    unsigned long long w[kCmpPer];
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0, y = y0, tx = tx0; j < kCmpPer; ++j) {
+      w[j] = 0;
+      if (q0 + j < q1)
+        w[j] = reinterpret_cast<const unsigned long long*>(lrec + (int64_t)((y / kTH) * ntx + tx) * kTRec +
+                                                           kRecKeep)[y % kTH];
+      cnt += __popcll(w[j]);
+      if (++tx == ntx) { tx = 0; ++y; }
+    }
+    int o, o1;
+    scan2<11>(sh, cnt, 0, o, o1);  // <= kCmpPer * 64
+#pragma unroll
+    for (int j = 0, y = y0, tx = tx0; j < kCmpPer; ++j) {
+      unsigned long long word = w[j];
+      if (word) {
+        const uint8_t* rec = lrec + (int64_t)((y / kTH) * ntx + tx) * kTRec;
+        const uint8_t* sc = rec + kRecSc + reinterpret_cast<const uint16_t*>(rec + kRecPre)[y % kTH];
+        for (int k = 0; word; ++k) {
+          const int bit = __builtin_ctzll(word);
+          word &= word - 1ull;
+          const uint32_t e = ((uint32_t)sc[k] << 24) | ((uint32_t)y << 12) | (uint32_t)(64 * tx + bit);
+          out[o] = e;
+          if (o < CAP) s_out[o] = e;
+          ++o;
+        }
+      }
+      if (++tx == ntx) { tx = 0; ++y; }
+    }
+  }
+  return sh.carry[0];
+}
+
+// KeyPointsFilter::retainBest on one (image, level) per block.  The array and the two
+// position lists live in LDS while the level's count fits (CAP), else in global memory (the
+// same code, on the global array and the scratch lists).  COMPACT: the candidates are first
+// compacted from the FAST tile records (the first retainBest of ORB); otherwise they are
+// read from arr (the Harris retainBest).  The first r elements of the result go back to arr.
+template <class E, int CAP, bool COMPACT>
+__global__ __launch_bounds__(kSelThreads, 4) void k_select(const OrbDev G, const uint8_t* __restrict__ trec, int ntiles,
+                                                        int edge, typename E::T* __restrict__ arr,
+                                                        int32_t* __restrict__ nin, int32_t* __restrict__ nout,
                                                         int32_t* __restrict__ scratch, int64_t scratch_per,
                                                         int64_t cand_total, int nlevels, int keep_mult) {
-  int l = blockIdx.x, b = blockIdx.y;
+  using T = typename E::T;
+  const int b = blockIdx.x, l = blockIdx.y;  // level-major dispatch: the large level-0 blocks start first
   __shared__ SelShared sh;
-  typename E::T* a = arr + b * cand_total + G.cand_off[l];
-  int n = nin[b * nlevels + l];
-  int* SA = scratch + (int64_t)(b * nlevels + l) * scratch_per;
-  int* SB = SA + scratch_per / 2;
-  int r = select_block<E>(sh, a, n, keep_mult * G.nfeat[l], SA, SB);
+  __shared__ T s_a[CAP];
+  __shared__ uint16_t s_pa[CAP], s_pb[CAP];
+  T* a = arr + b * cand_total + G.cand_off[l];
+  int n;
+  if constexpr (COMPACT) {
+    n = compact_level<CAP>(sh, G, trec, ntiles, edge, l, b, a, s_a);
+    if (threadIdx.x == 0) nin[b * nlevels + l] = n;
+  } else {
+    n = nin[b * nlevels + l];
+    if (n <= CAP)
+      for (int i = threadIdx.x; i < n; i += blockDim.x) s_a[i] = a[i];
+  }
+  __syncthreads();
+  const int keep = keep_mult * G.nfeat[l];
+  int r;
+  if (n <= CAP) {
+    r = select_block<E, uint16_t>(sh, s_a, n, keep, s_pa, s_pb);
+    if (r < n || !COMPACT)
+      for (int i = threadIdx.x; i < r; i += blockDim.x) a[i] = s_a[i];
+  } else {
+    int* SA = scratch + (int64_t)(b * nlevels + l) * scratch_per;
+    r = select_block<E, int>(sh, a, n, keep, SA, SA + scratch_per / 2);
+  }
   if (threadIdx.x == 0) nout[b * nlevels + l] = r;
 }
 
@@ -1160,7 +1194,7 @@ int orb_init(fvo_ctx* ctx) {
   ctx->scratch_per = 2 * maxcand;
   // (the full FAST score map, ctx->score, is allocated on first debug request)
   if ((rc = fvo_alloc(ctx, &ctx->pyr, B * g.total_px)) ||
-      (rc = fvo_alloc(ctx, &ctx->rowoff, B * g.total_rows)) || (rc = fvo_alloc(ctx, &ctx->cand, B * g.cand_total)) ||
+      (rc = fvo_alloc(ctx, &ctx->cand, B * g.cand_total)) ||
       (rc = fvo_alloc(ctx, &ctx->hel, B * g.cand_total)) || (rc = fvo_alloc(ctx, &ctx->ncand, B * c.nlevels)) ||
       (rc = fvo_alloc(ctx, &ctx->nsel1, B * c.nlevels)) || (rc = fvo_alloc(ctx, &ctx->nsel2, B * c.nlevels)) ||
       (rc = fvo_alloc(ctx, &ctx->koff, B * (c.nlevels + 1))) ||
@@ -1230,16 +1264,14 @@ int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride
                        ctx->rt.yc1 + ctx->rt.yoff[l]));
   FVO_TIMED(ctx, KN_ORB_FAST, s, hipLaunchKernelGGL(k_fast_nms<false>, dim3(ntiles, batch), dim3(256), 0, s, G, ctx->pyr,
                      nullptr, ctx->fast_rec, total, thr, c.edge_threshold, ntiles));
-  FVO_TIMED(ctx, KN_ORB_ROW_SCAN, s, hipLaunchKernelGGL(k_row_scan, dim3(L, batch), dim3(256), 0, s, G, ctx->fast_rec, ctx->rowoff, ctx->ncand, g.total_rows,
-                     L, ntiles));
-  FVO_TIMED(ctx, KN_ORB_COMPACT, s, hipLaunchKernelGGL(k_keep_compact, dim3(g.total_rows, batch), dim3(64), 0, s, G, ctx->fast_rec,
-                     ctx->rowoff, ctx->cand, g.cand_total, c.edge_threshold, ntiles));
-  FVO_TIMED(ctx, KN_ORB_SELECT1, s, hipLaunchKernelGGL(k_select<ElemFast>, dim3(L, batch), dim3(kSelThreads), 0, s, G, ctx->cand, ctx->ncand, ctx->nsel1,
-                     ctx->scratch, ctx->scratch_per, g.cand_total, L, 2));
+  FVO_TIMED(ctx, KN_ORB_SELECT1, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_select<ElemFast, kSelCap1, true>), dim3(batch, L),
+                     dim3(kSelThreads), 0, s, G, ctx->fast_rec, ntiles, c.edge_threshold, ctx->cand, ctx->ncand,
+                     ctx->nsel1, ctx->scratch, ctx->scratch_per, g.cand_total, L, 2));
   FVO_TIMED(ctx, KN_ORB_HARRIS, s, hipLaunchKernelGGL(k_harris, dim3(32, L, batch), dim3(256), 0, s, G, ctx->pyr, ctx->cand, ctx->nsel1, ctx->hel, total,
                      g.cand_total, L));
-  FVO_TIMED(ctx, KN_ORB_SELECT2, s, hipLaunchKernelGGL(k_select<ElemHarris>, dim3(L, batch), dim3(kSelThreads), 0, s, G, ctx->hel, ctx->nsel1, ctx->nsel2,
-                     ctx->scratch, ctx->scratch_per, g.cand_total, L, 1));
+  FVO_TIMED(ctx, KN_ORB_SELECT2, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_select<ElemHarris, kSelCap2, false>), dim3(batch, L),
+                     dim3(kSelThreads), 0, s, G, nullptr, ntiles, c.edge_threshold, ctx->hel, ctx->nsel1,
+                     ctx->nsel2, ctx->scratch, ctx->scratch_per, g.cand_total, L, 1));
   FVO_TIMED(ctx, KN_ORB_OFFSETS, s, hipLaunchKernelGGL(k_offsets, dim3((batch + 63) / 64), dim3(64), 0, s, ctx->nsel2, ctx->koff, counts, batch, L, cap));
   FVO_TIMED(ctx, KN_ORB_ANGLE, s, hipLaunchKernelGGL(k_angle, dim3(16, L, batch), dim3(256), 0, s, G, ctx->pyr, ctx->hel, ctx->nsel2, ctx->koff, kp,
                      total, g.cand_total, L, cap, c.patch_size));
