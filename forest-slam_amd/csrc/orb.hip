@@ -761,7 +761,9 @@ __global__ __launch_bounds__(kSelThreads, 4) void k_select(const OrbDev G, const
   int r;
   if (n <= CAP) {
     r = select_block<E, uint16_t>(sh, s_a, n, keep, s_pa, s_pb);
-    if (r < n || !COMPACT)
+    // the selection permutes the array whenever it runs (n > keep), even when ties keep all
+    // n; only an untouched compacted array is already in place
+    if (n > keep || !COMPACT)
       for (int i = threadIdx.x; i < r; i += blockDim.x) a[i] = s_a[i];
   } else {
     int* SA = scratch + (int64_t)(b * nlevels + l) * scratch_per;
@@ -986,10 +988,10 @@ __global__ __launch_bounds__(256) void k_blur(const OrbDev G, const uint8_t* __r
 constexpr int kBrR = 19, kBrP = 2 * kBrR + 1, kBrS = kBrP + 6;  // sample radius, blurred / source side
 constexpr int kBrSW = kBrS + 3, kBrPW = kBrP + 1;                // LDS row pitches
 
-__global__ __launch_bounds__(256) void k_brief(const OrbDev G, const uint8_t* __restrict__ pyr,
+__global__ __launch_bounds__(256, 4) void k_brief(const OrbDev G, const uint8_t* __restrict__ pyr,
                                                const float* __restrict__ kp, const int32_t* __restrict__ counts,
                                                uint8_t* __restrict__ desc, int64_t total, int cap) {
-  __shared__ uint8_t s_src[4][kBrS][kBrSW];
+  __shared__ __attribute__((aligned(16))) uint8_t s_src[4][kBrS][kBrSW];
   __shared__ uint8_t s_blr[4][kBrP][kBrPW];
   const XcdBlock xb = xcd_block();  // one image's blocks on one XCD: overlapping patches in one L2
   const int b = xb.y;
@@ -1009,45 +1011,63 @@ __global__ __launch_bounds__(256) void k_brief(const OrbDev G, const uint8_t* __
     const int w = G.w[l], h = G.h[l];
     const uint8_t* im = pyr + b * total + G.off[l];
     const int sx0 = cx - kBrR - 3, sy0 = cy - kBrR - 3;
-    // the 45 x 45 patch in two batches of 16 unconditional byte loads per lane (the tail
-    // slots re-read the last byte and are not stored), each batch in flight together
-    constexpr int kBrN = kBrS * kBrS, kBrIt = (kBrN + 63) / 64;
+    if (sx0 >= 0 && sy0 >= 0 && sx0 + kBrS <= w && sy0 + kBrS <= h) {
+      // the usual case (keypoints lie edgeThreshold >= 31 px inside their level, the patch
+      // reaches 22): no border handling, each row's 48 bytes as 12 dwords from aligned loads
+      // (v_alignbyte), all 9 of a lane's loads in flight together
+      constexpr int kRW = kBrSW / 4, kN = kBrS * kRW, kIt = (kN + 63) / 64;
+      const uint8_t* p0 = im + (int64_t)sy0 * w + sx0;
 #pragma unroll
-    for (int i0 = 0; i0 < kBrIt; i0 += 16) {
-      uint32_t pv[16];
-#pragma unroll
-      for (int k2 = 0; k2 < 16; ++k2) {
-        const int i = min(lane + 64 * (i0 + k2), kBrN - 1);
+      for (int t = 0; t < kIt; ++t) {
+        const int i = min(lane + 64 * t, kN - 1);
+        const int r = i / kRW, q = i - r * kRW;
+        const uintptr_t pa = reinterpret_cast<uintptr_t>(p0 + r * w + 4 * q);
+        const uint32_t* a4 = reinterpret_cast<const uint32_t*>(pa & ~(uintptr_t)3);
+        const uint32_t v = __builtin_amdgcn_alignbyte(a4[1], a4[0], (uint32_t)pa & 3u);
+        if (lane + 64 * t < kN) reinterpret_cast<uint32_t*>(&src[r][0])[q] = v;
+      }
+    } else {
+      // a patch crossing the level's border (REFLECT_101 per byte): not reached by keypoints
+      // of the default edgeThreshold, kept small in registers
+      constexpr int kBrN = kBrS * kBrS;
+#pragma unroll 1
+      for (int i = lane; i < kBrN; i += 64) {
         const int r = i / kBrS, c = i - r * kBrS;
         const int y = reflect101(min(sy0 + r, 2 * (h - 1)), h);
         const int x = reflect101(min(sx0 + c, 2 * (w - 1)), w);
-        pv[k2] = im[(int64_t)y * w + x];
-      }
-#pragma unroll
-      for (int k2 = 0; k2 < 16; ++k2) {
-        const int i = lane + 64 * (i0 + k2);
-        if (i0 + k2 < kBrIt && i < kBrN) (&src[0][0])[(i / kBrS) * kBrSW + i % kBrS] = (uint8_t)pv[k2];
+        src[r][c] = im[(int64_t)y * w + x];
       }
     }
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
     if (lane < kBrP) {
       const int c = lane;
+      // vertical 7 taps from a 7-row ring: rows in groups of 7 (ring slot = row % 7, static
+      // inside the unrolled group), the group loop itself not unrolled
       int win[7] = {0, 0, 0, 0, 0, 0, 0};
+      const uint32_t sh = (uint32_t)c & 3u;
+#pragma unroll 1
+      for (int r0 = 0; r0 < kBrS; r0 += 7) {
 #pragma unroll
-      for (int r = 0; r < kBrS; ++r) {
-        int hs = 0;
+        for (int t = 0; t < 7; ++t) {
+          const int r = r0 + t;
+          if (r < kBrS) {
+            // horizontal 7 taps: bytes c..c+6 from three dwords, two v_dot4_u32_u8 with the
+            // kernel's bytes (integer sums: exact, any order)
+            const uint32_t* rw = reinterpret_cast<const uint32_t*>(&src[r][0]) + (c >> 2);
+            const uint32_t d0 = rw[0], d1 = rw[1], d2 = rw[2];
+            win[t] = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, sh), 0x00122231u,
+                                                 __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, sh),
+                                                                        0x37312212u, 0u, false),
+                                                 false);
+            if (r >= 6) {
+              int sv = 0;
 #pragma unroll
-        for (int t = 0; t < 7; ++t) hs += c_gk[t] * src[r][c + t];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) win[q] = win[q + 1];
-        win[6] = hs;
-        if (r >= 6) {
-          int sv = 0;
-#pragma unroll
-          for (int q = 0; q < 7; ++q) sv += c_gk[q] * win[q];
-          const int v = (sv + 32767 + ((sv >> 16) & 1)) >> 16;  // round half to even, as k_blur
-          blr[r - 6][c] = (uint8_t)min(v, 255);
+              for (int q = 0; q < 7; ++q) sv += c_gk[q] * win[(t + 1 + q) % 7];  // rows r-6 .. r
+              const int v = (sv + 32767 + ((sv >> 16) & 1)) >> 16;  // round half to even, as k_blur
+              blr[r - 6][c] = (uint8_t)min(v, 255);
+            }
+          }
         }
       }
     }

@@ -94,6 +94,32 @@ def test_orb_bit_exact(oracle_mod, frames, nfeatures):
         assert np.array_equal(desc, rdesc)
 
 
+def test_orb_bit_exact_tied_selection(oracle_mod):
+    """Undistorted frames (black borders, few corners) at nfeatures 500: at the upper levels
+    the first retainBest runs (n > 2 n_l) but the score ties at its threshold keep all n, so
+    the selection permutes the array without shrinking it -- the result must still be
+    OpenCV's order (a permuted-but-full selection was once not written back)."""
+    import forest_slam_amd.synth as synth
+    from forest_slam_amd import _lib
+    from forest_slam_amd import pipeline as pl
+    seq = synth.StereoSequence(seed=9, n_frames=2, W=960, H=600, device="cpu", start=200)
+    imgs = []
+    for i in range(2):
+        L = seq.frame(i)[0].numpy()
+        imgs.append(oracle_mod.undistort_gray(np.stack([L, L, 255 - L], axis=2), pl.K0, pl.DIST_L))
+    ctx = _lib.Context(960, 600, max_batch=2, nfeatures=500)
+    got, _ = _orb_gpu(ctx, imgs)
+    ncand = ctx.debug_buffer(3).view(torch.int32).view(2, -1).numpy()
+    nsel1 = ctx.debug_buffer(4).view(torch.int32).view(2, -1).numpy()
+    nsel2 = ctx.debug_buffer(5).view(torch.int32).view(2, -1).numpy()
+    assert ((ncand > 2 * nsel2) & (nsel1 == ncand)).any()  # the tied-full case occurs
+    for img, (kp, desc) in zip(imgs, got):
+        rkp, rdesc = oracle_mod.orb_detect_compute(img, 500)
+        assert kp.shape[0] == rkp.shape[0]
+        assert np.array_equal(kp[:, :6], rkp), np.argwhere(kp[:, :6] != rkp)[:5]
+        assert np.array_equal(desc, rdesc)
+
+
 def test_bf_match_bit_exact(oracle_mod, frames):
     from forest_slam_amd import _lib
     ctx = _lib.Context(960, 600, max_batch=3, nfeatures=1000)
