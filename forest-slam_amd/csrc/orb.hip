@@ -170,7 +170,8 @@ __constant__ int c_cdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2
 // full-level score map and no scattered per-row keep words or counters cross HBM (the row
 // counts are popcounts of the records' words, taken by k_row_scan; the score map itself is
 // produced only on request, by the SCOREMAP instance, for the debug hook).
-constexpr int kTW = 64, kTH = 32;
+constexpr int kTW = 64, kTH = 32, kFT = 256;  // tile, threads per tile block
+static_assert(kTH <= 64 && kFT >= 2 * kTH && kFT % 64 == 0, "FAST tile shape");
 constexpr int kRecKeep = 0, kRecPre = 8 * kTH, kRecSc = kRecPre + 2 * kTH;  // byte offsets in a record
 constexpr int kTRec = kRecSc + kTH * kTW / 2;  // + <= 1024 kept scores
 
@@ -220,7 +221,7 @@ __device__ __forceinline__ int tile_level(const OrbDev& G, int t) {
 }
 
 template <bool SCOREMAP>
-__global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t* __restrict__ pyr,
+__global__ __launch_bounds__(kFT) void k_fast_nms(const OrbDev G, const uint8_t* __restrict__ pyr,
                                                   uint8_t* __restrict__ score, uint8_t* __restrict__ trec,
                                                   int64_t total, int thr, int edge, int ntiles) {
   __shared__ __attribute__((aligned(16))) uint8_t s_img[kIH][kIW];
@@ -243,7 +244,7 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   if (x0 >= 8 && x0 + kTW + 12 <= w && y0 >= 4 && y0 + kTH + 4 <= h) {
     // interior tile: the staged rows and the aligned dwords around them lie inside the level
     // row, so a row's 76 bytes come from 20 aligned dwords, byte-aligned by v_alignbyte
-    for (int i = threadIdx.x; i < kIH * (kIW / 4); i += 256) {
+    for (int i = threadIdx.x; i < kIH * (kIW / 4); i += kFT) {
       const int r = i / (kIW / 4), k = i % (kIW / 4);
       const uint8_t* p = im + (int64_t)(y0 - 4 + r) * w + x0 - 1 - kIC + 4 * k;
       const uint32_t* a = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
@@ -251,13 +252,13 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
       *reinterpret_cast<uint32_t*>(&s_img[r][4 * k]) = __builtin_amdgcn_alignbyte(a[1], a[0], sh);
     }
   } else {
-    for (int i = threadIdx.x; i < kIH * kIW; i += 256) {
+    for (int i = threadIdx.x; i < kIH * kIW; i += kFT) {
       const int r = i / kIW, c = i % kIW;
       const int y = min(max(y0 - 4 + r, 0), h - 1), x = min(max(x0 - 1 - kIC + c, 0), w - 1);
       s_img[r][c] = im[(int64_t)y * w + x];
     }
   }
-  for (int i = threadIdx.x; i < kFH * kFW / 4; i += 256) reinterpret_cast<uint32_t*>(&s_sc[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < kFH * kFW / 4; i += kFT) reinterpret_cast<uint32_t*>(&s_sc[0][0])[i] = 0;
   if (threadIdx.x < 2 * kTH) (&s_m[0][0])[threadIdx.x] = 0u;
   if (threadIdx.x == 0) { s_n = 0; s_npre = 0; }
   __syncthreads();
@@ -269,7 +270,7 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   // subtracts).  (2) The full 16-pixel test on the pre-list; corners go to the list.  Same
   // corners as testing every position.
   const u16x2 tt = {(unsigned short)thr, (unsigned short)thr};
-  for (int i0 = 0; i0 < kFH * kPG; i0 += 256) {  // uniform trip count: ballots see whole waves
+  for (int i0 = 0; i0 < kFH * kPG; i0 += kFT) {  // uniform trip count: ballots see whole waves
     const int i = i0 + threadIdx.x;
     const int r = i / kPG, g = i % kPG;
     const int y = y0 - 1 + r, xg = x0 - 1 + 4 * g;
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   }
   __syncthreads();
   const int npre = s_npre;
-  for (int j0 = 0; j0 < npre; j0 += 256) {  // uniform trip count
+  for (int j0 = 0; j0 < npre; j0 += kFT) {  // uniform trip count
     const int j = j0 + threadIdx.x;
     bool corner = false;
     int i = 0;
@@ -341,7 +342,7 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   __syncthreads();
   // cornerScore<16>: max(t, max over 9-arcs of min(v-p), max over 9-arcs of min(p-v)) - 1
   const int nc = s_n;
-  for (int j = threadIdx.x; j < nc; j += 256) {
+  for (int j = threadIdx.x; j < nc; j += kFT) {
     const int i = s_list[j];
     const int r = i / kFW, c = i % kFW;
     const int v = s_img[r + 3][c + kIC];
@@ -373,7 +374,7 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   __syncthreads();
   if (SCOREMAP) {  // debug hook: the score of every tile pixel (0 = no corner)
     const int c = threadIdx.x & 63, x = x0 + c;
-    for (int rr = threadIdx.x >> 6; rr < kTH; rr += 4) {
+    for (int rr = threadIdx.x >> 6; rr < kTH; rr += kFT / 64) {
       const int y = y0 + rr;
       if (y < h && x < w) score[b * total + G.off[l] + (int64_t)y * w + x] = s_sc[rr + 1][c + 1];
     }
@@ -381,7 +382,7 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
   }
   // strict 3x3 NMS + border filter, on the corners only (every other pixel scores 0): a kept
   // corner sets its bit in its row's keep word and is marked in the list
-  for (int j = threadIdx.x; j < nc; j += 256) {
+  for (int j = threadIdx.x; j < nc; j += kFT) {
     const int i = s_list[j];
     const int r = i / kFW, c = i % kFW;
     const int x = x0 - 1 + c, y = y0 - 1 + r;
@@ -401,7 +402,7 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
     const int v = c < kTH ? __popc(s_m[c][0]) + __popc(s_m[c][1]) : 0;
     int inc = v;
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
+    for (int o = 1; o < kTH; o <<= 1) {
       const int u = __shfl_up(inc, o, 64);
       if (c >= o) inc += u;
     }
@@ -414,7 +415,7 @@ __global__ __launch_bounds__(256) void k_fast_nms(const OrbDev G, const uint8_t*
         (unsigned long long)s_m[threadIdx.x][0] | (unsigned long long)s_m[threadIdx.x][1] << 32;
   else if (threadIdx.x < 2 * kTH)
     reinterpret_cast<uint16_t*>(rec + kRecPre)[threadIdx.x - kTH] = (uint16_t)s_rp[threadIdx.x - kTH];
-  for (int j = threadIdx.x; j < nc; j += 256) {
+  for (int j = threadIdx.x; j < nc; j += kFT) {
     const int e = s_list[j];
     if (!(e & 0x8000)) continue;
     const int i = e & 0x7FFF;
@@ -1282,7 +1283,7 @@ int orb_run(fvo_ctx* ctx, const uint8_t* images, int batch, int64_t image_stride
     FVO_TIMED(ctx, KN_ORB_RESIZE, s, hipLaunchKernelGGL(k_resize, dim3((g.w[l] + 256 * kResCols - 1) / (256 * kResCols), (g.h[l] + kResRows - 1) / kResRows, batch), dim3(256), 0, s, G, ctx->pyr, total, l,
                        ctx->rt.xofs + ctx->rt.xoff[l], ctx->rt.xc1 + ctx->rt.xoff[l], ctx->rt.yofs + ctx->rt.yoff[l],
                        ctx->rt.yc1 + ctx->rt.yoff[l]));
-  FVO_TIMED(ctx, KN_ORB_FAST, s, hipLaunchKernelGGL(k_fast_nms<false>, dim3(ntiles, batch), dim3(256), 0, s, G, ctx->pyr,
+  FVO_TIMED(ctx, KN_ORB_FAST, s, hipLaunchKernelGGL(k_fast_nms<false>, dim3(ntiles, batch), dim3(kFT), 0, s, G, ctx->pyr,
                      nullptr, ctx->fast_rec, total, thr, c.edge_threshold, ntiles));
   FVO_TIMED(ctx, KN_ORB_SELECT1, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_select<ElemFast, kSelCap1, true>), dim3(batch, L),
                      dim3(kSelThreads), 0, s, G, ctx->fast_rec, ntiles, c.edge_threshold, ctx->cand, ctx->ncand,
@@ -1332,7 +1333,7 @@ int orb_score_debug(fvo_ctx* ctx) {
   if (ctx->orb_last_batch > 0) {
     const OrbDev G = make_dev(g);
     const int ntiles = G.tile0[g.nlevels];
-    hipLaunchKernelGGL(k_fast_nms<true>, dim3(ntiles, ctx->orb_last_batch), dim3(256), 0, 0, G, ctx->pyr, ctx->score,
+    hipLaunchKernelGGL(k_fast_nms<true>, dim3(ntiles, ctx->orb_last_batch), dim3(kFT), 0, 0, G, ctx->pyr, ctx->score,
                        nullptr, g.total_px, std::min(std::max(ctx->cfg.fast_threshold, 0), 255),
                        ctx->cfg.edge_threshold, ntiles);  // the threshold orb_run uses
     FVO_LAUNCH_CHECK(ctx);
