@@ -280,7 +280,7 @@ __device__ __forceinline__ void derive16(const uint32_t* vp, const uint32_t* v, 
 // row's image bytes are loaded right after the current row is staged and taken before the
 // row's C / V stores (vmcnt retires in order: a wait for them behind the stores would also
 // wait for the stores).  Integer arithmetic as oracle/sgbm_ref.cpp (order-independent sums).
-// The left->right path (LP = true, the default schedule): the block also runs the L path of
+// The left->right path (LP = true, FVO_SG_MODE=lpath; classic is the default): the block also runs the L path of
 // its CB columns -- per group of 4 output rows, one wave (16 lanes per row, D/16 disparities
 // per lane) steps the 4 rows across the columns over C read back from a 4-row LDS ring, starting
 // from the state the block of the previous column range handed over for those rows, stores the
