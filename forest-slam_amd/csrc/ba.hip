@@ -924,6 +924,52 @@ __device__ __forceinline__ void lin_tile(int k, int ntu, int NT, int& I, int& J)
 // (starts before its arithmetic, the observation record before its MFMA phase), so its
 // arithmetic starts from registers.
 // MAXT: 16x16 tiles per wave (1 at NR = 64: 10 tiles over 16 waves; 3 at NR = 128: 36 tiles)
+// Sum / OR of a value over an aligned group of GL lanes (2 <= GL <= 32, a power of two), every
+// lane receiving the same result: within a DPP row by quad permutes (xor 1, xor 2), the half-row
+// mirror and the row mirror (each pairs lanes whose partial sums are equal, so both ends of a
+// pair add the same two values: bit-identical results in every lane), across the two rows of
+// 32 lanes by one ds_swizzle (xor 16) -- no LDS round trips for the first four steps.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+__device__ __forceinline__ double swz16_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)u, 0x401F);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(u >> 32), 0x401F);
+  return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+template <int GL, int N>
+__device__ __forceinline__ void group_sum_or(double (&v)[N], uint32_t& fm) {
+  static_assert(GL >= 2 && GL <= 32 && (GL & (GL - 1)) == 0, "group of 2..32 lanes");
+#pragma unroll
+  for (int q = 0; q < N; ++q) v[q] += dpp_f64<0xB1>(v[q]);  // quad_perm [1,0,3,2]
+  fm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fm, 0xB1, 0xF, 0xF, false);
+  if constexpr (GL >= 4) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] += dpp_f64<0x4E>(v[q]);  // quad_perm [2,3,0,1]
+    fm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fm, 0x4E, 0xF, 0xF, false);
+  }
+  if constexpr (GL >= 8) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] += dpp_f64<0x141>(v[q]);  // row_half_mirror
+    fm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fm, 0x141, 0xF, 0xF, false);
+  }
+  if constexpr (GL >= 16) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] += dpp_f64<0x140>(v[q]);  // row_mirror
+    fm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fm, 0x140, 0xF, 0xF, false);
+  }
+  if constexpr (GL >= 32) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] += swz16_f64(v[q]);
+    fm |= (uint32_t)__builtin_amdgcn_ds_swizzle((int)fm, 0x401F);
+  }
+}
+
 template <int MAXT>
 __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm, BaCam cam) {
   extern __shared__ double sY[];  // [3 LPC][NR + 2]
@@ -1001,11 +1047,14 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
       }
     }
     uint32_t fm = has && f > 0 ? 1u << f : 0u;  // frames with pose columns that see the landmark
-    for (int m = GL >> 1; m >= 1; m >>= 1) {
+    if (GL == 32) group_sum_or<32>(hg, fm);
+    else if (GL == 16) group_sum_or<16>(hg, fm);
+    else
+      for (int m = GL >> 1; m >= 1; m >>= 1) {
 #pragma unroll
-      for (int q = 0; q < 9; ++q) hg[q] += __shfl_xor(hg[q], m, 64);
-      fm |= (uint32_t)__shfl_xor((int)fm, m, 64);
-    }
+        for (int q = 0; q < 9; ++q) hg[q] += __shfl_xor(hg[q], m, 64);
+        fm |= (uint32_t)__shfl_xor((int)fm, m, 64);
+      }
     const double* H = hg;
     const double a00 = H[0] + lam * H[0] + 1e-6, a11 = H[3] + lam * H[3] + 1e-6, a22 = H[5] + lam * H[5] + 1e-6;
     const double i00 = rsq_r(a00), l00 = a00 * i00;
