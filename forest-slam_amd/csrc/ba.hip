@@ -942,32 +942,27 @@ __device__ __forceinline__ double swz16_f64(double v) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(u >> 32), 0x401F);
   return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
 }
+template <int GL>
+__device__ __forceinline__ double group_sum(double v) {
+  static_assert(GL >= 2 && GL <= 32 && (GL & (GL - 1)) == 0, "group of 2..32 lanes");
+  v += dpp_f64<0xB1>(v);                         // quad_perm [1,0,3,2]
+  if constexpr (GL >= 4) v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  if constexpr (GL >= 8) v += dpp_f64<0x141>(v);  // row_half_mirror
+  if constexpr (GL >= 16) v += dpp_f64<0x140>(v); // row_mirror
+  if constexpr (GL >= 32) v += swz16_f64(v);      // xor 16
+  return v;
+}
 template <int GL, int N>
 __device__ __forceinline__ void group_sum_or(double (&v)[N], uint32_t& fm) {
-  static_assert(GL >= 2 && GL <= 32 && (GL & (GL - 1)) == 0, "group of 2..32 lanes");
+  // one value at a time through all its steps (few live temporaries: the kernel is at its
+  // register budget)
 #pragma unroll
-  for (int q = 0; q < N; ++q) v[q] += dpp_f64<0xB1>(v[q]);  // quad_perm [1,0,3,2]
+  for (int q = 0; q < N; ++q) v[q] = group_sum<GL>(v[q]);
   fm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fm, 0xB1, 0xF, 0xF, false);
-  if constexpr (GL >= 4) {
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] += dpp_f64<0x4E>(v[q]);  // quad_perm [2,3,0,1]
-    fm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fm, 0x4E, 0xF, 0xF, false);
-  }
-  if constexpr (GL >= 8) {
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] += dpp_f64<0x141>(v[q]);  // row_half_mirror
-    fm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fm, 0x141, 0xF, 0xF, false);
-  }
-  if constexpr (GL >= 16) {
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] += dpp_f64<0x140>(v[q]);  // row_mirror
-    fm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fm, 0x140, 0xF, 0xF, false);
-  }
-  if constexpr (GL >= 32) {
-#pragma unroll
-    for (int q = 0; q < N; ++q) v[q] += swz16_f64(v[q]);
-    fm |= (uint32_t)__builtin_amdgcn_ds_swizzle((int)fm, 0x401F);
-  }
+  if constexpr (GL >= 4) fm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fm, 0x4E, 0xF, 0xF, false);
+  if constexpr (GL >= 8) fm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fm, 0x141, 0xF, 0xF, false);
+  if constexpr (GL >= 16) fm |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fm, 0x140, 0xF, 0xF, false);
+  if constexpr (GL >= 32) fm |= (uint32_t)__builtin_amdgcn_ds_swizzle((int)fm, 0x401F);
 }
 
 template <int MAXT>
@@ -1131,16 +1126,28 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
       const double* yb = sY + (lane >> 4) * NRP + 16 * J + (lane & 15);
       uint64_t m = __ballot(((actl >> I) & 1u) && (((actl >> J) & 1u) || J == NT - 1));
       if (!m) continue;
+      // operands loaded two active steps ahead of the MFMA that uses them (the phase waits on
+      // its LDS loads, not on the matrix core); the steps still ascend into one accumulator
       int g = __builtin_ctzll(m);
-      double av = ya[4 * g * NRP], bv = yb[4 * g * NRP];
-      for (m &= m - 1; m; m &= m - 1) {
+      m &= m - 1;
+      double a0 = ya[4 * g * NRP], b0 = yb[4 * g * NRP];
+      bool h1 = m != 0;
+      if (h1) {
         g = __builtin_ctzll(m);
-        const double an = ya[4 * g * NRP], bn = yb[4 * g * NRP];
-        acc[lt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[lt], 0, 0, 0);
-        av = an;
-        bv = bn;
+        m &= m - 1;
       }
-      acc[lt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[lt], 0, 0, 0);
+      double a1 = ya[4 * g * NRP], b1 = yb[4 * g * NRP];
+      while (h1) {
+        const bool h2 = m != 0;
+        if (h2) {
+          g = __builtin_ctzll(m);
+          m &= m - 1;
+        }
+        const double a2 = ya[4 * g * NRP], b2 = yb[4 * g * NRP];
+        acc[lt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[lt], 0, 0, 0);
+        a0 = a1, b0 = b1, a1 = a2, b1 = b2, h1 = h2;
+      }
+      acc[lt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[lt], 0, 0, 0);
     }
     __syncthreads();  // sY / s_tm are rewritten by the next chunk
   }
