@@ -356,11 +356,15 @@ def test_sgbm_variants_bit_exact(frames, sgbm_ref, monkeypatch, mode, g, cb):
         assert len(bad) == 0, f"pair {i}: {len(bad)} px differ, first {bad[:5]}"
 
 
+@pytest.mark.parametrize("mode", ["classic", "lpath"])
 @pytest.mark.parametrize("W,H,nd", [(333, 217, 64), (200, 120, 96), (1024, 100, 128), (500, 77, 96)])
-def test_sgbm_ragged_geometries_bit_exact(oracle_mod, W, H, nd):
+def test_sgbm_ragged_geometries_bit_exact(oracle_mod, monkeypatch, W, H, nd, mode):
     """Image widths that leave a partial 16-column chunk / 8-column segment and heights that
-    leave a partial 16-row band (the row kernel's edge cases), every supported D."""
+    leave a partial 16-row band (the row kernel's edge cases), every supported D; under the
+    L-path schedule also a partial last column block (W - D not a multiple of its 32 columns)
+    and its hand-off chain across column blocks."""
     from forest_slam_amd import _lib
+    monkeypatch.setenv("FVO_SG_MODE", mode)
     rng = np.random.default_rng(W * 7 + H)
     import forest_slam_amd.synth as synth
     seq = synth.StereoSequence(seed=W % 13, n_frames=1, W=W, H=H, device="cpu")
