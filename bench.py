@@ -317,9 +317,13 @@ def exchange_fields(world: int, rank0_only: bool, send_bytes: int, stream_ms, co
         return {"mode": "off (one rank: no exchange)", "send_bytes_per_rank_per_step": 0,
                 "recv_bytes_per_rank_per_step": 0, "stream_ms_per_step": None, "collective_ms_per_step": None,
                 "host_ms_per_step": None, "steps_timed": 0}
+    # bytes over the link: a rank's own slice of the gathered result never leaves it
     return {"mode": ("gather to rank 0, map on rank 0 only" if rank0_only
                      else "all-gather, every rank places the whole map"),
-            "send_bytes_per_rank_per_step": send_bytes, "recv_bytes_per_rank_per_step": send_bytes * world,
+            "send_bytes_per_rank_per_step": send_bytes, "recv_bytes_per_rank_per_step": send_bytes * (world - 1),
+            "gathered_bytes_per_step": send_bytes * world,
+            "padding": "points3D travel at the context's keypoint capacity (fixed-shape collective, device-side "
+                       "counts, no host sync; DESIGN.md section 6)",
             "stream_ms_per_step": None if stream_ms is None else round(stream_ms, 4),
             "collective_ms_per_step": None if collective_ms is None else round(collective_ms, 4),
             "host_ms_per_step": None if host_ms is None else round(host_ms, 4), "steps_timed": steps}
@@ -521,6 +525,8 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=6, help="CPU baseline 1-thread sample, frames (0 = skip)")
     ap.add_argument("--cpu-ate", type=int, default=1, help="ATE of the CPU reference path on the ATE frames")
     ap.add_argument("--overlap-sgbm", type=int, default=1, help="SGBM of step k+1 on a side stream during step k")
+    ap.add_argument("--sgbm-mode", choices=("classic", "lpath"), default="classic",
+                    help="SGBM schedule (fvo_config.sgbm_mode): classic, or the L path inside the cost pass")
     ap.add_argument("--ba-max-landmarks", type=int, default=0, help="per-window landmark cap (0 = library default)")
     ap.add_argument("--ba-max-obs", type=int, default=0, help="per-window observation cap (0 = library default)")
     ap.add_argument("--shard", choices=("sequences", "frames"), default="sequences",
@@ -555,8 +561,11 @@ def main():
     L_all, R_all = seq.frames(range(B + 1))
     torch.cuda.synchronize()
     ba_caps = {k: v for k, v in (("ba_max_landmarks", args.ba_max_landmarks), ("ba_max_obs", args.ba_max_obs)) if v}
+    from forest_slam_amd import _lib
+    sg_mode = _lib.SGBM_LPATH if args.sgbm_mode == "lpath" else _lib.SGBM_CLASSIC
     fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=B, nfeatures=args.nfeatures, device=dev,
-                           ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm), **ba_caps)
+                           ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm), sgbm_mode=sg_mode,
+                           **ba_caps)
     fe.prime(L_all[0], R_all[0])
     # Steps walk the rendered frames forward (1..B) then backward (B-1..0) and so on, so every
     # frame pair the front end sees -- including the carried pair across a step boundary -- is
@@ -613,11 +622,16 @@ def main():
     dom_t = fe.ctx.timing_read()
     fe.ctx.timing_enable([])
     elapsed = rk.max_elapsed(elapsed)
+    # SGBM hand-off timeouts over the context's life (control word 2; only the L-path schedule
+    # can have any: its pairs then carry STATUS_SGBM_FAILED)
+    sg_timeouts = int(fe.ctx.debug_buffer(9).view(torch.int32)[2].item())
     xs = rank_step.exchange_stats()
     rank_step.timing(False)
     exchange = exchange_fields(world, bool(args.map_rank0), xs["send_bytes_per_rank_per_step"] if xs else 0,
                                xs.get("stream_ms_per_step") if xs else None, xs.get("collective_ms_per_step") if xs else None,
                                xs.get("host_ms_per_step") if xs else None, xs["steps_timed"] if xs else 0)
+    if xs:
+        exchange["useful_send_bytes_last_step"] = xs["useful_send_bytes_last_step"]
 
     global_map = None
     if rank_step.gmap is not None:
@@ -740,6 +754,7 @@ def main():
             "global_map": global_map,
             "exchange": exchange,
             "stages_ms_per_step": stage_ms,
+            "sgbm": {"mode": args.sgbm_mode, "handoff_timeouts": sg_timeouts},
             "workspace_gb": round(fe.ctx.workspace_bytes / 1e9, 2),
         }
         out.update(rk.fields())

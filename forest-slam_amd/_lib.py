@@ -28,7 +28,7 @@ class FvoConfig(ctypes.Structure):
             "nlevels", "edge_threshold", "first_level", "wta_k", "score_type", "patch_size", "fast_threshold",
             "min_disparity", "num_disparities", "block_size", "P1", "P2", "disp12_max_diff", "pre_filter_cap",
             "uniqueness_ratio", "sgbm_stripes", "kp_capacity", "stages", "ba_window", "ba_max_landmarks",
-            "ba_max_obs", "sgbm_max_batch")]
+            "ba_max_obs", "sgbm_max_batch", "sgbm_mode", "sgbm_lanes", "sgbm_cols", "sgbm_handoff_us")]
 
 
 class FvoRegion(ctypes.Structure):
@@ -37,8 +37,10 @@ class FvoRegion(ctypes.Structure):
 
 
 FVO_MAX_REGIONS = 32
-ABI_VERSION = 6  # FVO_ABI_VERSION of include/fvo.h
+ABI_VERSION = 7  # FVO_ABI_VERSION of include/fvo.h
 STAGE_ORB, STAGE_BF, STAGE_SGBM, STAGE_POSE, STAGE_BA, STAGE_MONO = 1, 2, 4, 8, 16, 32
+SGBM_CLASSIC, SGBM_LPATH = 0, 1  # fvo_config.sgbm_mode
+SGBM_OK, SGBM_HANDOFF_TIMEOUT = 0, -1  # fvo_sgbm status values
 
 # name -> (restype, argtypes); mirrors include/fvo.h
 _P = ctypes.c_void_p
@@ -56,7 +58,7 @@ SIGNATURES = {
     "fvo_workspace_bytes": (ctypes.c_int64, [_P]),
     "fvo_orb_detect_compute": (ctypes.c_int, [_P, _P, _I, _L, _I, _P, _P, _P, _I, _P]),
     "fvo_bf_match": (ctypes.c_int, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
-    "fvo_sgbm": (ctypes.c_int, [_P, _P, _P, _I, _L, _I, _P, _P]),
+    "fvo_sgbm": (ctypes.c_int, [_P, _P, _P, _I, _L, _I, _P, _P, _P]),
     "fvo_backproject": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, _P, ctypes.c_double, _P, _P, _P, _P]),
     "fvo_pnp_ransac": (ctypes.c_int, [_P, _P, _P, _P, _I, _I, _P, _P, ctypes.c_float, ctypes.c_double, _I, _P, _P,
                                       _P, _P, _P, _P]),
@@ -241,14 +243,19 @@ class Context:
                                         cap, _ptr(m), _ptr(nm), _stream(self.device)))
         return m, nm
 
-    def sgbm(self, left, right, out=None):
+    def sgbm(self, left, right, out=None, status=None):
+        """StereoSGBM 3-way + medianBlur(3) of u8 [B,H,W] pairs -> int16 [B,H,W] disparity*16.
+        status: optional int32 [B] device tensor, written SGBM_OK / SGBM_HANDOFF_TIMEOUT."""
         if left.dim() == 2:
             left, right = left[None], right[None]
         left, right = left.contiguous(), right.contiguous()
         B, H, W = left.shape
         if out is None:
             out = torch.empty((B, H, W), dtype=torch.int16, device=self.device)
-        self._check(self.L.fvo_sgbm(self.h, _ptr(left), _ptr(right), B, H * W, W, _ptr(out), _stream(self.device)))
+        if status is not None and (status.dtype != torch.int32 or status.numel() < B or not status.is_contiguous()):
+            raise TypeError("status must be a contiguous int32 tensor of >= batch entries")
+        self._check(self.L.fvo_sgbm(self.h, _ptr(left), _ptr(right), B, H * W, W, _ptr(out), _ptr(status),
+                                    _stream(self.device)))
         return out
 
     def backproject(self, disp, kp0, kp1, matches, nmatch, K, baseline, out=None):

@@ -22,9 +22,10 @@ hipEvent_t fvo_event(fvo_ctx* ctx) {
   return e;
 }
 
-// The ABI layout: 26 int32 / float fields + sgbm_max_batch, no padding (include/fvo.h).
-static_assert(sizeof(fvo_config) == 27 * 4, "fvo_config layout changed: bump FVO_ABI_VERSION");
-static_assert(offsetof(fvo_config, scale_factor) == 16 && offsetof(fvo_config, sgbm_max_batch) == 104,
+// The ABI layout: 31 int32 / float fields, no padding (include/fvo.h).
+static_assert(sizeof(fvo_config) == 31 * 4, "fvo_config layout changed: bump FVO_ABI_VERSION");
+static_assert(offsetof(fvo_config, scale_factor) == 16 && offsetof(fvo_config, sgbm_max_batch) == 104 &&
+                  offsetof(fvo_config, sgbm_handoff_us) == 120,
               "fvo_config field offsets changed: bump FVO_ABI_VERSION");
 
 extern "C" {
@@ -41,7 +42,7 @@ int32_t fvo_config_offset(const char* f) {
   FVO_OFS(fast_threshold) FVO_OFS(min_disparity) FVO_OFS(num_disparities) FVO_OFS(block_size) FVO_OFS(P1)
   FVO_OFS(P2) FVO_OFS(disp12_max_diff) FVO_OFS(pre_filter_cap) FVO_OFS(uniqueness_ratio) FVO_OFS(sgbm_stripes)
   FVO_OFS(kp_capacity) FVO_OFS(stages) FVO_OFS(ba_window) FVO_OFS(ba_max_landmarks) FVO_OFS(ba_max_obs)
-  FVO_OFS(sgbm_max_batch)
+  FVO_OFS(sgbm_max_batch) FVO_OFS(sgbm_mode) FVO_OFS(sgbm_lanes) FVO_OFS(sgbm_cols) FVO_OFS(sgbm_handoff_us)
 #undef FVO_OFS
   return -1;
 }
@@ -75,6 +76,10 @@ void fvo_config_default(fvo_config* c, int32_t width, int32_t height) {
   c->ba_max_landmarks = 4096;
   c->ba_max_obs = 32768;
   c->sgbm_max_batch = 0;
+  c->sgbm_mode = FVO_SGBM_CLASSIC;
+  c->sgbm_lanes = 0;
+  c->sgbm_cols = 0;
+  c->sgbm_handoff_us = 0;
 }
 
 static void release(fvo_ctx* c) {
@@ -169,14 +174,14 @@ int fvo_bf_match(fvo_ctx* c, const uint8_t* query, const int32_t* n_query, const
 }
 
 int fvo_sgbm(fvo_ctx* c, const uint8_t* left, const uint8_t* right, int32_t batch, int64_t image_stride,
-             int32_t pitch, int16_t* disparity, fvo_stream stream) {
+             int32_t pitch, int16_t* disparity, int32_t* status, fvo_stream stream) {
   if (check_batch(c, batch, FVO_STAGE_SGBM)) return -1;
   if (batch == 0) return 0;
   if (!left || !right || !disparity) return fvo_fail(c, "null pointer argument");
   if (pitch < c->cfg.width || image_stride < (int64_t)pitch * c->cfg.height) return fvo_fail(c, "bad pitch/stride");
   if (batch > (c->cfg.sgbm_max_batch > 0 ? c->cfg.sgbm_max_batch : c->cfg.max_batch))
     return fvo_fail(c, "batch exceeds sgbm_max_batch");
-  return sgbm_run(c, left, right, batch, image_stride, pitch, disparity, (hipStream_t)stream);
+  return sgbm_run(c, left, right, batch, image_stride, pitch, disparity, status, (hipStream_t)stream);
 }
 
 int fvo_backproject(fvo_ctx* c, const int16_t* disparity, const float* kp0, const float* kp1, const int32_t* matches,

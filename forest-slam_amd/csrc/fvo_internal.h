@@ -148,7 +148,7 @@ int bf_run(fvo_ctx* ctx, const uint8_t* q, const int32_t* nq, const uint8_t* t, 
            int32_t* matches, int32_t* nmatch, hipStream_t s);
 int sgbm_init(fvo_ctx* ctx);
 int sgbm_run(fvo_ctx* ctx, const uint8_t* L, const uint8_t* R, int batch, int64_t image_stride, int pitch,
-             int16_t* disp, hipStream_t s);
+             int16_t* disp, int32_t* status, hipStream_t s);
 int pose_init(fvo_ctx* ctx);
 int ransac_table_init(fvo_ctx* ctx);
 int orb_blur_debug(fvo_ctx* ctx);

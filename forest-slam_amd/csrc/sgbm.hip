@@ -280,7 +280,7 @@ __device__ __forceinline__ void derive16(const uint32_t* vp, const uint32_t* v, 
 // row's image bytes are loaded right after the current row is staged and taken before the
 // row's C / V stores (vmcnt retires in order: a wait for them behind the stores would also
 // wait for the stores).  Integer arithmetic as oracle/sgbm_ref.cpp (order-independent sums).
-// The left->right path (LP = true, FVO_SG_MODE=lpath; classic is the default): the block also runs the L path of
+// The left->right path (LP = true, fvo_config.sgbm_mode = FVO_SGBM_LPATH; classic is the default): the block also runs the L path of
 // its CB columns -- per group of 4 output rows, one wave (16 lanes per row, D/16 disparities
 // per lane) steps the 4 rows across the columns over C read back from a 4-row LDS ring, starting
 // from the state the block of the previous column range handed over for those rows, stores the
@@ -291,6 +291,8 @@ struct SgLink {
   int nck, nk;              // checkpoint slots per row; column blocks per stripe
   uint64_t* hand;           // [B][H][2][PQ16][16] hand-off granules {tag, word}, by column-block parity
   uint32_t* ctl;            // [0] ticket, [1] generation, [2] timeouts, [4 + b] pair failed
+  uint64_t deadline;        // bound on one hand-off wait, s_memrealtime ticks (100 MHz)
+  int force_timeout;        // test hook (sgbm_handoff_us = -1): every hand-off times out
 };
 
 typedef __attribute__((address_space(1))) unsigned long long sg_gu64;
@@ -344,20 +346,23 @@ __device__ __attribute__((noinline)) void sg_run_L(SgLink lk, lds_cu32* ring, in
     uint64_t gv[PQ16];
     sg_load_granules<PQ16>(lk, b, H, kb, y0, nrows, gv);
     uint64_t t0 = 0;
+    const bool force = __builtin_amdgcn_readfirstlane(lk.force_timeout) != 0;
     for (int it = 0;; ++it) {
-      bool ok = true;
+      bool ok = !force;
 #pragma unroll
       for (int g = 0; g < PQ16; ++g) {
         lst[g] = (uint32_t)gv[g];
         ok &= (uint32_t)(gv[g] >> 32) == tag;
       }
       if (__all(ok)) break;
-      // bounded wait: after 20 ms (or once the pair is marked failed upstream) give up, mark the
-      // pair failed (its disparities come out invalid) and count the timeout
+      // bounded wait: past the deadline (and at least 64 polls, so one long preemption of the
+      // queue -- the clock runs while the waves are suspended -- cannot end a wait on its first
+      // re-check), or once the pair is marked failed upstream, give up: mark the pair failed (its
+      // disparities come out invalid, fvo_sgbm's status says so) and count the timeout
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
       if (it == 0) t0 = now;
       const bool failed = __hip_atomic_load((sg_gu32*)lk.ctl + 4 + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-      if (failed || now - t0 > 2000000ull) {
+      if (failed || force || (it >= 64 && now - t0 > lk.deadline)) {
         if (lane == 0 && !failed) {
           __hip_atomic_fetch_or((sg_gu32*)lk.ctl + 4 + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_fetch_add((sg_gu32*)lk.ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1091,10 +1096,12 @@ __global__ __launch_bounds__(64, D <= 96 ? 4 : 2) void k_sg_rows(const uint16_t*
 }
 
 // ------------------------------------------------------------------ median 3x3
-// fail (may be null): pairs whose L-path hand-off timed out come out invalid everywhere
+// fail (may be null): pairs whose L-path hand-off timed out come out invalid everywhere;
+// status (may be null): per pair FVO_SGBM_OK / FVO_SGBM_HANDOFF_TIMEOUT, for the caller
 __global__ void k_sg_median(const int16_t* __restrict__ raw, int16_t* __restrict__ out, int W, int H,
-                            const uint32_t* __restrict__ fail, int16_t invalid) {
+                            const uint32_t* __restrict__ fail, int16_t invalid, int32_t* __restrict__ status) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, b = blockIdx.z;
+  if (status && x == 0 && y == 0) status[b] = (fail && fail[b]) ? FVO_SGBM_HANDOFF_TIMEOUT : FVO_SGBM_OK;
   if (x >= W) return;
   const int16_t* s = raw + (int64_t)b * W * H;
   int v[9];
@@ -1127,21 +1134,14 @@ __global__ void k_sg_prep(uint32_t* ctl, int nb) {
   for (int b = t; b < nb; b += blockDim.x) ctl[4 + b] = 0;
 }
 
-// Schedules and launch shapes (read per launch; every variant is bit-identical and
-// parity-tested), FVO_SG_MODE:
-//   (default)  one cost pass, one row pass running both sweeps, with FVO_SG_G lanes per column
-//              (4, 8 or 16) and FVO_SG_CB columns per block (G=4: 32/64; G=8: 16/32; G=16: 32)
-//   lpath      the L path in the cost pass, handed from column block to column block: one V read
-//              per pair fewer (<= 300 MB/pair) but slower -- DESIGN.md §4.2 r5
-int env_int(const char* name, int def) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : def;
-}
-enum SgMode { kSgClassic, kSgLPath };
-SgMode sg_mode() {
-  const char* v = getenv("FVO_SG_MODE");
-  return v && std::string(v) == "lpath" ? kSgLPath : kSgClassic;
-}
+// Schedules and launch shapes (fvo_config, validated by sgbm_init; every variant is
+// bit-identical and parity-tested), sgbm_mode:
+//   FVO_SGBM_CLASSIC  one cost pass, one row pass running both sweeps, with sgbm_lanes lanes per
+//                     column (4, 8 or 16) and sgbm_cols columns per block (4: 32/64; 8: 16/32; 16: 32)
+//   FVO_SGBM_LPATH    the L path in the cost pass, handed from column block to column block: one V
+//                     read per pair fewer (<= 300 MB/pair) but slower -- DESIGN.md §4.2 r5
+int sg_lanes(const fvo_config& c) { return c.sgbm_lanes > 0 ? c.sgbm_lanes : 8; }
+int sg_cols(const fvo_config& c) { return c.sgbm_cols > 0 ? c.sgbm_cols : (sg_lanes(c) == 4 ? 64 : 32); }
 
 SgParams make_params(const fvo_config& c) {
   SgParams p;
@@ -1174,16 +1174,15 @@ int sg_nk(const SgParams& p) { return (p.width1 + kSgCB - 1) / kSgCB; }
 
 template <int D>
 void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_t* R, int nb, int64_t stride,
-                 int pitch, int16_t* disp, hipStream_t s) {
+                 int pitch, int16_t* disp, int32_t* status, hipStream_t s) {
   uint16_t* V = ctx->sg_V;
   uint16_t* M = ctx->sg_M;
   const int nck = sg_nck(p);
   const int16_t invalid = (int16_t)((p.minD - 1) * 16);
-  const SgMode mode = sg_mode();
-  if (mode == kSgClassic) {
-    // (G, CB) of the cost pass: the grid follows the kernel actually launched, so an unsupported
-    // FVO_SG_CB falls back to that G's default shape instead of leaving columns uncomputed
-    const int g = env_int("FVO_SG_G", 8), cbr = env_int("FVO_SG_CB", g == 4 ? 64 : 32);
+  const fvo_config& cfg = ctx->cfg;
+  if (cfg.sgbm_mode == FVO_SGBM_CLASSIC) {
+    // (G, CB) of the cost pass, validated by sgbm_init; the grid follows the kernel launched
+    const int g = sg_lanes(cfg), cbr = sg_cols(cfg);
     typedef void (*CostKernel)(const uint8_t*, const uint8_t*, int64_t, int, SgParams, uint16_t*, uint16_t*, SgLink);
     CostKernel kern;
     int gg, cb;
@@ -1198,11 +1197,12 @@ void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_
     FVO_TIMED(ctx, KN_SG_ROWS, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_rows<D, kSwBoth>), dim3(sg_nblk(p), nb), dim3(64), 0, s,
                                                      V, M, p, ctx->sg_ckpt, nck, ctx->sg_raw));
     FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.W + 255) / 256, p.H, nb), dim3(256), 0, s,
-                                                       ctx->sg_raw, disp, p.W, p.H, nullptr, invalid));
+                                                       ctx->sg_raw, disp, p.W, p.H, nullptr, invalid, status));
     return;
   }
   const int nk = sg_nk(p);
-  const SgLink lk{ctx->sg_ckpt, nck, nk, ctx->sg_hand, ctx->sg_ctl};
+  const int64_t us = cfg.sgbm_handoff_us > 0 ? cfg.sgbm_handoff_us : 250000;
+  const SgLink lk{ctx->sg_ckpt, nck, nk, ctx->sg_hand, ctx->sg_ctl, (uint64_t)us * 100u, cfg.sgbm_handoff_us < 0 ? 1 : 0};
   hipLaunchKernelGGL(k_sg_prep, dim3(1), dim3(256), 0, s, ctx->sg_ctl, nb);
   FVO_TIMED(ctx, KN_SG_VERT, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_costvert<D, kSgCB, 8, true>),
                                                    dim3(nk * p.nstripes * nb), dim3(8 * kSgCB), 0, s, L, R, stride, pitch,
@@ -1210,7 +1210,7 @@ void launch_sgbm(fvo_ctx* ctx, const SgParams& p, const uint8_t* L, const uint8_
   FVO_TIMED(ctx, KN_SG_ROWS, s, hipLaunchKernelGGL(HIP_KERNEL_NAME(k_sg_rows<D, kSwRight>), dim3(sg_nblk(p), nb), dim3(64), 0, s,
                                                    V, M, p, ctx->sg_ckpt, nck, ctx->sg_raw));
   FVO_TIMED(ctx, KN_SG_MEDIAN, s, hipLaunchKernelGGL(k_sg_median, dim3((p.W + 255) / 256, p.H, nb), dim3(256), 0, s,
-                                                     ctx->sg_raw, disp, p.W, p.H, ctx->sg_ctl + 4, invalid));
+                                                     ctx->sg_raw, disp, p.W, p.H, ctx->sg_ctl + 4, invalid, status));
 }
 
 }  // namespace
@@ -1222,6 +1222,16 @@ int sgbm_init(fvo_ctx* ctx) {
     return fvo_fail(ctx, "SGBM: numDisparities must be 64, 96 or 128");
   if (c.uniqueness_ratio != 0) return fvo_fail(ctx, "SGBM: only uniquenessRatio=0 is supported");
   if (c.sgbm_stripes < 1) return fvo_fail(ctx, "SGBM: stripes must be >= 1");
+  if (c.sgbm_mode != FVO_SGBM_CLASSIC && c.sgbm_mode != FVO_SGBM_LPATH)
+    return fvo_fail(ctx, "SGBM: sgbm_mode must be FVO_SGBM_CLASSIC or FVO_SGBM_LPATH");
+  if (c.sgbm_mode == FVO_SGBM_CLASSIC) {
+    const int g = sg_lanes(c), cb = sg_cols(c);
+    if (!((g == 4 && (cb == 32 || cb == 64)) || (g == 8 && (cb == 16 || cb == 32)) || (g == 16 && cb == 32)))
+      return fvo_fail(ctx, "SGBM: (sgbm_lanes, sgbm_cols) must be (4, 32|64), (8, 16|32) or (16, 32)");
+  } else if (c.sgbm_lanes != 0 || c.sgbm_cols != 0) {
+    return fvo_fail(ctx, "SGBM: sgbm_lanes / sgbm_cols apply to the classic schedule only (leave them 0)");
+  }
+  if (c.sgbm_handoff_us < -1) return fvo_fail(ctx, "SGBM: sgbm_handoff_us must be >= -1");
   SgParams p = make_params(c);
   if (p.width1 <= 0) return fvo_fail(ctx, "SGBM: image narrower than numDisparities");
   // path values are at most C + P2 with C <= 49 x the largest BT pixel cost (2 ftzero + 255/4);
@@ -1245,7 +1255,9 @@ int sgbm_init(fvo_ctx* ctx) {
   // sg_hand: the L path's hand-off granules [B][H][2][D/32][16] u64; sg_ctl: ticket, generation,
   // timeout count, per-pair failure flags.  Both zeroed once (tags of a zeroed granule never match)
   const int64_t hand = (int64_t)p.H * 2 * (p.D / 32) * 16;
-  if (sg_nk(p) >= 128) return fvo_fail(ctx, "SGBM: image too wide (width - numDisparities > 4064)");
+  // the L path's hand-off tags carry the column block in 7 bits
+  if (c.sgbm_mode == FVO_SGBM_LPATH && sg_nk(p) >= 128)
+    return fvo_fail(ctx, "SGBM: FVO_SGBM_LPATH needs width - numDisparities <= 4064 (use the classic schedule)");
   // sg_M: min over d of every stored V row, [B][HG4 + nstripes][width1][4] u16
   if ((rc = fvo_alloc(ctx, &ctx->sg_V, B * vol)) || (rc = fvo_alloc(ctx, &ctx->sg_M, B * vol / p.D)) ||
       (rc = fvo_alloc(ctx, &ctx->sg_ckpt, B * ckp)) ||
@@ -1258,12 +1270,12 @@ int sgbm_init(fvo_ctx* ctx) {
 }
 
 int sgbm_run(fvo_ctx* ctx, const uint8_t* L, const uint8_t* R, int batch, int64_t image_stride, int pitch,
-             int16_t* disp, hipStream_t s) {
+             int16_t* disp, int32_t* status, hipStream_t s) {
   SgParams p = make_params(ctx->cfg);
   switch (p.D) {
-    case 64: launch_sgbm<64>(ctx, p, L, R, batch, image_stride, pitch, disp, s); break;
-    case 96: launch_sgbm<96>(ctx, p, L, R, batch, image_stride, pitch, disp, s); break;
-    default: launch_sgbm<128>(ctx, p, L, R, batch, image_stride, pitch, disp, s); break;
+    case 64: launch_sgbm<64>(ctx, p, L, R, batch, image_stride, pitch, disp, status, s); break;
+    case 96: launch_sgbm<96>(ctx, p, L, R, batch, image_stride, pitch, disp, status, s); break;
+    default: launch_sgbm<128>(ctx, p, L, R, batch, image_stride, pitch, disp, status, s); break;
   }
   FVO_LAUNCH_CHECK(ctx);
   return 0;

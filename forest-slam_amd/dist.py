@@ -164,7 +164,12 @@ def exchange_frame_map(T_step: torch.Tensor, st_step: torch.Tensor, P3: torch.Te
 
 def exchange_bytes(B: int, cap: int) -> int:
     """Bytes one rank contributes to a step's map exchange: T f64 [B,4,4] + status i32 [B] +
-    points3D f32 [B,cap,3] + counts i32 [B]."""
+    points3D f32 [B,cap,3] + counts i32 [B] -- 1,593,856 B at 600p (B = 64, cap 2064).  The point
+    sets travel at the context's capacity: a collective's shape must be known on the host when it
+    is queued, and the step's point counts exist only on the device, so a compacted send would
+    need a host round trip per step (the step is asynchronous by design) or a lossy fixed cap;
+    ORB's retainBest keeps ties past nfeatures, so no tighter exact bound than the keypoint
+    capacity exists.  DESIGN.md §6 has the measured padding share."""
     return B * (16 * 8 + 4 + cap * 3 * 4 + 4)
 
 
@@ -206,7 +211,8 @@ class SequenceRank:
     (``exchange_frame_map``) and, with ``map_capacity`` > 0, their placement in the
     multi-sequence map (``GlobalMap``; ``self.gmap``).  ``map_rank0_only``: the map lives on rank
     0 only -- the step data are gathered there instead of all-gathered (the other ranks send
-    their 12 MB per step and receive nothing), and only rank 0 places them.
+    their ``exchange_bytes`` -- 1.59 MB per step at 600p, B = 64 -- and receive nothing), and only
+    rank 0 places them.
 
     The exchange and the map run on their own stream behind the step's kernels: the host does
     not wait for them (nor for the step), and the next step's back stage only waits for the
@@ -254,11 +260,15 @@ class SequenceRank:
         placement, the collectives' share of it, and the host time of the exchange call."""
         if not self.exchange:
             return None
-        recv = self.send_bytes * self.world if (not self.rank0_only or self.rank == 0) else 0
+        # bytes over the link: the rank's own slice of the gathered result never leaves it
+        recv = self.send_bytes * (self.world - 1) if (not self.rank0_only or self.rank == 0) else 0
+        # the last step's payload without the capacity padding (reads the counts: synchronises)
+        self.stream.synchronize()
+        useful = int(self.sN.numel()) * (16 * 8 + 4 + 4) + int(self.sN.clamp(min=0).sum().item()) * 12
         out = {"mode": ("gather to rank 0, map on rank 0 only" if self.rank0_only
                         else "all-gather, every rank places the whole map"),
                "send_bytes_per_rank_per_step": self.send_bytes, "recv_bytes_per_rank_per_step": recv,
-               "steps_timed": len(self._ev)}
+               "useful_send_bytes_last_step": useful, "steps_timed": len(self._ev)}
         if self._ev:
             self.stream.synchronize()
             tot = [a.elapsed_time(d) for a, b, c, d in self._ev]

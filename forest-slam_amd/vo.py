@@ -30,6 +30,9 @@ from . import _lib
 # guard at stereo_slam.py:292), STATUS_KP_OVERFLOW: an image of the pair had more ORB keypoints
 # than the context's kp_capacity (no result; raise kp_capacity).
 STATUS_KP_OVERFLOW = -3
+# ... STATUS_SGBM_FAILED: the pair's SGBM hand-off timed out (only under sgbm_mode=SGBM_LPATH;
+# fvo_sgbm status SGBM_HANDOFF_TIMEOUT), so it has no disparities and no pose.
+STATUS_SGBM_FAILED = -4
 
 
 class StereoFrontEnd:
@@ -70,6 +73,8 @@ class StereoFrontEnd:
         self.prevL = e((B, height, width), torch.uint8)
         self.prevR = e((B, height, width), torch.uint8)
         self.disp_buf = two((B, height, width), torch.int16)
+        self.sg_status_buf = two((B,), torch.int32)
+        self.sgbm_can_fail = int(self.ctx.cfg.sgbm_mode) == _lib.SGBM_LPATH
         # the BA's per-keypoint stereo points of the step's previous-left frames, computed in the
         # front stage (they need only its disparities and keypoints) into a slot like disp
         self.kstereo_buf = two((B, cap, 4), torch.float32) if self.ba_window else [None, None]
@@ -175,7 +180,7 @@ class StereoFrontEnd:
             # (C) after BF the last frame's keypoints / descriptors / counts
             ctx.copy_regions(self._sgbm_pairs(L, R, n) + [(self.imgs[:n], L), (self.imgs[n:2 * n], R)])
             # SGBM first: ORB + BF first measured slower (r3 4242 vs 4284, r4 5051 vs 5227 frames/s)
-            disp = ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n])
+            disp = ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n], status=self.sg_status[:n])
             kp, desc, cnt = ctx.orb(self.imgs[:2 * n], out=(self.kp[:2 * n], self.desc[:2 * n], self.cnt[:2 * n]))
             # query (previous) sets: left frames then right frames; previous-left keypoints
             ctx.copy_regions([(self.q_desc[0], self.last_desc[0]), (self.q_cnt[0:1], self.last_cnt[0:1]),
@@ -209,6 +214,8 @@ class StereoFrontEnd:
         ctx.count_guard(cnt, n, 2 if self.match_right else 1, q_counts=self.q_cnt, status=st,
                         code=STATUS_KP_OVERFLOW,
                         clamped_out=self.hnkp[self.ba_window - 1:self.ba_window - 1 + n] if self.ba_window else None)
+        if self.sgbm_can_fail:  # the L-path schedule's dropped pairs (classic SGBM cannot fail)
+            ctx.count_guard(self.sg_status[:n], n, 1, status=st, code=STATUS_SGBM_FAILED)
         out = T
         if self.ba_window:
             out = self._local_ba(n, kp, cnt, m, nm, disp, T)
@@ -229,6 +236,7 @@ class StereoFrontEnd:
         self.q_cnt, self.q_kp = self.q_cnt_buf[slot], self.q_kp_buf[slot]
         self.matches, self.nmatch = self.matches_buf[slot], self.nmatch_buf[slot]
         self.disp = self.disp_buf[slot]
+        self.sg_status = self.sg_status_buf[slot]
         self.kstereo = self.kstereo_buf[slot]
 
     def _local_ba(self, n, kp, cnt, m, nm, disp, T):
@@ -282,8 +290,9 @@ def run_sequence(frontend: StereoFrontEnd, L_all: torch.Tensor, R_all: torch.Ten
     _check_overflow(st)
     # status -1 = fewer than 6 points: the reference skips the frame (no pose, no TUM row,
     # stereo_slam.py:292); status 0 = RANSAC failure: identity T (the reference would chain
-    # whatever solvePnPRansac left in rvec/tvec), row emitted.
-    valid = st != -1
+    # whatever solvePnPRansac left in rvec/tvec), row emitted; STATUS_SGBM_FAILED (the pair had no
+    # disparities) is skipped like -1.
+    valid = (st != -1) & (st != STATUS_SGBM_FAILED)
     cum = ev.chain(T, valid)
     if stamps is None:
         stamps = np.arange(n, dtype=np.float64)

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define FVO_ABI_VERSION 6
+#define FVO_ABI_VERSION 7
 
 typedef struct fvo_ctx fvo_ctx;
 typedef void* fvo_stream; /* hipStream_t */
@@ -97,7 +97,23 @@ typedef struct fvo_config {
   int32_t ba_max_obs;       /* per-window observation cap (32768) */
   int32_t sgbm_max_batch;   /* max pairs per fvo_sgbm call (0 = max_batch): the SGBM path
                                volume (one u16 volume, ~100 MB per pair at 600p) is sized by it */
+  /* SGBM schedule (every schedule and launch shape is bit-identical).  Chosen
+   * here, at fvo_create, and nowhere else: the library reads no environment variables. */
+  int32_t sgbm_mode;        /* FVO_SGBM_CLASSIC (0, default) or FVO_SGBM_LPATH */
+  int32_t sgbm_lanes;       /* classic cost pass: lanes per column, 4 / 8 / 16 (0 = 8) */
+  int32_t sgbm_cols;        /* classic cost pass: columns per block (0 = default; lanes 4: 32 or 64
+                               (default 64), lanes 8: 16 or 32 (default 32), lanes 16: 32) */
+  int32_t sgbm_handoff_us;  /* lpath: bound on one column-block hand-off wait in microseconds
+                               (0 = 250000); -1 = test hook: every hand-off times out */
 } fvo_config;
+
+/* fvo_config.sgbm_mode */
+#define FVO_SGBM_CLASSIC 0 /* cost pass + row pass running both horizontal sweeps */
+#define FVO_SGBM_LPATH 1   /* left->right path inside the cost pass, handed between column blocks */
+/* fvo_sgbm status values */
+#define FVO_SGBM_OK 0
+#define FVO_SGBM_HANDOFF_TIMEOUT (-1) /* lpath: a hand-off wait of the pair timed out; its disparity
+                                         map is all invalid ((min_disparity-1)*16) */
 
 /* fvo_config.stages: a context only serves the stages it was created for (e.g. a
  * BFMatcher-only context needs no image-sized workspace). */
@@ -145,9 +161,11 @@ int fvo_bf_match(fvo_ctx* ctx, const uint8_t* query, const int32_t* n_query, con
                  fvo_stream stream);
 
 /* StereoSGBM 3-way disparity (incl. the final 3x3 median) of `batch` rectified pairs.
- * disparity: [batch][height][width] i16, disparity*16, invalid = (min_disparity-1)*16. */
+ * disparity: [batch][height][width] i16, disparity*16, invalid = (min_disparity-1)*16.
+ * status:    [batch] i32 (device, may be NULL): FVO_SGBM_OK, or FVO_SGBM_HANDOFF_TIMEOUT (only
+ *            under FVO_SGBM_LPATH) when the pair's disparities were dropped. */
 int fvo_sgbm(fvo_ctx* ctx, const uint8_t* left, const uint8_t* right, int32_t batch, int64_t image_stride,
-             int32_t pitch, int16_t* disparity, fvo_stream stream);
+             int32_t pitch, int16_t* disparity, int32_t* status, fvo_stream stream);
 
 /* Matched-keypoint back-projection through the disparity map (stereo_slam.py:262-289).
  * kp0/kp1:   keypoint records of the previous / current left images ([batch][cap][8]).

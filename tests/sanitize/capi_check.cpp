@@ -45,7 +45,8 @@ int main() {
                           "first_level", "wta_k", "score_type", "patch_size", "fast_threshold", "min_disparity",
                           "num_disparities", "block_size", "P1", "P2", "disp12_max_diff", "pre_filter_cap",
                           "uniqueness_ratio", "sgbm_stripes", "kp_capacity", "stages", "ba_window",
-                          "ba_max_landmarks", "ba_max_obs", "sgbm_max_batch"};
+                          "ba_max_landmarks", "ba_max_obs", "sgbm_max_batch", "sgbm_mode", "sgbm_lanes",
+                          "sgbm_cols", "sgbm_handoff_us"};
   for (size_t i = 0; i < sizeof(fields) / sizeof(fields[0]); ++i) CHECK(fvo_config_offset(fields[i]) == (int32_t)(4 * i));
   CHECK(fvo_config_offset("nope") == -1 && fvo_config_offset(nullptr) == -1);
   CHECK(fvo_abi_version() == FVO_ABI_VERSION);
@@ -102,10 +103,10 @@ int main() {
   reset(); reached(fvo_bf_match(c, u8, i32, u8, i32, 2, cap, i32, i32, nullptr), "bf_run");
 
   // ---- SGBM
-  reset(); rejected(c, fvo_sgbm(c, u8, nullptr, 1, W * H, W, i16, nullptr));
-  reset(); rejected(c, fvo_sgbm(c, u8, u8, 1, W * H, W - 8, i16, nullptr));
-  reset(); rejected(c, fvo_sgbm(c, u8, u8, 9, W * H, W, i16, nullptr));
-  reset(); reached(fvo_sgbm(c, u8, u8, 4, W * H, W, i16, nullptr), "sgbm_run");
+  reset(); rejected(c, fvo_sgbm(c, u8, nullptr, 1, W * H, W, i16, nullptr, nullptr));
+  reset(); rejected(c, fvo_sgbm(c, u8, u8, 1, W * H, W - 8, i16, nullptr, nullptr));
+  reset(); rejected(c, fvo_sgbm(c, u8, u8, 9, W * H, W, i16, nullptr, nullptr));
+  reset(); reached(fvo_sgbm(c, u8, u8, 4, W * H, W, i16, nullptr, nullptr), "sgbm_run");
 
   // ---- back-projection / PnP
   reset(); rejected(c, fvo_backproject(c, i16, f32, f32, i32, i32, 1, cap, nullptr, 0.25, f32, f32, i32, nullptr));
@@ -218,7 +219,7 @@ int main() {
   cfg.kp_capacity = 64;
   CHECK(fvo_create(0, &cfg, &c) == 0);
   reset(); rejected(c, fvo_orb_detect_compute(c, u8, 1, W * H, W, f32, u8, i32, 64, nullptr));
-  reset(); rejected(c, fvo_sgbm(c, u8, u8, 1, W * H, W, i16, nullptr));
+  reset(); rejected(c, fvo_sgbm(c, u8, u8, 1, W * H, W, i16, nullptr, nullptr));
   reset(); reached(fvo_bf_match(c, u8, i32, u8, i32, 1, 64, i32, i32, nullptr), "bf_run");
   fvo_destroy(c);
 

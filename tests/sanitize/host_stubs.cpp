@@ -59,7 +59,7 @@ int bf_run(fvo_ctx*, const uint8_t*, const int32_t*, const uint8_t*, const int32
            hipStream_t) {
   return hit("bf_run");
 }
-int sgbm_run(fvo_ctx*, const uint8_t*, const uint8_t*, int, int64_t, int, int16_t*, hipStream_t) {
+int sgbm_run(fvo_ctx*, const uint8_t*, const uint8_t*, int, int64_t, int, int16_t*, int32_t*, hipStream_t) {
   return hit("sgbm_run");
 }
 int backproject_run(fvo_ctx*, const int16_t*, const float*, const float*, const int32_t*, const int32_t*, int, int,

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(path)
     missing = [n for n in _declared() if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.fvo_abi_version() == 6
+    assert lib.fvo_abi_version() == 7
 
 
 def test_binding_signatures_cover_header():
@@ -49,6 +49,17 @@ def test_config_default_matches_reference_constants():
     assert cfg.sgbm_stripes == 4
     assert cfg.stages == 63  # FVO_STAGE_ALL
     assert (cfg.ba_window, cfg.ba_max_landmarks, cfg.ba_max_obs) == (10, 4096, 32768)
+    # the SGBM schedule: classic, default launch shape, default hand-off bound
+    assert (cfg.sgbm_mode, cfg.sgbm_lanes, cfg.sgbm_cols, cfg.sgbm_handoff_us) == (_lib.SGBM_CLASSIC, 0, 0, 0)
+
+
+def test_library_reads_no_environment():
+    """the SGBM schedule was chosen by FVO_SG_* environment variables read on every
+    launch; it is fvo_config's now (ABI 7), and no source of the library reads the environment."""
+    csrc = os.path.join(ROOT, "forest-slam_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        text = open(os.path.join(csrc, f)).read()
+        assert "getenv" not in text and "FVO_SG_" not in text, f
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-GPU failure path")
@@ -63,7 +74,7 @@ def test_config_layout_matches_binding():
     every field offset), or fvo_config_default writes past the Python object."""
     from forest_slam_amd import _lib
     L = _lib.load()
-    assert L.fvo_config_size() == ctypes.sizeof(_lib.FvoConfig) == 27 * 4
+    assert L.fvo_config_size() == ctypes.sizeof(_lib.FvoConfig) == 31 * 4
     for name, _ in _lib.FvoConfig._fields_:
         assert L.fvo_config_offset(name.encode()) == getattr(_lib.FvoConfig, name).offset, name
     assert L.fvo_config_offset(b"no_such_field") == -1

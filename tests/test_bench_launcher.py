@@ -33,8 +33,11 @@ def test_gpus_2_starts_two_ranks():
     # tensors of the bench shapes: B = 64 frames, cap = 2 * 1000 + 64 keypoints)
     x = j["exchange"]
     send = 64 * (16 * 8 + 4 + (2 * 1000 + 64) * 3 * 4 + 4)
+    assert send == 1_593_856  # DESIGN.md §6 / dist.exchange_bytes: 1.59 MB per rank per step at 600p
     assert x["mode"].startswith("all-gather") and x["send_bytes_per_rank_per_step"] == send
-    assert x["recv_bytes_per_rank_per_step"] == 2 * send and x["steps_timed"] == 3 and x["host_ms_per_step"] > 0
+    # two ranks: each receives the other's slice over the link (its own never leaves it)
+    assert x["recv_bytes_per_rank_per_step"] == send and x["gathered_bytes_per_step"] == 2 * send
+    assert x["steps_timed"] == 3 and x["host_ms_per_step"] > 0
     assert "stream_ms_per_step" in x and "collective_ms_per_step" in x
 
 

@@ -157,21 +157,71 @@ def sgbm_ctl(ctx):
     return ctx.debug_buffer(9).view(torch.int32).numpy()
 
 
-def test_sgbm_bit_exact(oracle_mod, frames):
+SG_MODE = {"classic": 0, "lpath": 1}  # fvo_config.sgbm_mode (_lib.SGBM_CLASSIC / SGBM_LPATH)
+
+
+@pytest.mark.parametrize("mode", ["classic", "lpath"])
+def test_sgbm_bit_exact(oracle_mod, frames, mode):
     from forest_slam_amd import _lib
-    ctx = _lib.Context(960, 600, max_batch=2)
+    ctx = _lib.Context(960, 600, max_batch=2, sgbm_mode=SG_MODE[mode])
     L = np.stack([frames[0][0], frames[1][0]])
     R = np.stack([frames[0][1], frames[1][1]])
     for rep in range(2):  # a second call (lpath: the hand-off granules of the first carry an older tag)
-        d = ctx.sgbm(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda())
+        st = torch.full((2,), 7, dtype=torch.int32, device="cuda")
+        d = ctx.sgbm(torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda(), status=st)
         torch.cuda.synchronize()
         d = d.cpu().numpy()
         for i in range(2):
             want = oracle_mod.sgbm(L[i], R[i])
             bad = np.argwhere(d[i] != want)
             assert len(bad) == 0, f"call {rep} pair {i}: {len(bad)} px differ, first {bad[:5]}"
+        assert st.tolist() == [_lib.SGBM_OK] * 2  # written by every call, in both schedules
         ctl = sgbm_ctl(ctx)
         assert ctl[2] == 0 and not ctl[4:6].any()  # no L-path hand-off timed out (lpath schedule)
+
+
+def test_sgbm_lpath_timeout_reaches_the_caller(frames):
+    """ADVICE/VERDICT r5: an L-path hand-off that times out must reach the caller.  The test hook
+    sgbm_handoff_us = -1 makes every hand-off time out: each pair (more than one column block)
+    comes out all-invalid with status SGBM_HANDOFF_TIMEOUT through fvo_sgbm's status array, and
+    StereoFrontEnd marks those frames STATUS_SGBM_FAILED."""
+    from forest_slam_amd import _lib, synth, vo
+    ctx = _lib.Context(960, 600, max_batch=2, sgbm_mode=_lib.SGBM_LPATH, sgbm_handoff_us=-1,
+                       stages=_lib.STAGE_SGBM)
+    L = torch.from_numpy(np.stack([frames[0][0], frames[1][0]])).cuda()
+    R = torch.from_numpy(np.stack([frames[0][1], frames[1][1]])).cuda()
+    st = torch.zeros((2,), dtype=torch.int32, device="cuda")
+    d = ctx.sgbm(L, R, status=st)
+    torch.cuda.synchronize()
+    assert st.tolist() == [_lib.SGBM_HANDOFF_TIMEOUT] * 2
+    assert bool((d == -16).all())  # (min_disparity - 1) * 16 everywhere
+    assert sgbm_ctl(ctx)[2] > 0
+    fe = vo.StereoFrontEnd(960, 600, synth.K0, synth.DIST_L, synth.BASELINE, batch=2, nfeatures=500,
+                           ba_window=3, sgbm_mode=_lib.SGBM_LPATH, sgbm_handoff_us=-1)
+    Ls = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
+    Rs = torch.from_numpy(np.stack([f[1] for f in frames])).cuda()
+    fe.prime(Ls[0], Rs[0])
+    _, sts = fe.step(Ls[1:3], Rs[1:3])
+    torch.cuda.synchronize()
+    assert sts.tolist() == [vo.STATUS_SGBM_FAILED] * 2
+
+
+def test_sgbm_schedule_config_is_validated():
+    """The schedule lives in fvo_config (ABI 7), validated at fvo_create: unknown modes, unsupported
+    (lanes, cols) shapes and shapes given for the L-path schedule are refused; the L path's 7-bit
+    column-block tag limits only that schedule's image width, not the classic one's."""
+    from forest_slam_amd import _lib
+    S = _lib.STAGE_SGBM
+    for bad in ({"sgbm_mode": 2}, {"sgbm_lanes": 8, "sgbm_cols": 64}, {"sgbm_lanes": 16, "sgbm_cols": 16},
+                {"sgbm_lanes": 3}, {"sgbm_mode": _lib.SGBM_LPATH, "sgbm_lanes": 8}, {"sgbm_handoff_us": -2}):
+        with pytest.raises(RuntimeError, match="fvo_create"):
+            _lib.Context(320, 200, stages=S, **bad)
+    for ok in ({"sgbm_lanes": 4}, {"sgbm_lanes": 4, "sgbm_cols": 32}, {"sgbm_lanes": 16},
+               {"sgbm_mode": _lib.SGBM_LPATH, "sgbm_handoff_us": 1000}):
+        _lib.Context(320, 200, stages=S, **ok).close()
+    _lib.Context(4300, 64, stages=S).close()  # width1 = 4204 > 4064: classic is fine
+    with pytest.raises(RuntimeError, match="fvo_create"):
+        _lib.Context(4300, 64, stages=S, sgbm_mode=_lib.SGBM_LPATH)
 
 
 def test_sgbm_small_geometry(oracle_mod):
@@ -336,16 +386,14 @@ def sgbm_ref(oracle_mod, frames):
 
 
 @pytest.mark.parametrize("mode,g,cb", [("classic", 4, 64), ("classic", 4, 32), ("classic", 8, 32), ("classic", 8, 16),
-                                       ("classic", 16, 32), ("lpath", 8, 32)])
-def test_sgbm_variants_bit_exact(frames, sgbm_ref, monkeypatch, mode, g, cb):
+                                       ("classic", 16, 32), ("lpath", 0, 0)])
+def test_sgbm_variants_bit_exact(frames, sgbm_ref, mode, g, cb):
     """Every SGBM schedule and launch variant is bit-identical to the oracle: the default schedule
     (one row pass running both sweeps) with each cost-pass shape (lanes per column, columns per
-    block), and the L path run inside the cost pass with its column-block hand-off (lpath)."""
+    block), and the L path run inside the cost pass with its column-block hand-off (lpath).  The
+    schedule is chosen through fvo_config (sgbm_mode / sgbm_lanes / sgbm_cols)."""
     from forest_slam_amd import _lib
-    monkeypatch.setenv("FVO_SG_MODE", mode)
-    monkeypatch.setenv("FVO_SG_G", str(g))
-    monkeypatch.setenv("FVO_SG_CB", str(cb))
-    ctx = _lib.Context(960, 600, max_batch=len(frames))
+    ctx = _lib.Context(960, 600, max_batch=len(frames), sgbm_mode=SG_MODE[mode], sgbm_lanes=g, sgbm_cols=cb)
     L = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
     R = torch.from_numpy(np.stack([f[1] for f in frames])).cuda()
     d = ctx.sgbm(L, R)
@@ -358,19 +406,18 @@ def test_sgbm_variants_bit_exact(frames, sgbm_ref, monkeypatch, mode, g, cb):
 
 @pytest.mark.parametrize("mode", ["classic", "lpath"])
 @pytest.mark.parametrize("W,H,nd", [(333, 217, 64), (200, 120, 96), (1024, 100, 128), (500, 77, 96)])
-def test_sgbm_ragged_geometries_bit_exact(oracle_mod, monkeypatch, W, H, nd, mode):
+def test_sgbm_ragged_geometries_bit_exact(oracle_mod, W, H, nd, mode):
     """Image widths that leave a partial 16-column chunk / 8-column segment and heights that
     leave a partial 16-row band (the row kernel's edge cases), every supported D; under the
     L-path schedule also a partial last column block (W - D not a multiple of its 32 columns)
     and its hand-off chain across column blocks."""
     from forest_slam_amd import _lib
-    monkeypatch.setenv("FVO_SG_MODE", mode)
     rng = np.random.default_rng(W * 7 + H)
     import forest_slam_amd.synth as synth
     seq = synth.StereoSequence(seed=W % 13, n_frames=1, W=W, H=H, device="cpu")
     L, R = (x.numpy() for x in seq.frame(0))
     Ln = np.clip(L.astype(np.int32) + rng.integers(-3, 4, L.shape), 0, 255).astype(np.uint8)
-    ctx = _lib.Context(W, H, max_batch=2, num_disparities=nd, stages=_lib.STAGE_SGBM)
+    ctx = _lib.Context(W, H, max_batch=2, num_disparities=nd, stages=_lib.STAGE_SGBM, sgbm_mode=SG_MODE[mode])
     d = ctx.sgbm(torch.from_numpy(np.stack([L, Ln])).cuda(), torch.from_numpy(np.stack([R, R])).cuda())
     torch.cuda.synchronize()
     for i, img in enumerate((L, Ln)):

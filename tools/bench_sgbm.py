@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """SGBM alone on the GPU: B=64 synthetic 960x600 pairs, per-kernel times (HIP events) and
-the whole-call time, for the cost-pass launch variant selected by FVO_SG_G / FVO_SG_CB.
+the whole-call time, for the schedule / cost-pass launch shape given on the command line
+(fvo_config.sgbm_mode / sgbm_lanes / sgbm_cols):
+    python tools/bench_sgbm.py [--mode classic|lpath] [--lanes G] [--cols CB] [--batch B]
 Prints one JSON line."""
+import argparse
 import json
 import os
 import sys
@@ -14,11 +17,19 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", choices=["classic", "lpath"], default="classic")
+    ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--cols", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=64)
+    a = ap.parse_args()
     from forest_slam_amd import _lib, synth
-    B, W, H = int(os.environ.get("B", "64")), 960, 600
+    B, W, H = a.batch, 960, 600
     seq = synth.StereoSequence(seed=0, n_frames=B, W=W, H=H, device="cuda")
     L, R = seq.frames(range(B))
-    ctx = _lib.Context(W, H, max_batch=B, stages=_lib.STAGE_SGBM)
+    mode = _lib.SGBM_LPATH if a.mode == "lpath" else _lib.SGBM_CLASSIC
+    ctx = _lib.Context(W, H, max_batch=B, stages=_lib.STAGE_SGBM, sgbm_mode=mode, sgbm_lanes=a.lanes,
+                       sgbm_cols=a.cols)
     out = torch.empty((B, H, W), dtype=torch.int16, device="cuda")
     for _ in range(2):
         ctx.sgbm(L, R, out=out)
@@ -35,7 +46,7 @@ def main():
     torch.cuda.synchronize()
     st = {k: round(v[0] / n, 4) for k, v in ctx.timing_read().items()}
     ctx.timing_enable([])
-    var = {k: os.environ.get(k, "") for k in ("FVO_SG_G", "FVO_SG_CB")}
+    var = {"mode": a.mode, "lanes": a.lanes, "cols": a.cols}
     print(json.dumps({"variant": var, "call_ms": round(call_ms, 3), "kernels_ms": st,
                       "workspace_gb": round(ctx.workspace_bytes / 1e9, 2)}), flush=True)
 
