@@ -622,9 +622,9 @@ def main():
     dom_t = fe.ctx.timing_read()
     fe.ctx.timing_enable([])
     elapsed = rk.max_elapsed(elapsed)
-    # SGBM hand-off timeouts over the context's life (control word 2; only the L-path schedule
-    # can have any: its pairs then carry STATUS_SGBM_FAILED)
-    sg_timeouts = int(fe.ctx.debug_buffer(9).view(torch.int32)[2].item())
+    # SGBM pairs dropped by an L-path hand-off timeout in the last two steps (fvo_sgbm's status
+    # of the two front-stage slots; the classic schedule cannot time out)
+    sg_failed = int(sum(int((t == _lib.SGBM_HANDOFF_TIMEOUT).sum().item()) for t in fe.sg_status_buf))
     xs = rank_step.exchange_stats()
     rank_step.timing(False)
     exchange = exchange_fields(world, bool(args.map_rank0), xs["send_bytes_per_rank_per_step"] if xs else 0,
@@ -754,7 +754,7 @@ def main():
             "global_map": global_map,
             "exchange": exchange,
             "stages_ms_per_step": stage_ms,
-            "sgbm": {"mode": args.sgbm_mode, "handoff_timeouts": sg_timeouts},
+            "sgbm": {"mode": args.sgbm_mode, "pairs_failed_last_2_steps": sg_failed},
             "workspace_gb": round(fe.ctx.workspace_bytes / 1e9, 2),
         }
         out.update(rk.fields())

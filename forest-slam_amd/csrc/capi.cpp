@@ -85,7 +85,7 @@ void fvo_config_default(fvo_config* c, int32_t width, int32_t height) {
 static void release(fvo_ctx* c) {
   void* ptrs[] = {c->pyr,        c->blur,      c->score,     c->cand,     c->hel,
                   c->ncand,      c->nsel1,     c->nsel2,     c->koff,     c->scratch, c->fast_rec, c->rt.xofs,  c->rt.xc1,
-                  c->rt.yofs,    c->rt.yc1,    c->umax,      c->bf_sidx,  c->bf_sdist, c->bf_tidx, c->sg_ckpt,
+                  c->rt.yofs,    c->rt.yc1,    c->umax,      c->bf_rowkey, c->bf_colkey, c->sg_ckpt,
                   c->sg_V,      c->sg_M,      c->sg_raw,    c->sg_hand,   c->sg_ctl,    c->pnp_hyp,  c->pnp_good,
                   c->pnp_sub,    c->rs_table, c->pnp_models, c->pnp_ws, c->pnp_state, c->pnp_plan, c->pnp_pts, c->ba_ws,
                   c->em_x, c->em_models, c->em_good, c->em_nmod, c->em_state, c->em_ws};

@@ -74,9 +74,8 @@ struct fvo_ctx {
   ResizeTab rt{};
   int32_t* umax = nullptr;    // IC angle row extents
   // BF workspace
-  int32_t* bf_sidx = nullptr; // [B][cap]
-  int32_t* bf_sdist = nullptr;
-  int32_t* bf_tidx = nullptr;
+  uint32_t* bf_rowkey = nullptr;  // [B][cap] (distance << 16 | train index) minimum per query row
+  uint32_t* bf_colkey = nullptr;  // [B][cap] (distance << 16 | query index) minimum per train column
   // SGBM workspace
   uint16_t* sg_V = nullptr;     // top-down path V, [B][HG4 + nstripes][width1][4][D] (4-row groups)
   uint16_t* sg_M = nullptr;     // min over d of each V row, [B][HG4 + nstripes][width1][4]

@@ -16,6 +16,8 @@
 //   b16m     the per-row minima: lane (r, q) reads 2 B of the [group][x][4] u16 array at sub-row
 //            r - 1 (row 0: sub-row 3 of the previous group)
 //   st64     8-B-per-lane non-temporal stores in the cost pass's layout (WRITE_SIZE calibration)
+//   st64t    the same with temporal stores
+//   st128    the same volume written 16 B per lane, each column's 192-B row piece by 12 lanes
 // Usage: fetch_calib [pattern ...]  (default: all); prints one JSON line per pattern with the
 // bytes it moves and the time per launch (HIP events), so the rocprofv3 pass is joined by name.
 #include <hip/hip_runtime.h>
@@ -142,12 +144,46 @@ __global__ __launch_bounds__(256) void k_cal_st64(uint16_t* __restrict__ vol) {
   }
 }
 
+// the same volume with plain (temporal) 8-B stores, and with whole 16-B-per-lane row pieces: lane
+// (c, k) of a 12-lane column group writes bytes [16k, 16k + 16) of the column's 192-B row piece
+template <bool NT>
+__global__ __launch_bounds__(256) void k_cal_st64t(uint16_t* __restrict__ vol) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const int tid = threadIdx.x, q = tid & 7, col = tid >> 3;
+  const int x = blockIdx.x * 32 + col, b = blockIdx.y;
+  if (x >= kCols) return;
+  constexpr int D = 96;
+  const uint64_t plane = (uint64_t)kCols * 4 * D;
+  uint16_t* pb = vol + (uint64_t)b * kGroups * plane;
+  for (int y = 0; y < kGroups * 4; ++y) {
+    u32x2* p = reinterpret_cast<u32x2*>(pb + (uint64_t)(y >> 2) * plane + (uint64_t)x * 4 * D + (y & 3) * D + q * 12);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if constexpr (NT) __builtin_nontemporal_store(u32x2{(uint32_t)y, (uint32_t)x + i}, p + i);
+      else p[i] = u32x2{(uint32_t)y, (uint32_t)x + i};
+    }
+  }
+}
+__global__ __launch_bounds__(192) void k_cal_st128(uint16_t* __restrict__ vol) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x, k = tid % 12, col = tid / 12;  // 16 columns x 12 lanes
+  const int x = blockIdx.x * 16 + col, b = blockIdx.y;
+  if (x >= kCols) return;
+  constexpr int D = 96;
+  const uint64_t plane = (uint64_t)kCols * 4 * D;
+  uint16_t* pb = vol + (uint64_t)b * kGroups * plane;
+  for (int y = 0; y < kGroups * 4; ++y) {
+    u32x4* p = reinterpret_cast<u32x4*>(pb + (uint64_t)(y >> 2) * plane + (uint64_t)x * 4 * D + (y & 3) * D) + k;
+    __builtin_nontemporal_store(u32x4{(uint32_t)y, (uint32_t)x, 0u, 1u}, p);
+  }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   std::vector<std::string> pats;
   for (int i = 1; i < argc; ++i) pats.push_back(argv[i]);
-  if (pats.empty()) pats = {"b128", "b32", "b96v", "b96vp", "b64v", "b16m", "st64"};
+  if (pats.empty()) pats = {"b128", "b32", "b96v", "b96vp", "b64v", "b16m", "st64", "st64t", "st128"};
   const size_t volBytes = (size_t)kPairs * kGroups * kCols * 768;  // 6.37 GB: the row pass's V at B = 64
   const size_t mBytes = (size_t)kPairs * kGroups * kCols * 8;
   uint8_t* vol;
@@ -180,6 +216,12 @@ int main(int argc, char** argv) {
       } else if (pt == "b16m") {
         bytes = (double)mBytes;
         hipLaunchKernelGGL(k_cal_b16m, dim3(kGroups, kPairs), dim3(64), 0, 0, (const uint16_t*)mv, sink);
+      } else if (pt == "st64t") {
+        bytes = (double)volBytes;
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_cal_st64t<false>), dim3((kCols + 31) / 32, kPairs), dim3(256), 0, 0, (uint16_t*)vol);
+      } else if (pt == "st128") {
+        bytes = (double)volBytes;
+        hipLaunchKernelGGL(k_cal_st128, dim3((kCols + 15) / 16, kPairs), dim3(192), 0, 0, (uint16_t*)vol);
       } else if (pt == "st64") {
         bytes = (double)volBytes;
         hipLaunchKernelGGL(k_cal_st64, dim3((kCols + 31) / 32, kPairs), dim3(256), 0, 0, (uint16_t*)vol);

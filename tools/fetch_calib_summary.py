@@ -10,7 +10,8 @@ import sys
 from collections import defaultdict
 
 KERNEL = {"b128": "k_cal_b128", "b32": "k_cal_b32", "b96v": "k_cal_rows<3, false>", "b96vp": "k_cal_rows<3, true>",
-          "b64v": "k_cal_rows<2, false>", "b16m": "k_cal_b16m", "st64": "k_cal_st64"}
+          "b64v": "k_cal_rows<2, false>", "b16m": "k_cal_b16m", "st64": "k_cal_st64",
+          "st64t": "k_cal_st64t<false>", "st128": "k_cal_st128"}
 
 
 def counters(d, name):
@@ -22,7 +23,7 @@ def counters(d, name):
         if r["Counter_Name"] == name:
             k = r["Kernel_Name"]
             for pat, kn in KERNEL.items():
-                if kn.replace(" ", "") in k.replace(" ", ""):
+                if kn.replace(" ", "") + "(" in k.replace(" ", ""):
                     per[pat].append(float(r["Counter_Value"]) * 1024)
     return per
 
