@@ -241,7 +241,7 @@ def cpu_reference_ate(L_all, R_all, K, stamps, gt, nfeatures: int) -> dict:
 # stage name (fvo_kernel_name) -> kernel symbol prefix in rocprofv3 summaries
 KERNEL_SYMBOL = {"sgbm_rows": "k_sg_rows", "sgbm_vert": "k_sg_costvert",
                  "sgbm_median": "k_sg_median", "orb_fast_score": "k_fast_nms", "orb_brief": "k_brief",
-                 "pnp_ransac": "k_pnp_hyp", "bf_argmin": "k_bf_argmin"}
+                 "pnp_ransac": "k_pnp_hyp", "bf_argmin": "k_bf_pass"}
 
 
 def shape_key(W: int, H: int, N: int, B: int, K: int) -> str:
@@ -301,7 +301,7 @@ def pmc_valu(shape: str):
     rows, src = _pmc_rows("valu_per_kernel.csv", shape)
     if not rows:
         return None
-    hot = ("k_sg_rows", "k_sg_costvert", "k_fast_nms", "k_bf_argmin", "k_pnp_hyp", "k_ba_lin", "k_blur", "k_brief")
+    hot = ("k_sg_rows", "k_sg_costvert", "k_fast_nms", "k_bf_pass", "k_pnp_hyp", "k_ba_lin", "k_blur", "k_brief")
     return {"source": src, "metric": "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles)",
             "kernels": {r["kernel"]: {"valu_util": float(r["valu_util"]),
                                       "valu_insts_per_launch": float(r["avg_SQ_INSTS_VALU"])}
@@ -525,6 +525,7 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=6, help="CPU baseline 1-thread sample, frames (0 = skip)")
     ap.add_argument("--cpu-ate", type=int, default=1, help="ATE of the CPU reference path on the ATE frames")
     ap.add_argument("--overlap-sgbm", type=int, default=1, help="SGBM of step k+1 on a side stream during step k")
+    ap.add_argument("--sgbm-last", type=int, default=0, help="front stage: ORB + BF before SGBM")
     ap.add_argument("--sgbm-mode", choices=("classic", "lpath"), default="classic",
                     help="SGBM schedule (fvo_config.sgbm_mode): classic, or the L path inside the cost pass")
     ap.add_argument("--ba-max-landmarks", type=int, default=0, help="per-window landmark cap (0 = library default)")
@@ -565,7 +566,7 @@ def main():
     sg_mode = _lib.SGBM_LPATH if args.sgbm_mode == "lpath" else _lib.SGBM_CLASSIC
     fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=B, nfeatures=args.nfeatures, device=dev,
                            ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm), sgbm_mode=sg_mode,
-                           **ba_caps)
+                           sgbm_last=bool(args.sgbm_last), **ba_caps)
     fe.prime(L_all[0], R_all[0])
     # Steps walk the rendered frames forward (1..B) then backward (B-1..0) and so on, so every
     # frame pair the front end sees -- including the carried pair across a step boundary -- is

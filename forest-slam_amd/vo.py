@@ -38,7 +38,7 @@ STATUS_SGBM_FAILED = -4
 class StereoFrontEnd:
     def __init__(self, width: int, height: int, K: np.ndarray, dist: np.ndarray, baseline: float, batch: int,
                  nfeatures: int = 500, match_right: bool = True, device=None, ba_window: int = 10,
-                 ba_iters: int = 10, overlap_sgbm: bool = False, **params):
+                 ba_iters: int = 10, overlap_sgbm: bool = False, sgbm_last: bool = False, **params):
         self.B = batch
         self.K = np.asarray(K, np.float64)
         self.dist = np.resize(np.asarray(dist, np.float64), 5)
@@ -113,6 +113,9 @@ class StereoFrontEnd:
         # replayed graph runs the step without the cross-step overlap (front stage of step k+1
         # beside the back stage of step k): capture is for launch-bound callers, not for speed.
         self.overlap_sgbm = bool(overlap_sgbm)
+        # front-stage order: SGBM first (default), or ORB + BF first and SGBM last (the previous
+        # step's back stage then starts beside the small ORB / BF blocks instead of SGBM's)
+        self.sgbm_last = bool(sgbm_last)
         self.s_sgbm = torch.cuda.Stream(dev) if self.overlap_sgbm else None
         # prime() runs on the caller's stream: the first front stage after it waits for it
         self.primed = None
@@ -180,7 +183,8 @@ class StereoFrontEnd:
             # (C) after BF the last frame's keypoints / descriptors / counts
             ctx.copy_regions(self._sgbm_pairs(L, R, n) + [(self.imgs[:n], L), (self.imgs[n:2 * n], R)])
             # SGBM first: ORB + BF first measured slower (r3 4242 vs 4284, r4 5051 vs 5227 frames/s)
-            disp = ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n], status=self.sg_status[:n])
+            if not self.sgbm_last:
+                disp = ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n], status=self.sg_status[:n])
             kp, desc, cnt = ctx.orb(self.imgs[:2 * n], out=(self.kp[:2 * n], self.desc[:2 * n], self.cnt[:2 * n]))
             # query (previous) sets: left frames then right frames; previous-left keypoints
             ctx.copy_regions([(self.q_desc[0], self.last_desc[0]), (self.q_cnt[0:1], self.last_cnt[0:1]),
@@ -195,6 +199,8 @@ class StereoFrontEnd:
             ctx.copy_regions([(self.last_kp, kp[n - 1]), (self.last_desc[0], desc[n - 1]),
                               (self.last_desc[1], desc[2 * n - 1]), (self.last_cnt[0:1], cnt[n - 1:n]),
                               (self.last_cnt[1:2], cnt[2 * n - 1:2 * n])])
+            if self.sgbm_last:
+                disp = ctx.sgbm(self.prevL[:n], self.prevR[:n], out=self.disp[:n], status=self.sg_status[:n])
             if self.ba_window:  # (a negative count -- ORB overflow -- reads as no keypoints)
                 ctx.keypoint_stereo(disp[:n], self.q_kp[:n], self.q_cnt[:n], self.K, self.baseline,
                                     out=self.kstereo[:n])

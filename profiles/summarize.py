@@ -56,7 +56,11 @@ def main(trace, fetch, write, out, shape):
         for k, v in sorted(pmc.items()):
             fe = sum(v["FETCH_SIZE"]) / max(len(v["FETCH_SIZE"]), 1)
             wr = sum(v["WRITE_SIZE"]) / max(len(v["WRITE_SIZE"]), 1)
-            # gfx950: FETCH_SIZE reports 1/2 of wide coalesced read bytes (x2); units of kB (x1024)
+            # gfx950: FETCH_SIZE reports 1/2 of the bytes read -- calibrated for 16-, 12-, 8-, 4- and
+            # 2-B-per-lane streaming loads in the row pass's own pattern (tools/fetch_calib.hip,
+            # profiles/r6/fetch_calib.csv: factor 0.500 for every width) -- so x2; WRITE_SIZE is taken
+            # as is (1.000 for write-back 8-B stores; non-temporal 8-B stores in the cost pass's
+            # pattern read 1.68x in the microbenchmark, 1.07x in the cost pass itself); units kB (x1024)
             w.writerow([k, shape, max(len(v["FETCH_SIZE"]), len(v["WRITE_SIZE"])), round(fe, 1), round(wr, 1),
                         int((2 * fe + wr) * 1024)])
     print("summaries written to", out)
