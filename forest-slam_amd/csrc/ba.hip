@@ -58,7 +58,12 @@ constexpr int kBlock = 256;
 // iteration, fewer leave the BA latency-bound.  Measured (bench.py, overlapped): 600p / 64
 // windows / 64 chunks: 16 parts 4770 frames/s, 8: 4787, 4: 4848, 2: 4556, 1: 4054; 1080p /
 // 32 windows / 256 chunks: 16 parts 1219, 8: 1120, 4: 1125.
-constexpr int kLinParts = 16, kLinChunksPerPart = 16;
+// r6: at most 12 parts -- at 1080p (16 windows per stream, 16 parts) one stream's k_ba_lin took
+// every CU and the other stream's k_ba_solve waited for it; with 12, 64 CUs stay free for it:
+// BA 1080p 3.99-4.05 -> 3.74 ms in order (16 / 15 / 14 / 12 / 10 / 8 / 6 parts: 4.03 / 3.82 / 3.77
+// / 3.74 / 3.87 / 3.93 / 4.43 ms), overlapped 1080p bench 1542-1544 -> 1545-1555 frames/s; 600p
+// (4 parts) unchanged, 3 / 2 parts slower there (1.82 / 2.29 vs 1.63 ms)
+constexpr int kLinParts = 12, kLinChunksPerPart = 16;
 // landmarks per k_ba_lin chunk at NR = 64 (half at NR = 128); measured: 32 / 16 per chunk
 // (4610 / 4404 frames/s) and two 8-wave blocks per CU (4796) lose to one 16-wave block with 64
 constexpr int kLinLPC64 = 64, kLinWavesDefault = 16;
@@ -230,6 +235,14 @@ __device__ __forceinline__ void exp_so3(const double* w, double* R) {
 }
 
 // 1 / sqrt(d): the hardware estimate refined by one Newton step (relative error ~1e-15)
+// a lane's double, read by the whole wave (two v_readlane_b32)
+__device__ __forceinline__ double rl_f64(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), src);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 __device__ __forceinline__ double rsq_r(double d) {
   const double r = __builtin_amdgcn_rsq(d);
   return r * fma(-0.5 * d * r, r, 1.5);
@@ -1161,10 +1174,12 @@ __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims 
   }
 }
 
-// With many k_ba_lin partials (NPART >= kGsumParts: 1080p / K = 20 has 16 of 128 x 128) their
-// sum is formed by the whole GPU first (k_ba_gsum, into partial 0, the order k_ba_solve's own
-// sum has), so the one block per window that assembles S reads one partial instead of NPART.
-constexpr int kGsumParts = 8;
+// With more than one k_ba_lin partial their sum is formed by the whole GPU first (k_ba_gsum,
+// into partial 0, the order k_ba_solve's own sum had), so the one block per window that
+// assembles S reads one partial instead of NPART.  r6: for every NPART >= 2 (r4/r5: >= 8, the
+// 1080p case; at 600p the solve summed 4 partials itself -- its assembly took ~0.4 of the 1.65 ms
+// BA, measured by a no-assembly ablation)
+constexpr int kGsumParts = 2;
 __global__ __launch_bounds__(256) void k_ba_gsum(void* ws, BaDims dm) {
   const BaWin v = view(ws, dm, blockIdx.x);
   const BaState* S = v.st;
@@ -1191,12 +1206,14 @@ __global__ __launch_bounds__(256) void k_ba_gsum(void* ws, BaDims dm) {
 // (identity in the padding) with row stride NP + 2 (== 2 mod 32 doubles: the 16 rows x 2
 // columns of a wave half's 16x16x4 MFMA operand fetch hit 32 distinct bank pairs).  Factor:
 // right-looking Cholesky by 16-column panels, three phases per panel —
-//   (A) the diagonal 16x16 tile by wave 0 in registers (lane = row i, column group of 4;
-//       pivots as rsq + one Newton step, columns broadcast by shuffles),
+//   (A) the diagonal 16x16 tile by wave 0 in registers (lane = row i; pivots as rsq + one
+//       Newton step; r6: the pivot and the column entries by v_readlane, no LDS round trip),
 //   (B) the panel below it, one thread per row (16-step substitution against the tile),
 //   (C) the trailing update S_IJ -= L_Ip L_Jp^T of every lower tile on
-//       v_mfma_f64_16x16x4_f64 (4 K-steps per panel), tiles spread over the 8 waves —
-// three barriers per panel instead of two per 4 columns; the update, the bulk of the
+//       v_mfma_f64_16x16x4_f64 (4 K-steps per panel), tiles spread over the waves; r6: with
+//       look-ahead -- wave 0 updates the next diagonal tile and factors it (A of the next
+//       panel) while waves 1..7 update the rest —
+// two barriers per panel (r5: three; r3: two per 4 columns); the update, the bulk of the
 // arithmetic, leaves the LDS-bound scalar loop for the matrix pipe.
 constexpr int kSolveBlock = 512, kSolveWaves = kSolveBlock / 64;
 __host__ __device__ constexpr int ba_np16(int np) { return (np + 15) & ~15; }
@@ -1221,42 +1238,52 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
     const int a = t / NP, b = t - a * NP;
     if (a >= np || b >= np) sS[a * STR + b] = a == b ? 1.0 : 0.0;
   }
-  // S = H_pp + lam diag + 1e-6 I - sum_c G_c (upper triangle, mirrored).  A thread takes 4
-  // consecutive columns b0..b0+3 of a row a (b0 from the row's diagonal 16 x 16 tile, which
-  // k_ba_lin writes in full) and loads the 4-wide slices of every partial before summing, so
-  // the partials' reads are all in flight at once.  Partial order kept (c ascending).
+  // S = H_pp + lam diag + 1e-6 I - sum_c G_c (upper triangle, mirrored), G summed by
+  // k_ba_gsum (nch == 1 whenever NPART > 1).  A thread takes 4 consecutive columns b0..b0+3 of
+  // a row a (b0 from the row's diagonal 16 x 16 tile, which k_ba_lin writes in full).  r6: all of
+  // a thread's global reads (its <= kAsmIt slices of G and the H_pp entries they need) are
+  // issued before any LDS write -- the reads go through generic pointers, so the compiler kept
+  // each iteration's read behind the previous iteration's LDS stores (one global latency per
+  // iteration, ~0.8 ms of the 1080p BA by a no-assembly ablation)
+  typedef double d4 __attribute__((ext_vector_type(4)));
   const int nq = (np + 3) / 4;  // column quads per row
-  for (int t = tid; t < np * nq; t += kSolveBlock) {
+  constexpr int kAsmIt = 8;     // ceil(np nq / kSolveBlock) <= 7 for np <= 120
+  d4 gq[kAsmIt];
+  double hq[kAsmIt][4];
+#pragma unroll
+  for (int k = 0; k < kAsmIt; ++k) {
+    const int t = tid + k * kSolveBlock;
     const int a = t / nq, b0 = 4 * (t - a * nq);
-    if (b0 + 3 < a) continue;
-    typedef double d4 __attribute__((ext_vector_type(4)));
-    d4 gs = {0.0, 0.0, 0.0, 0.0};
+    gq[k] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) hq[k][u] = 0.0;
+    if (t >= np * nq || b0 + 3 < a) continue;
     const d4* gp = reinterpret_cast<const d4*>(v.Gp + a * NR + b0);
-#pragma unroll
-    for (int c0 = 0; c0 < kLinParts; c0 += 8) {  // 8 slices in flight per batch (VGPR budget)
-      d4 part[8];
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-        if (c0 + c < nch) part[c] = gp[(int64_t)(c0 + c) * NR * NR / 4];
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-        if (c0 + c < nch) gs += part[c];
-    }
+    d4 gs = {0.0, 0.0, 0.0, 0.0};
+    for (int c = 0; c < nch; ++c) gs += gp[(int64_t)c * NR * NR / 4];  // nch == 1 but for NPART == 1
+    gq[k] = gs;
     const int fa = a / 6 + 1, ia = a - 6 * (fa - 1);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int bb = b0 + u;
+      if (bb < a || bb >= np || bb / 6 + 1 != fa) continue;
+      const int j = bb - 6 * (fa - 1);
+      hq[k][u] = S->Hpp[fa][ia * 6 - ia * (ia - 1) / 2 + (j - ia)];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kAsmIt; ++k) {
+    const int t = tid + k * kSolveBlock;
+    const int a = t / nq, b0 = 4 * (t - a * nq);
+    if (t >= np * nq || b0 + 3 < a) continue;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int bb = b0 + u;
       if (bb < a || bb >= np) continue;
-      const int fb = bb / 6 + 1;
-      double hv = 0.0;
-      if (fa == fb) {
-        const int i = ia, j = bb - 6 * (fb - 1);
-        const int q = i * 6 - i * (i - 1) / 2 + (j - i);
-        hv = S->Hpp[fa][q];
-        if (i == j) hv += lam * hv + 1e-6;
-      }
-      sS[a * STR + bb] = hv - gs[u];
-      sS[bb * STR + a] = hv - gs[u];
+      double hv = hq[k][u];
+      if (bb == a) hv += lam * hv + 1e-6;
+      sS[a * STR + bb] = hv - gq[k][u];
+      sS[bb * STR + a] = hv - gq[k][u];
     }
   }
   for (int a = tid; a < NP; a += kSolveBlock) {
@@ -1272,38 +1299,57 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
   }
   __syncthreads();
   typedef double d4 __attribute__((ext_vector_type(4)));
-  for (int p = 0; p < NTl; ++p) {
-    const int c0 = 16 * p;
-    // (A) diagonal tile: lane (i = lane & 15, cg = lane >> 4) holds S[c0 + i][c0 + 4 cg .. +3]
-    if (wid == 0) {
-      const int i = lane & 15, cg = lane >> 4;
-      double d[4];
+  // (A) the diagonal tile of panel p on wave 0: lane i (< 16; lanes 16..63 mirror row i & 15)
+  // holds row i of the tile in registers; the pivot and every L[j][c] an update needs are
+  // wave-uniform reads (v_readlane) of the lane that owns them, so the column chain has no LDS
+  // round trip (r5: three ds_bpermute per column).  Pivots as rsq + one Newton step.
+  auto factor_diag = [&](int p) {
+    const int c0 = 16 * p, i = lane & 15;
+    double r[16];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) d[q] = sS[(c0 + i) * STR + c0 + 4 * cg + q];
-      bool bad = false;
+    for (int q = 0; q < 16; ++q) r[q] = sS[(c0 + i) * STR + c0 + q];
+    bool bad = false;
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const int colane = 16 * (c >> 2);  // lanes holding column c: colane + row
-        const double piv = __shfl(d[c & 3], colane + c, 64);
-        bad |= !(piv > 0.0);
-        const double rp = rsq_r(piv);
-        const double vc = d[c & 3] * rp;  // column c of L on the lanes of column group c >> 2
-        const double lic = __shfl(vc, colane + i, 64);
+    for (int c = 0; c < 16; ++c) {
+      const double piv = rl_f64(r[c], c);
+      bad |= !(piv > 0.0);
+      const double rp = rsq_r(piv);
+      const double lic = r[c] * rp;  // L[i][c] (the diagonal piv rp on row c)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int j = 4 * cg + q;
-          const double ljc = __shfl(vc, colane + j, 64);
-          if (j > c && i >= j) d[q] -= lic * ljc;
-        }
-        if (cg == (c >> 2)) d[c & 3] = i >= c ? vc : 0.0;
-        if (lane == 0) rinv[c0 + c] = rp;
+      for (int j = c + 1; j < 16; ++j) {
+        const double ljc = rl_f64(lic, j);
+        if (i >= j) r[j] -= lic * ljc;
       }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sS[(c0 + i) * STR + c0 + 4 * cg + q] = d[q];
-      if (bad && lane == 0) s_fail = 1;
+      r[c] = i >= c ? lic : 0.0;
+      if (lane == 0) rinv[c0 + c] = rp;
     }
-    __syncthreads();
-    if (s_fail) break;  // uniform: read after the barrier
+    if (lane < 16) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sS[(c0 + i) * STR + c0 + q] = r[q];
+    }
+    if (bad && lane == 0) s_fail = 1;
+  };
+  // S_IJ -= L_Ip L_Jp^T of one lower tile on MFMA (A[i][k] = L[16I + i][c0 + k], B[k][j] =
+  // L[16J + j][c0 + k]), 4 K-steps
+  auto tile_upd = [&](int c0, int I, int J) {
+    const double* pa = sS + (16 * I + (lane & 15)) * STR + c0 + (lane >> 4);
+    const double* pb = sS + (16 * J + (lane & 15)) * STR + c0 + (lane >> 4);
+    const double a0 = pa[0], a1 = pa[4], a2 = pa[8], a3 = pa[12];
+    const double b0 = pb[0], b1 = pb[4], b2 = pb[8], b3 = pb[12];
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a3, b3, acc, 0, 0, 0);
+    double* pc = sS + (16 * I + (lane >> 4)) * STR + 16 * J + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pc[4 * r * STR] -= acc[r];
+  };
+  if (wid == 0) factor_diag(0);
+  __syncthreads();
+  for (int p = 0; p < NTl; ++p) {
+    if (s_fail) break;  // uniform: read after the barrier that follows the tile's factorisation
+    const int c0 = 16 * p;
     // (B) the panel's rows below the tile: L_Ip = S_Ip L_pp^-T, one thread per row
     const int nb = NP - c0 - 16;
     if (tid < nb) {
@@ -1323,28 +1369,26 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
       for (int c = 0; c < 16; ++c) row[c] = x[c];
     }
     __syncthreads();
-    // (C) trailing update of the lower tiles (I, J), p < J <= I < NTl, on MFMA:
-    // acc = L_Ip L_Jp^T (A[i][k] = L[16I + i][c0 + k], B[k][j] = L[16J + j][c0 + k])
+    // (C) trailing update of the lower tiles (I, J), p < J <= I < NTl, with look-ahead: wave 0
+    // updates the next diagonal tile (p + 1, p + 1) and factors it at once (A of panel p + 1)
+    // while waves 1..7 update every other tile -- two barriers per panel instead of three, and
+    // the next tile's serial factorisation overlaps this panel's update (r6; each element still
+    // gets the same updates in the same panel order: bit-identical)
     const int m = NTl - p - 1;
-    for (int t = wid; t < m * (m + 1) / 2; t += kSolveWaves) {
-      int I = p + 1, rem = t;
-      while (rem >= I - p) {
-        rem -= I - p;
-        ++I;
+    if (m > 0) {
+      if (wid == 0) {
+        tile_upd(c0, p + 1, p + 1);
+        factor_diag(p + 1);
+      } else {
+        for (int t = wid; t < m * (m + 1) / 2; t += kSolveWaves - 1) {
+          int I = p + 1, rem = t;
+          while (rem >= I - p) {
+            rem -= I - p;
+            ++I;
+          }
+          tile_upd(c0, I, p + 1 + rem);
+        }
       }
-      const int J = p + 1 + rem;
-      const double* pa = sS + (16 * I + (lane & 15)) * STR + c0 + (lane >> 4);
-      const double* pb = sS + (16 * J + (lane & 15)) * STR + c0 + (lane >> 4);
-      const double a0 = pa[0], a1 = pa[4], a2 = pa[8], a3 = pa[12];
-      const double b0 = pb[0], b1 = pb[4], b2 = pb[8], b3 = pb[12];
-      d4 acc = {0.0, 0.0, 0.0, 0.0};
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a3, b3, acc, 0, 0, 0);
-      double* pc = sS + (16 * I + (lane >> 4)) * STR + 16 * J + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) pc[4 * r * STR] -= acc[r];
     }
     __syncthreads();
   }
