@@ -420,7 +420,7 @@ __device__ __attribute__((noinline)) void sg_run_L(SgLink lk, lds_cu32* ring, in
 }
 
 template <int D, int CB, int G, bool LP>
-__global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
+__global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : (G == 8 ? (D <= 96 ? 4 : 3) : 1))) void k_sg_costvert(const uint8_t* __restrict__ Limg, const uint8_t* __restrict__ Rimg,
                                                     int64_t stride, int pitch, SgParams p, uint16_t* __restrict__ Vvol,
                                                     uint16_t* __restrict__ Mvol, SgLink lk) {
   constexpr int DQ = D / G, PQ = DQ / 2, NV2 = DQ / 4;  // NV2 = 0: a run of 6 (G = 16) moves as words
@@ -436,10 +436,12 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void
   // the 4 rows' lanes (3 words apart within a row) hit disjoint banks
   constexpr int RW = LP ? CB * D / 2 + 16 : 1;
   __shared__ uint8_t sImg[4][NLI + NRI];                            // image rows (ring by row & 3), L then R
-  __shared__ uint32_t sCh[kCX + 2 + NRC + 2];                       // (Sobel, intensity), L then R
-  __shared__ uint32_t sU[6][kCX];                                  // left BT words per channel (splat)
-  __shared__ uint32_t sV[6][NRC];                                  // right BT words per channel (pixel pairs)
-  __shared__ __attribute__((aligned(16))) uint16_t sPC[kCX][D];    // pixel cost
+  // per hsum row of a call (two per call in the classic schedule, one under LP)
+  constexpr int NRS = LP ? 1 : 2;
+  __shared__ uint32_t sCh[NRS][kCX + 2 + NRC + 2];                  // (Sobel, intensity), L then R
+  __shared__ uint32_t sU[NRS][6][kCX];                             // left BT words per channel (splat)
+  __shared__ uint32_t sV[NRS][6][NRC];                             // right BT words per channel (pixel pairs)
+  __shared__ __attribute__((aligned(16))) uint16_t sPC[NRS][kCX][D];  // pixel cost
   __shared__ uint32_t sRing[LP ? 4 : 1][RW];
   __shared__ int sUnit;
   const int tid = threadIdx.x, lane = tid & 63, q = lane % G;
@@ -480,23 +482,37 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void
 
   // ---- image rows: a 4-slot LDS ring (slot = image row & 3) of the block's core columns (+2 each
   // side) of both images; hsum row r reads rows r-1, r, r+1 (clamped), so each new hsum row stages
-  // one new image row, loaded one hsum row ahead into a register (one byte per thread)
+  // one new image row, loaded one call ahead into registers (one byte per thread and row; up to
+  // two rows wait, A and B, for a two-row call)
   const uint8_t* colsrc[PER];  // this thread's bytes of a staged row (clamped columns)
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int jb = min(tid + NT * k, NIMG - 1);
     colsrc[k] = jb < NLI ? Lb + min(max(xl0 - 2 + jb, 0), W - 1) : Rb + min(max(xr0 - 2 + (jb - NLI), 0), W - 1);
   }
-  uint32_t pre[PER];
-  int pre_row = -1;  // image row held in `pre` (-1: none)
-  auto put_row = [&](int row) {
+  uint32_t preA[PER], preB[PER];
+  int pendA = -1, pendB = -1;  // image rows waiting in preA / preB (-1: none)
+  int hi = -1;                 // the highest image row in the ring or waiting
+  auto put_row = [&](const uint32_t* pr, int row) {
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-      if (tid + NT * k < NIMG) sImg[row & 3][tid + NT * k] = (uint8_t)pre[k];
+      if (tid + NT * k < NIMG) sImg[row & 3][tid + NT * k] = (uint8_t)pr[k];
   };
-  auto load_row = [&](int row) {
+  auto load_row = [&](uint32_t* pr, int row) {
 #pragma unroll
-    for (int k = 0; k < PER; ++k) pre[k] = colsrc[k][(int64_t)row * pitch];
+    for (int k = 0; k < PER; ++k) pr[k] = colsrc[k][(int64_t)row * pitch];
+  };
+  // a call's staging: the waiting rows into the ring, then the rows up to `upto` (<= 2 of them)
+  // loaded for the next call.  A call for hsum rows e.. (NR of them) needs image rows up to e + NR
+  // and loads up to e + NR + 2, so the next call -- one or two rows -- finds its rows waiting, and
+  // the ring (the 4 most recent rows) still holds row e + NR - 2, the first one it reads
+  auto stage = [&](int upto) {
+    if (pendA >= 0) put_row(preA, pendA);
+    if (pendB >= 0) put_row(preB, pendB);
+    pendA = pendB = -1;
+    upto = min(upto, H - 1);
+    if (hi + 1 <= upto) { load_row(preA, hi + 1); pendA = ++hi; }
+    if (hi + 1 <= upto) { load_row(preB, hi + 1); pendB = ++hi; }
   };
   // ---- per-thread pixel-cost tasks (8 disparities of one column each), fixed for the block:
   // left word index kl, right pair index of the first disparity pair, output offset
@@ -514,18 +530,17 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void
     tk_jr[m] = tk_kl[m] + (D - 1) - d0;  // right pixel of disparity d0 (pairs: d0 + 2j at tk_jr - 2j)
     tk_out[m] = (t < NSLOT && i < kCX) ? i * D + d0 : -1;
   }
-  // hsum row r from the ring -> acc (this lane's column and disparity run); `next` = the hsum
-  // row after it (-1: none), whose new image row is loaded here
-  auto hs_row = [&](uint32_t* acc, int r, int next) {
-    if (pre_row >= 0) put_row(pre_row);
-    pre_row = -1;
-    if (next >= 0 && next + 1 <= H - 1) {
-      load_row(next + 1);
-      pre_row = next + 1;
-    }
+  // hsum rows e .. e + NR - 1 (rows past H - 1 clamp to it) from the ring -> acc0 (, acc1): this
+  // lane's column and disparity run.  NR = 2 (classic schedule): two rows per phase, one barrier
+  // per phase for both (r6: 4 barriers per two rows instead of per row)
+  auto hs_rows = [&](auto nr_t, uint32_t* acc0, uint32_t* acc1, int e) {
+    constexpr int NR = decltype(nr_t)::value;
+    stage(e + NR + 2);
     __syncthreads();
     // channel words at core-1 .. core+1 of both images; borders (x < 1, x >= W-1) read ftzero
-    {
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      const int r = min(e + rr, H - 1);
       const uint8_t* r0 = sImg[(r > 0 ? r - 1 : r) & 3];
       const uint8_t* r1 = sImg[r & 3];
       const uint8_t* r2 = sImg[(r < H - 1 ? r + 1 : r) & 3];
@@ -539,7 +554,7 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void
           const int sb = (r1[jj + 1] - r1[jj - 1]) * 2 + r0[jj + 1] - r0[jj - 1] + r2[jj + 1] - r2[jj - 1];
           wv = (uint32_t)clip(sb) | ((uint32_t)r1[jj] << 16);
         }
-        sCh[left ? k : (kCX + 2) + k] = wv;
+        sCh[rr][left ? k : (kCX + 2) + k] = wv;
       }
     }
     __syncthreads();
@@ -555,11 +570,13 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void
       mn = vmin(vmin(hl, hr), u);
       mx = __builtin_elementwise_max(__builtin_elementwise_max(hl, hr), u);
     };
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr)
     for (int j = tid; j < nl + nr; j += NT) {
       const bool left = j < nl;
       const int k = left ? j : j - nl;
       const int x = left ? xl0 + k : xr0 + k;
-      const uint32_t* ch = left ? sCh : sCh + (kCX + 2);
+      const uint32_t* ch = left ? sCh[rr] : sCh[rr] + (kCX + 2);
       u16x2 u, mn, mx;
       btw(ch, k, x, u, mn, mx);
       if (left) {
@@ -567,15 +584,15 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void
 #pragma unroll
         for (int c = 0; c < 2; ++c)
 #pragma unroll
-          for (int e = 0; e < 3; ++e) sU[3 * c + e][k] = as_u(splat(c ? as_u(w3[e]) >> 16 : as_u(w3[e])));
+          for (int e = 0; e < 3; ++e) sU[rr][3 * c + e][k] = as_u(splat(c ? as_u(w3[e]) >> 16 : as_u(w3[e])));
       } else if (k > 0) {
         u16x2 up, mnp, mxp;  // the right pixel k - 1
         btw(ch, k - 1, x - 1, up, mnp, mxp);
         const uint32_t a3[3] = {as_u(u), as_u(mn), as_u(mx)}, b3[3] = {as_u(up), as_u(mnp), as_u(mxp)};
 #pragma unroll
         for (int e = 0; e < 3; ++e) {
-          sV[e][k] = (a3[e] & 0xFFFFu) | (b3[e] << 16);             // x-Sobel (k, k-1)
-          sV[3 + e][k] = (a3[e] >> 16) | (b3[e] & 0xFFFF0000u);     // intensity (k, k-1)
+          sV[rr][e][k] = (a3[e] & 0xFFFFu) | (b3[e] << 16);             // x-Sobel (k, k-1)
+          sV[rr][3 + e][k] = (a3[e] >> 16) | (b3[e] & 0xFFFF0000u);     // intensity (k, k-1)
         }
       }
     }
@@ -583,12 +600,14 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void
     // pixel costs of the kCX (clamped) columns x D disparities, 8 disparities per task, two per
     // packed operation: cost = BT(x-Sobel) + (BT(intensity) >> 2)
 #pragma unroll
+    for (int rr = 0; rr < NR; ++rr)
+#pragma unroll
     for (int m = 0; m < NTASK; ++m) {
       if (tk_out[m] < 0) continue;
       const int kl = tk_kl[m];
       u16x2 uu[6];
 #pragma unroll
-      for (int e = 0; e < 6; ++e) uu[e] = as_v(sU[e][kl]);
+      for (int e = 0; e < 6; ++e) uu[e] = as_v(sU[rr][e][kl]);
       uint32_t out[4];
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
@@ -596,7 +615,7 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void
         u16x2 mc[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-          const u16x2 v = as_v(sV[3 * c][jr]), v0 = as_v(sV[3 * c + 1][jr]), v1 = as_v(sV[3 * c + 2][jr]);
+          const u16x2 v = as_v(sV[rr][3 * c][jr]), v0 = as_v(sV[rr][3 * c + 1][jr]), v1 = as_v(sV[rr][3 * c + 2][jr]);
           const u16x2 u = uu[3 * c], u0 = uu[3 * c + 1], u1 = uu[3 * c + 2];
           const u16x2 cA = __builtin_elementwise_max(__builtin_elementwise_sub_sat(u, v1), __builtin_elementwise_sub_sat(v0, u));
           const u16x2 cB = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, u1), __builtin_elementwise_sub_sat(u0, v));
@@ -604,45 +623,53 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void
         }
         out[h] = as_u(mc[0] + (mc[1] >> 2));
       }
-      *reinterpret_cast<uint4*>(&sPC[0][0] + tk_out[m]) = make_uint4(out[0], out[1], out[2], out[3]);
+      *reinterpret_cast<uint4*>(&sPC[rr][0][0] + tk_out[m]) = make_uint4(out[0], out[1], out[2], out[3]);
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < PQ; ++k) acc[k] = 0;
+    for (int rr = 0; rr < NR; ++rr) {
+      uint32_t* acc = rr == 0 ? acc0 : acc1;
 #pragma unroll
-    for (int t = 0; t < 7; ++t) {
-      if constexpr (DQ % 4 == 0) {
-        const uint2* src = reinterpret_cast<const uint2*>(&sPC[col + t][q * DQ]);
+      for (int k = 0; k < PQ; ++k) acc[k] = 0;
 #pragma unroll
-        for (int k = 0; k < NV2; ++k) {
-          const uint2 w2 = src[k];
-          acc[2 * k] = as_u(as_v(acc[2 * k]) + as_v(w2.x));
-          acc[2 * k + 1] = as_u(as_v(acc[2 * k + 1]) + as_v(w2.y));
+      for (int t = 0; t < 7; ++t) {
+        if constexpr (DQ % 4 == 0) {
+          const uint2* src = reinterpret_cast<const uint2*>(&sPC[rr][col + t][q * DQ]);
+#pragma unroll
+          for (int k = 0; k < NV2; ++k) {
+            const uint2 w2 = src[k];
+            acc[2 * k] = as_u(as_v(acc[2 * k]) + as_v(w2.x));
+            acc[2 * k + 1] = as_u(as_v(acc[2 * k + 1]) + as_v(w2.y));
+          }
+        } else {
+          const uint32_t* src = reinterpret_cast<const uint32_t*>(&sPC[rr][col + t][q * DQ]);
+#pragma unroll
+          for (int k = 0; k < PQ; ++k) acc[k] = as_u(as_v(acc[k]) + as_v(src[k]));
         }
-      } else {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(&sPC[col + t][q * DQ]);
-#pragma unroll
-        for (int k = 0; k < PQ; ++k) acc[k] = as_u(as_v(acc[k]) + as_v(src[k]));
       }
     }
-    // no trailing barrier: the next row's first LDS write (its image row, in a ring slot no
-    // phase of this row reads) comes before its first barrier, and every later write after it
+    // no trailing barrier: the next call's first LDS writes (its image rows, into ring slots no
+    // phase still running reads -- those finished before this call's third barrier) come before
+    // its first barrier, and every later write after it
   };
+  const std::integral_constant<int, 1> one{};
+  const std::integral_constant<int, 2> two{};
 
   // window: win[k] = hsum(clamp(start - 3 + k)), k = 0..6, for the output row start
   uint32_t win[7][PQ], crun[PQ], st[PQ];
   // the first hsum row's image rows (start - 1, start, start + 1, clamped) straight into the ring
-  for (int row = max(start - 1, 0); row <= min(start + 1, H - 1); ++row) {
-    load_row(row);
-    put_row(row);
+  hi = min(start + 1, H - 1);
+  for (int row = max(start - 1, 0); row <= hi; ++row) {
+    load_row(preA, row);
+    put_row(preA, row);
   }
-  hs_row(win[6], start, start + 1 <= H - 1 ? start + 1 : -1);
+  hs_rows(one, win[6], nullptr, start);
   for (int r = start + 1; r <= start + 3; ++r) {
 #pragma unroll
     for (int k = 0; k < 6; ++k)
 #pragma unroll
       for (int j = 0; j < PQ; ++j) win[k][j] = win[k + 1][j];
-    if (r <= H - 1) hs_row(win[6], r, r + 1 <= H - 1 ? r + 1 : -1);
+    if (r <= H - 1) hs_rows(one, win[6], nullptr, r);
   }
   // win[3..6] = hs(start..start+3 clamped); rows above start clamp to start
 #pragma unroll
@@ -667,7 +694,7 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void
   auto vrow = [&](int y) {
     minPrev = hstepG<PQ, G>(st, crun, q, P1, minPrev, p.P2);
 #pragma unroll
-    for (int k = 0; k < PER; ++k) asm volatile("" : "+v"(pre[k]) :: "memory");
+    for (int k = 0; k < PER; ++k) asm volatile("" : "+v"(preA[k]), "+v"(preB[k]) :: "memory");
     // output rows, and for s > 0 the row above the stripe's first output row (the row pass
     // inverts the recurrence at first_out from it): group HG4 + s, sub-row 0
     const bool out_row = y >= first_out, top_row = s > 0 && y == first_out - 1;
@@ -709,28 +736,57 @@ __global__ __launch_bounds__(G * CB, LP ? 4 : (G == 16 && D <= 96 ? 6 : 1)) void
   };
   vrow(start);
   // rows start+1, ...: the 7-row window is a ring -- row y = start + t replaces slot (t-1) mod 7
-  // (the row leaving, y-4) by the row entering (y+3); the loop is unrolled by 7 so every slot
-  // index is static (no register shuffling).  Below H-1 the entering row is clamped, i.e. the
-  // last one entered (slot (t-2) mod 7).
+  // (the row leaving, y-4) by the row entering (y+3); the loop is unrolled by 7 (pairs of rows:
+  // 14) so every slot index is static (no register shuffling).  Below H-1 the entering row is
+  // clamped, i.e. the last one entered (slot (t-2) mod 7).
+  auto enter = [&](int ph, const uint32_t* nw) {
+#pragma unroll
+    for (int j = 0; j < PQ; ++j) {
+      crun[j] = as_u(as_v(crun[j]) - as_v(win[ph][j]) + as_v(nw[j]));
+      win[ph][j] = nw[j];
+    }
+  };
+  if constexpr (!LP) {
+    // two output rows per step: their entering hsum rows y + 3, y + 4 from one two-row call (the
+    // second clamps to H - 1 when past it; a call at or past H - 1 is not needed)
 #pragma unroll 1
-  for (int y0 = start + 1; y0 < end; y0 += 7) {
+    for (int y0 = start + 1; y0 < end; y0 += 14) {
 #pragma unroll
-    for (int ph = 0; ph < 7; ++ph) {
-      const int y = y0 + ph;
-      if (y >= end) break;
-      uint32_t nw[PQ];
-      if (y + 3 <= H - 1) {
-        hs_row(nw, y + 3, y + 4 <= H - 1 ? y + 4 : -1);
-      } else {
+      for (int pp = 0; pp < 7; ++pp) {
+        const int y = y0 + 2 * pp;
+        if (y >= end) break;
+        const int ph0 = (2 * pp) % 7, ph1 = (2 * pp + 1) % 7;
+        uint32_t nw0[PQ], nw1[PQ];
+        if (y + 3 <= H - 1) {
+          hs_rows(two, nw0, nw1, y + 3);
+        } else {
 #pragma unroll
-        for (int j = 0; j < PQ; ++j) nw[j] = win[(ph + 6) % 7][j];
+          for (int j = 0; j < PQ; ++j) nw0[j] = nw1[j] = win[(ph0 + 6) % 7][j];
+        }
+        enter(ph0, nw0);
+        vrow(y);
+        if (y + 1 >= end) break;
+        enter(ph1, nw1);
+        vrow(y + 1);
       }
+    }
+  } else {
+#pragma unroll 1
+    for (int y0 = start + 1; y0 < end; y0 += 7) {
 #pragma unroll
-      for (int j = 0; j < PQ; ++j) {
-        crun[j] = as_u(as_v(crun[j]) - as_v(win[ph][j]) + as_v(nw[j]));
-        win[ph][j] = nw[j];
+      for (int ph = 0; ph < 7; ++ph) {
+        const int y = y0 + ph;
+        if (y >= end) break;
+        uint32_t nw[PQ];
+        if (y + 3 <= H - 1) {
+          hs_rows(one, nw, nullptr, y + 3);
+        } else {
+#pragma unroll
+          for (int j = 0; j < PQ; ++j) nw[j] = win[(ph + 6) % 7][j];
+        }
+        enter(ph, nw);
+        vrow(y);
       }
-      vrow(y);
     }
   }
 }
