@@ -43,6 +43,10 @@ __device__ __forceinline__ u16x2 as_v(uint32_t x) { return __builtin_bit_cast(u1
 __device__ __forceinline__ uint32_t as_u(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ u16x2 vmin(u16x2 a, u16x2 b) { return __builtin_elementwise_min(a, b); }
 __device__ __forceinline__ u16x2 splat(uint32_t s) { return as_v((s & 0xFFFFu) | (s << 16)); }
+// (m + P2) in both halves for a path minimum m: one v_mad_u32_u24 (m * 0x10001 + P2 * 0x10001)
+// instead of add + shift + and_or.  Exact: m <= 49 x the largest pixel cost + P2, so m + P2 <
+// 3 (49 (2 ftzero + 63) + P2) <= 0xFFFF (sgbm_init) and no carry crosses the halves.
+__device__ __forceinline__ u16x2 splat_p2(uint32_t m, uint32_t P2) { return as_v(__umul24(m, 0x10001u) + P2 * 0x10001u); }
 
 struct SgParams {
   int W, H, D, minD, minX1, width1, P1, P2, ftzero, disp12, ss, ov, nstripes;
@@ -139,7 +143,7 @@ __device__ __forceinline__ uint32_t hstepG(uint32_t* st, const uint32_t* c, int 
   }
   const uint32_t lo0 = q == 0 ? (kSent << 16) : prevLast;
   const uint32_t hiN = q == G - 1 ? kSent : nextFirst;
-  const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
+  const u16x2 mp2 = splat_p2(minPrev, P2), mpv = splat(minPrev);
   u16x2 mn = splat(0xFFFF);
   uint32_t oldk = 0;
 #pragma unroll
@@ -187,7 +191,7 @@ __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q
   const uint32_t nextFirst = qperm<kQNext>(st[0]);
   const uint32_t lo0 = q == 0 ? (kSent << 16) : prevLast;
   const uint32_t hiN = q == 3 ? kSent : nextFirst;
-  const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
+  const u16x2 mp2 = splat_p2(minPrev, P2), mpv = splat(minPrev);
   u16x2 mn = splat(0xFFFF);
   uint32_t oldk = 0;
 #pragma unroll
@@ -226,7 +230,7 @@ __device__ __forceinline__ uint32_t step16(uint32_t* st, const uint32_t* c, int 
   // a row's lanes 0 / 15 have no left / right neighbour: the sentinel there
   const uint32_t lo0 = dshift_or<kRShr1>(st[PQ - 1], q == 0 ? kSent << 16 : 0u);
   const uint32_t hiN = dshift_or<kRShl1>(st[0], q == 15 ? kSent : 0u);
-  const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
+  const u16x2 mp2 = splat_p2(minPrev, P2), mpv = splat(minPrev);
   u16x2 mn = splat(0xFFFF);
   uint32_t oldk = 0;
 #pragma unroll
@@ -256,7 +260,7 @@ __device__ __forceinline__ void derive16(const uint32_t* vp, const uint32_t* v, 
   // a row's lanes 0 / 15 have no left / right neighbour: the sentinel there
   const uint32_t lo0 = dshift_or<kRShr1>(vp[PQ - 1], q == 0 ? kSent << 16 : 0u);
   const uint32_t hiN = dshift_or<kRShl1>(vp[0], q == 15 ? kSent : 0u);
-  const u16x2 mp2 = splat(m + P2), mpv = splat(m);
+  const u16x2 mp2 = splat_p2(m, P2), mpv = splat(m);
 #pragma unroll
   for (int k = 0; k < PQ; ++k) {
     const uint32_t cur = vp[k];
