@@ -143,7 +143,7 @@ __device__ __forceinline__ uint32_t hstepG(uint32_t* st, const uint32_t* c, int 
   }
   const uint32_t lo0 = q == 0 ? (kSent << 16) : prevLast;
   const uint32_t hiN = q == G - 1 ? kSent : nextFirst;
-  const u16x2 mp2 = splat_p2(minPrev, P2), mpv = splat(minPrev);
+  const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
   u16x2 mn = splat(0xFFFF);
   uint32_t oldk = 0;
 #pragma unroll
@@ -191,7 +191,7 @@ __device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q
   const uint32_t nextFirst = qperm<kQNext>(st[0]);
   const uint32_t lo0 = q == 0 ? (kSent << 16) : prevLast;
   const uint32_t hiN = q == 3 ? kSent : nextFirst;
-  const u16x2 mp2 = splat_p2(minPrev, P2), mpv = splat(minPrev);
+  const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
   u16x2 mn = splat(0xFFFF);
   uint32_t oldk = 0;
 #pragma unroll
