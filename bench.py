@@ -526,6 +526,8 @@ def main():
     ap.add_argument("--cpu-ate", type=int, default=1, help="ATE of the CPU reference path on the ATE frames")
     ap.add_argument("--overlap-sgbm", type=int, default=1, help="SGBM of step k+1 on a side stream during step k")
     ap.add_argument("--sgbm-last", type=int, default=0, help="front stage: ORB + BF before SGBM")
+    ap.add_argument("--births-ahead", type=int, default=0,
+                    help="local BA's birth counting on a side stream beside PnP (fvo_ba_count_births)")
     ap.add_argument("--sgbm-mode", choices=("classic", "lpath"), default="classic",
                     help="SGBM schedule (fvo_config.sgbm_mode): classic, or the L path inside the cost pass")
     ap.add_argument("--ba-max-landmarks", type=int, default=0, help="per-window landmark cap (0 = library default)")
@@ -566,7 +568,7 @@ def main():
     sg_mode = _lib.SGBM_LPATH if args.sgbm_mode == "lpath" else _lib.SGBM_CLASSIC
     fe = vo.StereoFrontEnd(W, H, seq.K, synth.DIST_L, synth.BASELINE, batch=B, nfeatures=args.nfeatures, device=dev,
                            ba_window=args.ba_window, overlap_sgbm=bool(args.overlap_sgbm), sgbm_mode=sg_mode,
-                           sgbm_last=bool(args.sgbm_last), **ba_caps)
+                           sgbm_last=bool(args.sgbm_last), births_ahead=bool(args.births_ahead), **ba_caps)
     fe.prime(L_all[0], R_all[0])
     # Steps walk the rendered frames forward (1..B) then backward (B-1..0) and so on, so every
     # frame pair the front end sees -- including the carried pair across a step boundary -- is

@@ -66,6 +66,7 @@ SIGNATURES = {
     "fvo_ba_windows": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, ctypes.c_double, _P, _I, _I,
                                       _P, _P, _P]),
     "fvo_ba_landmarks": (ctypes.c_int, [_P, _I, _P, _P, _P]),
+    "fvo_ba_count_births": (ctypes.c_int, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "fvo_gather_matches": (ctypes.c_int, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P]),
     "fvo_find_essential": (ctypes.c_int, [_P, _P, _P, _P, _I, _I, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                           ctypes.c_double, ctypes.c_double, _I, _P, _P, _P, _P]),
@@ -319,6 +320,15 @@ class Context:
                                           float(baseline), isig, nl, int(iterations), _ptr(Tout), _ptr(stats),
                                           _stream(self.device)))
         return Tout, stats
+
+    def ba_count_births(self, matches, nmatch, stereo, first_end, n_windows, first_valid):
+        """fvo_ba_count_births: the landmark-birth counting of the next ba_windows call with the
+        same frame arrays and window range, issued ahead on the current stream (it needs neither
+        T_rel nor the keypoints)."""
+        F, cap = matches.shape[0], matches.shape[1]
+        self._check(self.L.fvo_ba_count_births(self.h, _ptr(matches), _ptr(nmatch), _ptr(stereo), F, cap,
+                                               int(first_end), int(n_windows), int(first_valid),
+                                               _stream(self.device)))
 
     def ba_landmarks(self, window: int, out=None):
         """Refined landmarks of one window of the last ba_windows call (device tensors,

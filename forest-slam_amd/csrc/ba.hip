@@ -1735,12 +1735,13 @@ int ba_stereo_run(fvo_ctx* ctx, const int16_t* disp, const float* kp, const int3
 namespace {
 // build + LM iterations + final transform of windows [w0, w0 + nw) on stream s
 void ba_windows_launch(fvo_ctx* ctx, const BaIn& in, const BaCam& cam, const BaDims& d, int w0, int nw, int first_end,
-                       int first_valid, int iters, double* Tout, double* stats, hipStream_t s) {
+                       int first_valid, int iters, double* Tout, double* stats, hipStream_t s, bool births_done) {
   void* ws = static_cast<char*>(ctx->ba_ws) + (int64_t)d.win * w0;
   const int fe = first_end + w0;
   const size_t shb = build_shm(d);
   if (shb > (size_t)d.cap) {  // the match maps fit in LDS: the parallel construction
-    hipLaunchKernelGGL(k_ba_births, dim3(nw, d.K - 1), dim3(kBirthBlock), shb, s, in, ws, d, fe, first_valid);
+    if (!births_done)  // (fvo_ba_count_births ran it ahead for this window range)
+      hipLaunchKernelGGL(k_ba_births, dim3(nw, d.K - 1), dim3(kBirthBlock), shb, s, in, ws, d, fe, first_valid);
     hipLaunchKernelGGL(k_ba_emit, dim3(nw, d.K - 1), dim3(kBirthBlock), shb, s, in, ws, d, fe, first_valid);
     hipLaunchKernelGGL(k_ba_lists, dim3(nw, d.K), dim3(kBirthBlock), 0, s, in, ws, d, fe, first_valid);
   } else {
@@ -1784,6 +1785,11 @@ int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* mat
   BaIn in{kp, nkp, matches, nmatch, reinterpret_cast<const float4*>(stereo), Trel, {}, nlev};
   for (int i = 0; i < nlev; ++i) in.isig2[i] = inv_sigma2[i];
   const BaCam cam{K[0], K[4], K[2], K[5], baseline};
+  // the birth counts of exactly this call's window range already computed (fvo_ba_count_births)?
+  const auto& pb = ctx->ba_births;
+  const bool births_done = pb.valid && pb.matches == matches && pb.stereo == stereo && pb.nframes == nframes &&
+                           pb.first_end == first_end && pb.nwin == nwin && pb.first_valid == first_valid;
+  ctx->ba_births.valid = false;
   // The windows are independent: the batch is split in two halves whose LM sequences run on
   // two streams, so one half's latency-bound kernels (build, the per-window solve on one
   // block each) overlap the other half's whole-GPU kernels instead of leaving most CUs idle.
@@ -1794,14 +1800,42 @@ int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* mat
     FVO_HIP(ctx, hipStreamWaitEvent(ctx->ba_s2, ctx->ba_fork, 0));
   }
   FVO_TIMED(ctx, KN_BA_SOLVE, s, {
-    ba_windows_launch(ctx, in, cam, d, 0, nh, first_end, first_valid, iters, Tout, stats, s);
-    if (two) ba_windows_launch(ctx, in, cam, d, nh, nwin - nh, first_end, first_valid, iters, Tout, stats, ctx->ba_s2);
+    ba_windows_launch(ctx, in, cam, d, 0, nh, first_end, first_valid, iters, Tout, stats, s, births_done);
+    if (two)
+      ba_windows_launch(ctx, in, cam, d, nh, nwin - nh, first_end, first_valid, iters, Tout, stats, ctx->ba_s2,
+                        births_done);
     if (two) {
       (void)hipEventRecord(ctx->ba_join, ctx->ba_s2);
       (void)hipStreamWaitEvent(s, ctx->ba_join, 0);
     }
   });
   FVO_LAUNCH_CHECK(ctx);
+  return 0;
+}
+
+// k_ba_births of every window of a coming fvo_ba_windows call, ahead of it (it reads the match rows
+// and the stereo points only); recorded so that call skips it
+int ba_births_run(fvo_ctx* ctx, const int32_t* matches, const int32_t* nmatch, const float* stereo, int nframes,
+                  int cap, int first_end, int nwin, int first_valid, hipStream_t s) {
+  if (cap != ctx->kp_cap) return fvo_fail(ctx, "ba: cap must equal the context keypoint capacity");
+  if (nwin > ctx->cfg.max_batch) return fvo_fail(ctx, "ba: n_windows exceeds max_batch");
+  if (first_end < 1 || first_end + nwin > nframes) return fvo_fail(ctx, "ba: windows exceed the frame range");
+  if (first_valid < 0 || first_valid >= first_end) return fvo_fail(ctx, "ba: first_valid out of range");
+  const BaDims d = make_dims(ctx);
+  const size_t shb = build_shm(d);
+  if (!(shb > (size_t)d.cap)) return 0;  // serial construction: fvo_ba_windows counts in k_ba_build
+  BaIn in{nullptr, nullptr, matches, nmatch, reinterpret_cast<const float4*>(stereo), nullptr, {}, 1};
+  hipLaunchKernelGGL(k_ba_births, dim3(nwin, d.K - 1), dim3(kBirthBlock), shb, s, in, ctx->ba_ws, d, first_end,
+                     first_valid);
+  FVO_LAUNCH_CHECK(ctx);
+  auto& pb = ctx->ba_births;
+  pb.valid = true;
+  pb.matches = matches;
+  pb.stereo = stereo;
+  pb.nframes = nframes;
+  pb.first_end = first_end;
+  pb.nwin = nwin;
+  pb.first_valid = first_valid;
   return 0;
 }
 

@@ -237,6 +237,18 @@ int fvo_ba_windows(fvo_ctx* c, const float* keypoints, const int32_t* n_keypoint
                 first_valid, K, baseline, inv_sigma2, n_levels, iterations, T_out, stats, (hipStream_t)stream);
 }
 
+int fvo_ba_count_births(fvo_ctx* c, const int32_t* matches, const int32_t* n_matches, const float* stereo,
+                        int32_t n_frames, int32_t cap, int32_t first_end, int32_t n_windows, int32_t first_valid,
+                        fvo_stream stream) {
+  if (check_batch(c, n_windows, FVO_STAGE_BA)) return -1;
+  c->ba_births.valid = false;
+  if (n_windows == 0) return 0;
+  if (!matches || !n_matches || !stereo) return fvo_fail(c, "null pointer argument");
+  if (reinterpret_cast<uintptr_t>(stereo) & 15) return fvo_fail(c, "stereo buffer must be 16-byte aligned");
+  return ba_births_run(c, matches, n_matches, stereo, n_frames, cap, first_end, n_windows, first_valid,
+                       (hipStream_t)stream);
+}
+
 int fvo_ba_landmarks(fvo_ctx* c, int32_t window, double* xyz, int32_t* count, fvo_stream stream) {
   if (check_batch(c, 1, FVO_STAGE_BA)) return -1;
   if (!xyz || !count) return fvo_fail(c, "null pointer argument");

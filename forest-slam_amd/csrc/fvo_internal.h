@@ -83,6 +83,14 @@ struct fvo_ctx {
   int16_t* sg_raw = nullptr;    // [B][H][W] pre-median disparity
   uint64_t* sg_hand = nullptr;  // [B][H][2][D/32][16] L-path hand-off granules (cost pass, column block to block)
   uint32_t* sg_ctl = nullptr;   // [4 + B] ticket, generation, hand-off timeouts, per-pair failure flags
+  // fvo_ba_count_births's record: the window range whose birth counts are already in the BA
+  // workspace (valid until the next BA call)
+  struct {
+    bool valid = false;
+    const void* matches = nullptr;
+    const void* stereo = nullptr;
+    int nframes = 0, first_end = 0, nwin = 0, first_valid = 0;
+  } ba_births;
   // pose workspace
   double* pnp_hyp = nullptr;      // [B][cap][2] normalised inlier points (refinement)
   int32_t* pnp_sub = nullptr;     // [B][cap] inlier indices
@@ -189,6 +197,8 @@ int recover_run(fvo_ctx* ctx, const double* E, const int32_t* est, const float* 
 
 int ba_init(fvo_ctx* ctx);
 int ba_export_run(fvo_ctx* ctx, int window, double* xyz, int32_t* count, hipStream_t s);
+int ba_births_run(fvo_ctx* ctx, const int32_t* matches, const int32_t* nmatch, const float* stereo, int nframes,
+                  int cap, int first_end, int nwin, int first_valid, hipStream_t s);
 int ba_stereo_run(fvo_ctx* ctx, const int16_t* disp, const float* kp, const int32_t* nkp, int batch, int cap,
                   const double* K, double baseline, float* stereo, hipStream_t s);
 int ba_run(fvo_ctx* ctx, const float* kp, const int32_t* nkp, const int32_t* matches, const int32_t* nmatch,

@@ -38,7 +38,8 @@ STATUS_SGBM_FAILED = -4
 class StereoFrontEnd:
     def __init__(self, width: int, height: int, K: np.ndarray, dist: np.ndarray, baseline: float, batch: int,
                  nfeatures: int = 500, match_right: bool = True, device=None, ba_window: int = 10,
-                 ba_iters: int = 10, overlap_sgbm: bool = False, sgbm_last: bool = False, **params):
+                 ba_iters: int = 10, overlap_sgbm: bool = False, sgbm_last: bool = False, births_ahead: bool = False,
+                 **params):
         self.B = batch
         self.K = np.asarray(K, np.float64)
         self.dist = np.resize(np.asarray(dist, np.float64), 5)
@@ -117,6 +118,12 @@ class StereoFrontEnd:
         # step's back stage then starts beside the small ORB / BF blocks instead of SGBM's)
         self.sgbm_last = bool(sgbm_last)
         self.s_sgbm = torch.cuda.Stream(dev) if self.overlap_sgbm else None
+        # births_ahead: local BA's birth counting (fvo_ba_count_births) on its own stream beside PnP
+        # -- it needs the step's matches and stereo points only, and in the back stage's chain its
+        # launch waits for room beside the next front stage's SGBM waves (r6 VERDICT item 4).
+        # Measured slower on the overlapped bench (5632-5667 vs 5689-5705 frames/s), so off by
+        # default; bit-identical either way (tests/test_frontend_gpu.py)
+        self.s_births = torch.cuda.Stream(dev) if (self.ba_window and births_ahead) else None
         # prime() runs on the caller's stream: the first front stage after it waits for it
         self.primed = None
         self.sg_lastL = e((height, width), torch.uint8)
@@ -206,7 +213,10 @@ class StereoFrontEnd:
                                     out=self.kstereo[:n])
         if self.overlap_sgbm:
             main.wait_stream(fs)
-        # ---- back stage: back-projection, PnP, local BA
+        # ---- back stage: back-projection, PnP, local BA.  The BA history's frame data (everything
+        # but the PnP transforms) is in place before PnP, and the BA's birth counting starts on a
+        # side stream right away
+        births = self._ba_births(n, kp, m, nm) if self.ba_window else None  # (None without births_ahead)
         P3, p2, npts = ctx.backproject(disp, self.q_kp[:n], kp[:n], m[:n], nm[:n], self.K, self.baseline,
                                        out=(self.P3[:n], self.p2[:n], self.npts[:n]))
         rv, tv, T, st, _ = ctx.pnp_ransac(P3, p2, npts, self.K, self.dist,
@@ -224,7 +234,7 @@ class StereoFrontEnd:
             ctx.count_guard(self.sg_status[:n], n, 1, status=st, code=STATUS_SGBM_FAILED)
         out = T
         if self.ba_window:
-            out = self._local_ba(n, kp, cnt, m, nm, disp, T)
+            out = self._local_ba(n, T, births)
         if self.overlap_sgbm and not capturing:
             self.main_done[slot] = main.record_event()
         self.k += 1
@@ -245,13 +255,31 @@ class StereoFrontEnd:
         self.sg_status = self.sg_status_buf[slot]
         self.kstereo = self.kstereo_buf[slot]
 
-    def _local_ba(self, n, kp, cnt, m, nm, disp, T):
+    def _ba_births(self, n, kp, m, nm):
+        """The step's frames into the BA history (keypoints, matches, stereo points; the PnP
+        transforms follow in _local_ba) and fvo_ba_count_births on the side stream; returns the
+        event _local_ba's BA call waits for."""
         Kw, ctx = self.ba_window, self.ctx
         a, b = Kw - 2, Kw - 1  # first pair slot, first new-frame slot
-        # (hnkp[b:b+n], the clamped counts, came from count_guard)
         ctx.copy_regions([(self.hkp[b:b + n], kp[:n]), (self.hmatch[a:a + n], m[:n]),
-                          (self.hnmatch[a:a + n], nm[:n]), (self.hT[a:a + n], T[:n]),
-                          (self.hstereo[a:a + n], self.kstereo[:n])])
+                          (self.hnmatch[a:a + n], nm[:n]), (self.hstereo[a:a + n], self.kstereo[:n])])
+        F = b + n
+        sb = self.s_births
+        if sb is None:  # births_ahead=False: fvo_ba_windows counts them itself, in its chain
+            return None
+        sb.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(sb):
+            ctx.ba_count_births(self.hmatch[:F], self.hnmatch[:F], self.hstereo[:F], b, n, self.valid_from)
+            return sb.record_event()
+
+    def _local_ba(self, n, T, births):
+        Kw, ctx = self.ba_window, self.ctx
+        a, b = Kw - 2, Kw - 1  # first pair slot, first new-frame slot
+        # (hnkp[b:b+n], the clamped counts, came from count_guard; the rest of the frame data from
+        # _ba_births)
+        ctx.copy_regions([(self.hT[a:a + n], T[:n])])
+        if births is not None:
+            torch.cuda.current_stream(self.dev).wait_event(births)
         F = b + n
         Tba, _ = ctx.ba_windows(self.hkp[:F], self.hnkp[:F], self.hmatch[:F], self.hnmatch[:F], self.hstereo[:F],
                                 self.hT[:F], b, n, self.valid_from, self.K, self.baseline, iterations=self.ba_iters,

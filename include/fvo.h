@@ -216,6 +216,18 @@ int fvo_ba_windows(fvo_ctx* ctx, const float* keypoints, const int32_t* n_keypoi
                    double baseline, const double* inv_sigma2, int32_t n_levels, int32_t iterations,
                    double* T_out, double* stats, fvo_stream stream);
 
+/* The first step of fvo_ba_windows -- counting each window's landmark births and observations
+ * per birth frame -- issued ahead of it, e.g. on a side stream while PnP runs (it reads only the
+ * match rows and the keypoints' stereo points, not T_rel or the keypoints).  Arguments as for
+ * fvo_ba_windows.  The next fvo_ba_windows call on this context with the same matches, stereo,
+ * n_frames, first_end, n_windows and first_valid skips that step; the caller orders the two calls
+ * (the stream of fvo_ba_windows waits for this one's).  Any other BA call in between (or a
+ * different window range) makes fvo_ba_windows count again itself.  A window range whose match
+ * maps exceed the LDS budget (the serial construction) is counted by fvo_ba_windows regardless. */
+int fvo_ba_count_births(fvo_ctx* ctx, const int32_t* matches, const int32_t* n_matches, const float* stereo,
+                        int32_t n_frames, int32_t cap, int32_t first_end, int32_t n_windows, int32_t first_valid,
+                        fvo_stream stream);
+
 /* Refined landmarks of BA window `window` of the most recent fvo_ba_windows call (the
  * keyframe map a rank shares with the others): xyz [ba_max_landmarks][3] f64
  * in the window's first-camera frame, count [1] i32.  Device-side, no host sync. */

@@ -79,6 +79,9 @@ int ba_run(fvo_ctx*, const float*, const int32_t*, const int32_t*, const int32_t
   return hit("ba_run");
 }
 int ba_export_run(fvo_ctx*, int, double*, int32_t*, hipStream_t) { return hit("ba_export_run"); }
+int ba_births_run(fvo_ctx*, const int32_t*, const int32_t*, const float*, int, int, int, int, int, hipStream_t) {
+  return hit("ba_births_run");
+}
 int gather_run(fvo_ctx*, const float*, const float*, const int32_t*, const int32_t*, int, int, float*, float*, int32_t*,
                hipStream_t) {
   return hit("gather_run");

@@ -362,6 +362,27 @@ def test_contexts_of_different_sizes_coexist(oracle_mod):
         assert np.array_equal(res[0][:, :6], kp) and np.array_equal(res[1], d)
 
 
+def test_ba_births_ahead_matches_in_chain(frames):
+    """r6: StereoFrontEnd(births_ahead=True) counts local BA's landmark births with
+    fvo_ba_count_births on a side stream beside PnP; fvo_ba_windows then skips that step.  The
+    refined transforms and statuses are bit-identical to counting them inside fvo_ba_windows, in
+    order and overlapped, over steps whose BA windows slide across the step boundary."""
+    from forest_slam_amd import synth, vo
+    Ls = torch.from_numpy(np.stack([f[0] for f in frames])).cuda()
+    Rs = torch.from_numpy(np.stack([f[1] for f in frames])).cuda()
+    for ov in (False, True):
+        outs = []
+        for ahead in (False, True):
+            fe = vo.StereoFrontEnd(960, 600, synth.K0, synth.DIST_L, synth.BASELINE, batch=2, nfeatures=500,
+                                   ba_window=3, overlap_sgbm=ov, births_ahead=ahead)
+            fe.prime(Ls[0], Rs[0])
+            res = [fe.step(Ls[i:i + 2], Rs[i:i + 2]) for i in (1, 1, 1)]
+            torch.cuda.synchronize()
+            outs.append([(T.cpu().numpy().copy(), st.cpu().numpy().copy()) for T, st in res])
+        for (Ta, sa), (Tb, sb) in zip(*outs):
+            assert np.array_equal(sa, sb) and np.array_equal(Ta, Tb)
+
+
 def test_overlapped_sgbm_stream_matches_serial(frames):
     """StereoFrontEnd(overlap_sgbm=True) (SGBM of step k+1 on a side stream, double-buffered
     disparities) gives bit-identical transforms and statuses to the in-order schedule."""
