@@ -134,6 +134,10 @@ int main() {
                                       f64, f64, nullptr));
   reset(); reached(fvo_ba_windows(c, f32, i32, i32, i32, f32, f64, 12, cap, 9, 2, 0, f64, 0.25, f64, 8, 10, f64, f64,
                                   nullptr), "ba_run");
+  reset(); rejected(c, fvo_ba_count_births(c, nullptr, i32, f32, 12, cap, 9, 2, 0, nullptr));
+  reset(); rejected(c, fvo_ba_count_births(c, i32, i32, unaligned, 12, cap, 9, 2, 0, nullptr));
+  reset(); rejected(c, fvo_ba_count_births(c, i32, i32, f32, 12, cap, 9, 5, 0, nullptr));  // n_windows > max_batch
+  reset(); reached(fvo_ba_count_births(c, i32, i32, f32, 12, cap, 9, 2, 0, nullptr), "ba_births_run");
   reset(); rejected(c, fvo_ba_landmarks(c, 0, nullptr, i32, nullptr));
   reset(); reached(fvo_ba_landmarks(c, 0, f64, i32, nullptr), "ba_export_run");
 

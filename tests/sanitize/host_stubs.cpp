@@ -41,7 +41,7 @@ const char* hipGetErrorString(hipError_t) { return "stub hip error"; }
 
 // --- stage inits: one small host allocation each, released by capi.cpp's hipFree
 int orb_init(fvo_ctx* c) { c->pyr = reinterpret_cast<uint8_t*>(new char[16]); return hit("orb_init"); }
-int bf_init(fvo_ctx* c) { c->bf_sidx = reinterpret_cast<int32_t*>(new char[16]); return hit("bf_init"); }
+int bf_init(fvo_ctx* c) { c->bf_rowkey = reinterpret_cast<uint32_t*>(new char[16]); return hit("bf_init"); }
 int sgbm_init(fvo_ctx* c) {
   if (c->cfg.block_size != 7) return fvo_fail(c, "SGBM: only blockSize=7 is supported");
   c->sg_raw = reinterpret_cast<int16_t*>(new char[16]);
