@@ -223,20 +223,40 @@ __host__ __device__ constexpr int sg_pow2(int n) { return n <= 1 ? 1 : 2 * sg_po
 __host__ __device__ constexpr int sg_ring_keys(int D) { return sg_pow2(2 * D + 32); }
 __host__ __device__ constexpr int sg_ring_raw(int D) { return sg_pow2(D + 16); }
 
-// One path step of a 16-lane row (PQ packed words per lane); returns the row minimum.
+// One path step of a 16-lane row (PQ packed words per lane).  The path minimum travels in both
+// u16 halves (mps, and the returned row minimum), and the step is regrouped so that it sits
+// two operations from the next state instead of five:
+//   c + min(A, mp + P2) - mp  ==  min((A + c) - mp, c + P2),  A = min(min(dm, dp) + P1, cur)
+// exact, not only modulo 2^16: A >= mp (every term is a state entry of the previous column or
+// a sentinel, and mp is their minimum), and A + c <= Lmax + Cmax <= 2 Cmax + P2 < 0xFFFF by
+// sgbm_init's bound (Cmax = 49 (2 ftzero + 63)), so neither side wraps and the min compares
+// true values.  A + c and c + P2 do not depend on mp.  The row minimum: the packed minimum of
+// the words, its halves swapped and min-ed (both halves then hold it), four DPP steps as u32
+// minima (a value splatted into both halves orders as u32 exactly as its u16) -- no split, and
+// no splat before the next step.
 template <int PQ>
-__device__ __forceinline__ uint32_t step16(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
+__device__ __forceinline__ uint32_t step16(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t mps,
                                            uint32_t P2) {
   // a row's lanes 0 / 15 have no left / right neighbour: the sentinel there
   const uint32_t lo0 = dshift_or<kRShr1>(st[PQ - 1], q == 0 ? kSent << 16 : 0u);
   const uint32_t hiN = dshift_or<kRShl1>(st[0], q == 15 ? kSent : 0u);
-  const u16x2 mp2 = splat_p2(minPrev, P2), mpv = splat(minPrev);
+  const u16x2 mpv = as_v(mps), p2 = splat(P2);
   u16x2 mn = splat(0xFFFF);
   uint32_t oldk = 0;
 #pragma unroll
-  for (int k = 0; k < PQ; ++k) mn = vmin(mn, as_v(sgm_pair<PQ>(st, k, oldk, c[k], P1, mp2, mpv, lo0, hiN)));
-  uint32_t m = as_u(mn);
-  m = min(m & 0xFFFFu, m >> 16);
+  for (int k = 0; k < PQ; ++k) {
+    const uint32_t cur = st[k];
+    const uint32_t lo = k > 0 ? oldk : lo0;
+    const uint32_t hi = k < PQ - 1 ? st[k + 1] : hiN;
+    const u16x2 dm = as_v(__builtin_amdgcn_alignbit(cur, lo, 16));  // (prev[2k-1], prev[2k])
+    const u16x2 dp = as_v(__builtin_amdgcn_alignbit(hi, cur, 16));  // (prev[2k+1], prev[2k+2])
+    const u16x2 A = vmin(vmin(dm, dp) + P1, as_v(cur));
+    const u16x2 nv = vmin(A + as_v(c[k]) - mpv, as_v(c[k]) + p2);
+    oldk = cur;
+    st[k] = as_u(nv);
+    mn = vmin(mn, nv);
+  }
+  uint32_t m = as_u(vmin(mn, __builtin_shufflevector(mn, mn, 1, 0)));
   m = dmin<kQX1>(m);
   m = dmin<kQX2>(m);
   m = dmin<kRHalfMirror>(m);
@@ -385,7 +405,8 @@ __device__ __attribute__((noinline)) void sg_run_L(SgLink lk, lds_cu32* ring, in
     m = dmin<kQX1>(m);
     m = dmin<kQX2>(m);
     m = dmin<kRHalfMirror>(m);
-    lmin = dmin<kRMirror>(m);
+    m = dmin<kRMirror>(m);
+    lmin = m | (m << 16);  // step16's minimum travels in both halves
   }
   const int nx = min(CB, width1 - c0);
   // checkpoints after the columns x1 = W1 - 9 - 8 m (m >= 0): the row pass's segment m starts there
