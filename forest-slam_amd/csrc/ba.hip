@@ -1219,7 +1219,7 @@ constexpr int kSolveBlock = 512, kSolveWaves = kSolveBlock / 64;
 __host__ __device__ constexpr int ba_np16(int np) { return (np + 15) & ~15; }
 __host__ __device__ constexpr int ba_sstride(int np16) { return np16 + 2; }
 __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
-  extern __shared__ double sS[];  // [NP][NP + 2] S then L (lower), rhs[NP], rinv[NP]
+  extern __shared__ double sS[];  // [NP][NP + 2] S then L (lower), rhs[NP], rinv[NP], linvT[NP / 16][16][16]
   __shared__ int s_fail;
   const BaWin v = view(ws, dm, blockIdx.x);
   BaState* S = v.st;
@@ -1232,6 +1232,8 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
   const double lam = S->lam;
   double* rhs = sS + NP * STR;
   double* rinv = rhs + NP;  // reciprocal pivots of the factor
+  constexpr int LS = 17;      // row stride of linvT (16 + 1: a column of stores hits 16 bank pairs)
+  double* linvT = rinv + NP;  // per panel p: row j = column j of L_pp^-1 (the blocked solves below)
   if (tid == 0) s_fail = 0;
   // padding: identity rows / columns past np
   for (int t = tid; t < NP * NP; t += kSolveBlock) {
@@ -1315,11 +1317,11 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
       bad |= !(piv > 0.0);
       const double rp = rsq_r(piv);
       const double lic = r[c] * rp;  // L[i][c] (the diagonal piv rp on row c)
+      // r6: every entry updated (one FMA, no select): a lane's entries right of its diagonal
+      // become garbage that nothing reads (pivots and multipliers come from lanes at or below
+      // their column) and are zeroed as each column completes
 #pragma unroll
-      for (int j = c + 1; j < 16; ++j) {
-        const double ljc = rl_f64(lic, j);
-        if (i >= j) r[j] -= lic * ljc;
-      }
+      for (int j = c + 1; j < 16; ++j) r[j] = fma(-lic, rl_f64(lic, j), r[j]);
       r[c] = i >= c ? lic : 0.0;
       if (lane == 0) rinv[c0 + c] = rp;
     }
@@ -1345,6 +1347,14 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) pc[4 * r * STR] -= acc[r];
   };
+  auto panel_subst = [&](double (&x)[16], int c0) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      x[c] *= rinv[c0 + c];
+#pragma unroll
+      for (int c2 = c + 1; c2 < 16; ++c2) x[c2] = fma(-x[c], sS[(c0 + c2) * STR + c0 + c], x[c2]);
+    }
+  };
   if (wid == 0) factor_diag(0);
   __syncthreads();
   for (int p = 0; p < NTl; ++p) {
@@ -1352,19 +1362,18 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
     const int c0 = 16 * p;
     // (B) the panel's rows below the tile: L_Ip = S_Ip L_pp^-T, one thread per row
     const int nb = NP - c0 - 16;
-    if (tid < nb) {
-      double* row = sS + (c0 + 16 + tid) * STR + c0;
+    // r6: right-looking substitution (x[c] final, then its term leaves every later entry at
+    // once: a chain of 16 multiply + FMA steps instead of the 136-deep dot products of the
+    // row-by-row substitution); the tile's column c is a uniform (broadcast) read.  The same
+    // substitution on the unit vectors e_j gives the columns of L_pp^-1 for the blocked solves
+    // below -- run by the last wave during (C) (it has the fewest tiles), for the last panel here.
+    const bool unit = p == NTl - 1 && tid < 16;
+    if (tid < nb || unit) {
+      double* row = unit ? linvT + (p * 16 + tid) * LS : sS + (c0 + 16 + tid) * STR + c0;
       double x[16];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) x[c] = row[c];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const double* lc = sS + (c0 + c) * STR + c0;  // row c of the tile: uniform (broadcast) reads
-        double sv = x[c];
-#pragma unroll
-        for (int c2 = 0; c2 < c; ++c2) sv -= x[c2] * lc[c2];
-        x[c] = sv * rinv[c0 + c];
-      }
+      for (int c = 0; c < 16; ++c) x[c] = unit ? (c == tid ? 1.0 : 0.0) : row[c];
+      panel_subst(x, c0);
 #pragma unroll
       for (int c = 0; c < 16; ++c) row[c] = x[c];
     }
@@ -1388,6 +1397,15 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
           }
           tile_upd(c0, I, p + 1 + rem);
         }
+        if (wid == kSolveWaves - 1 && lane < 16) {  // the columns of L_pp^-1 (above)
+          double x[16];
+#pragma unroll
+          for (int c = 0; c < 16; ++c) x[c] = c == lane ? 1.0 : 0.0;
+          panel_subst(x, c0);
+          double* row = linvT + (p * 16 + lane) * LS;
+#pragma unroll
+          for (int c = 0; c < 16; ++c) row[c] = x[c];
+        }
       }
     }
     __syncthreads();
@@ -1397,53 +1415,62 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
     return;
   }
   if (wid == 0) {
-    // L y = rhs, then L^T x = y, column-oriented on wave 0: lane owns rows lane and lane + 64
-    // (np <= 120); each step divides the finished row's value by its pivot (every lane, same
-    // arithmetic), broadcasts it with a wave-uniform read, and every remaining row subtracts
-    // its term -- one dependent step per row instead of a wave reduction per row.
-    auto bcast = [](double v, int src) {
-      const long long b = __double_as_longlong(v);
-      const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), src);
-      const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
-      return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+    // L y = rhs, then L^T x = y, blocked by the 16-row panels on wave 0 (r6; r5 walked the rows
+    // one dependent step each, 2 x 114 steps of readlane + multiply + FMA at 1080p, ~18 us): a
+    // quad of lanes per row of the panel, lane q of the quad summing every 4th term.
+    //   forward, panel p:  r = b_p - L_p,<p y_<p (left-looking), y_p = L_pp^-1 r
+    //   backward, panel p: t = y_p - L_>p,p^T x_>p,              x_p = L_pp^-T t
+    // the panel's intermediate vector crosses the quads through rhs (one wave: its LDS accesses
+    // complete in order once waited for).
+    const int i = lane >> 2, q = lane & 3;
+    auto quad_sum = [](double v) {
+      v += dpp_f64<0xB1>(v);  // quad_perm [1,0,3,2]
+      v += dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]
+      return v;
     };
-    // The factor's entries a step needs (column j of L for the forward pass, row j for the
-    // backward one) and the pivot's reciprocal are loaded one step ahead, so LDS latency stays
-    // off the chain (readlane -> multiply -> FMA); rows >= np carry garbage that is never read.
-    const int r0 = lane, r1 = lane + 64;
-    const int c0 = min(r0, np - 1), c1 = min(r1, np - 1);
-    double x0 = r0 < np ? rhs[r0] : 0.0, x1 = r1 < np ? rhs[r1] : 0.0;
-    {
-      double a0 = sS[c0 * STR], a1 = sS[c1 * STR], rv = rinv[0];
-      auto fwd = [&](int j, auto hi_t) {
-        constexpr bool HI = decltype(hi_t)::value;
-        const int jn = min(j + 1, np - 1);
-        const double na0 = sS[c0 * STR + jn], na1 = sS[c1 * STR + jn], nrv = rinv[jn];
-        const double yj = bcast(HI ? x1 : x0, j & 63) * rv;
-        x0 = r0 == j ? yj : (r0 > j ? x0 - a0 * yj : x0);
-        x1 = r1 == j ? yj : (r1 > j ? x1 - a1 * yj : x1);
-        a0 = na0; a1 = na1; rv = nrv;
-      };
-      const int jm = min(np, 64);
-      for (int j = 0; j < jm; ++j) fwd(j, std::false_type{});
-      for (int j = 64; j < np; ++j) fwd(j, std::true_type{});
+    auto lds_done = []() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+    // (four partial sums per lane, so the loads of a panel's terms are issued together)
+    for (int p = 0; p < NTl; ++p) {
+      const int c0 = 16 * p;
+      const double* Lr = sS + (c0 + i) * STR;
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int k0 = q; k0 < c0; k0 += 16)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a4[u] = fma(Lr[k0 + 4 * u], rhs[k0 + 4 * u], a4[u]);
+      const double acc = quad_sum((a4[0] + a4[1]) + (a4[2] + a4[3]));
+      const double r = rhs[c0 + i] - acc;
+      lds_done();
+      if (q == 0) rhs[c0 + i] = r;
+      lds_done();
+      const double* Li = linvT + p * 16 * LS;
+      double y = 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) y = fma(Li[(4 * q + u) * LS + i], rhs[c0 + 4 * q + u], y);
+      y = quad_sum(y);
+      lds_done();
+      if (q == 0) rhs[c0 + i] = y;
+      lds_done();
     }
-    {
-      double b0 = sS[(np - 1) * STR + c0], b1 = sS[(np - 1) * STR + c1], rv = rinv[np - 1];
-      auto bwd = [&](int j, auto hi_t) {
-        constexpr bool HI = decltype(hi_t)::value;
-        const int jn = max(j - 1, 0);
-        const double nb0 = sS[jn * STR + c0], nb1 = sS[jn * STR + c1], nrv = rinv[jn];
-        const double xj = bcast(HI ? x1 : x0, j & 63) * rv;
-        x0 = r0 == j ? xj : (r0 < j ? x0 - b0 * xj : x0);
-        x1 = r1 == j ? xj : (r1 < j ? x1 - b1 * xj : x1);
-        b0 = nb0; b1 = nb1; rv = nrv;
-      };
-      for (int j = np - 1; j >= 64; --j) bwd(j, std::true_type{});
-      for (int j = min(np, 64) - 1; j >= 0; --j) bwd(j, std::false_type{});
+    for (int p = NTl - 1; p >= 0; --p) {
+      const int c0 = 16 * p;
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int k0 = c0 + 16 + q; k0 < NP; k0 += 16)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a4[u] = fma(sS[(k0 + 4 * u) * STR + c0 + i], rhs[k0 + 4 * u], a4[u]);
+      const double acc = quad_sum((a4[0] + a4[1]) + (a4[2] + a4[3]));
+      const double t = rhs[c0 + i] - acc;
+      lds_done();
+      if (q == 0) rhs[c0 + i] = t;
+      lds_done();
+      const double* Li = linvT + (p * 16 + i) * LS;
+      double x = 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x = fma(Li[4 * q + u], rhs[c0 + 4 * q + u], x);
+      x = quad_sum(x);
+      lds_done();
+      if (q == 0) rhs[c0 + i] = x;
+      lds_done();
     }
-    if (r0 < np) rhs[r0] = x0;
-    if (r1 < np) rhs[r1] = x1;
   }
   __syncthreads();
   for (int a = tid; a < 6 * n; a += kSolveBlock) S->dp[a] = a < 6 ? 0.0 : rhs[a - 6];
@@ -1686,7 +1713,7 @@ size_t build_shm(const BaDims& d) {
 size_t lin_shm(const BaDims& d) { return (size_t)8 * 3 * d.LPC * (d.NR + 2); }
 size_t solve_shm(int K) {
   const int np = 6 * (K - 1), NP = ba_np16(np);
-  return (size_t)8 * (NP * ba_sstride(NP) + 2 * NP);  // S / L (padded), rhs, reciprocal pivots
+  return (size_t)8 * (NP * ba_sstride(NP) + 2 * NP + 17 * NP);  // S / L (padded), rhs, reciprocal pivots, L_pp^-1
 }
 
 }  // namespace
