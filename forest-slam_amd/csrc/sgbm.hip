@@ -54,25 +54,6 @@ struct SgParams {
   int HG4;  // row groups of 4 (volume layout)
 };
 
-// SGM recurrence for one packed pair k of a lane's disparity run, in place.  `old_km1`
-// carries the previous value of pair k-1 (already overwritten); lo0 / hiN are the words
-// that border the run (sentinels, or the neighbour lane's old values).
-template <int NPL>
-__device__ __forceinline__ uint32_t sgm_pair(uint32_t* st, int k, uint32_t& old_km1, uint32_t c, u16x2 P1,
-                                             u16x2 mp2, u16x2 mpv, uint32_t lo0, uint32_t hiN) {
-  uint32_t cur = st[k];
-  uint32_t lo = k > 0 ? old_km1 : lo0;
-  uint32_t hi = k < NPL - 1 ? st[k + 1] : hiN;
-  u16x2 dm = as_v(__builtin_amdgcn_alignbit(cur, lo, 16));  // (prev[2k-1], prev[2k])
-  u16x2 dp = as_v(__builtin_amdgcn_alignbit(hi, cur, 16));  // (prev[2k+1], prev[2k+2])
-  // min(dm + P1, dp + P1) = min(dm, dp) + P1: no path value + P1 wraps (sgbm_init bounds them)
-  u16x2 m = vmin(vmin(dm, dp) + P1, vmin(as_v(cur), mp2));
-  uint32_t nv = as_u(as_v(c) + m - mpv);
-  old_km1 = cur;
-  st[k] = nv;
-  return nv;
-}
-
 constexpr uint32_t kSent = 0x7FFFu;  // "no neighbour" entry: P1 + 0x7FFF never wins the min
 
 // ------------------------------------------------------------------ quad helpers
@@ -128,11 +109,12 @@ __device__ __forceinline__ uint32_t step16(uint32_t* st, const uint32_t* c, int 
 
 // One step of a path over a lane's run with G lanes per column (G = 4: quad; G = 8: half
 // row, neighbours by DPP row shifts, minimum by two quad steps + row_half_mirror; G = 16: a
-// DPP row, step16); returns the group-wide minimum.
+// DPP row, step16); the path minimum in both u16 halves in and out, the step regrouped as
+// step16's (below).
 template <int PQ, int G>
-__device__ __forceinline__ uint32_t hstepG(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
+__device__ __forceinline__ uint32_t hstepG(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t mps,
                                            uint32_t P2) {
-  if constexpr (G == 16) return step16<PQ>(st, c, q, P1, minPrev, P2);
+  if constexpr (G == 16) return step16<PQ>(st, c, q, P1, mps, P2);
   uint32_t prevLast, nextFirst;
   if (G == 4) {
     prevLast = qperm<kQPrev>(st[PQ - 1]);
@@ -143,13 +125,23 @@ __device__ __forceinline__ uint32_t hstepG(uint32_t* st, const uint32_t* c, int 
   }
   const uint32_t lo0 = q == 0 ? (kSent << 16) : prevLast;
   const uint32_t hiN = q == G - 1 ? kSent : nextFirst;
-  const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
+  const u16x2 mpv = as_v(mps), p2 = splat(P2);
   u16x2 mn = splat(0xFFFF);
   uint32_t oldk = 0;
 #pragma unroll
-  for (int k = 0; k < PQ; ++k) mn = vmin(mn, as_v(sgm_pair<PQ>(st, k, oldk, c[k], P1, mp2, mpv, lo0, hiN)));
-  uint32_t m = as_u(mn);
-  m = min(m & 0xFFFFu, m >> 16);
+  for (int k = 0; k < PQ; ++k) {
+    const uint32_t cur = st[k];
+    const uint32_t lo = k > 0 ? oldk : lo0;
+    const uint32_t hi = k < PQ - 1 ? st[k + 1] : hiN;
+    const u16x2 dm = as_v(__builtin_amdgcn_alignbit(cur, lo, 16));
+    const u16x2 dp = as_v(__builtin_amdgcn_alignbit(hi, cur, 16));
+    const u16x2 A = vmin(vmin(dm, dp) + P1, as_v(cur));
+    const u16x2 nv = vmin(A + as_v(c[k]) - mpv, as_v(c[k]) + p2);
+    oldk = cur;
+    st[k] = as_u(nv);
+    mn = vmin(mn, nv);
+  }
+  uint32_t m = as_u(vmin(mn, __builtin_shufflevector(mn, mn, 1, 0)));
   m = dmin<kQX1>(m);
   m = dmin<kQX2>(m);
   if (G == 8) m = dmin<0x141>(m);  // row_half_mirror
@@ -183,27 +175,6 @@ __device__ __forceinline__ void bload(__amdgpu_buffer_rsrc_t rs, uint32_t voff, 
   }
 }
 
-// One step of a horizontal path over a lane's run; returns the quad-wide minimum.
-template <int PQ>
-__device__ __forceinline__ uint32_t hstep(uint32_t* st, const uint32_t* c, int q, u16x2 P1, uint32_t minPrev,
-                                          uint32_t P2) {
-  const uint32_t prevLast = qperm<kQPrev>(st[PQ - 1]);
-  const uint32_t nextFirst = qperm<kQNext>(st[0]);
-  const uint32_t lo0 = q == 0 ? (kSent << 16) : prevLast;
-  const uint32_t hiN = q == 3 ? kSent : nextFirst;
-  const u16x2 mp2 = splat(minPrev + P2), mpv = splat(minPrev);
-  u16x2 mn = splat(0xFFFF);
-  uint32_t oldk = 0;
-#pragma unroll
-  for (int k = 0; k < PQ; ++k) mn = vmin(mn, as_v(sgm_pair<PQ>(st, k, oldk, c[k], P1, mp2, mpv, lo0, hiN)));
-  uint32_t m = as_u(mn);
-  m = min(m & 0xFFFFu, m >> 16);
-  m = dmin<kQX1>(m);
-  m = dmin<kQX2>(m);
-  return m;
-}
-
-
 // ------------------------------------------------------------------ row bands: C + left/right paths + WTA
 // A row of 16 lanes is one DPP row: neighbours by row_shr/row_shl:1, minima by quad xor 1/2,
 // row_half_mirror and row_mirror.
@@ -230,7 +201,8 @@ __host__ __device__ constexpr int sg_ring_raw(int D) { return sg_pow2(D + 16); }
 // exact, not only modulo 2^16: A >= mp (every term is a state entry of the previous column or
 // a sentinel, and mp is their minimum), and A + c <= Lmax + Cmax <= 2 Cmax + P2 < 0xFFFF by
 // sgbm_init's bound (Cmax = 49 (2 ftzero + 63)), so neither side wraps and the min compares
-// true values.  A + c and c + P2 do not depend on mp.  The row minimum: the packed minimum of
+// true values; min(dm + P1, dp + P1) = min(dm, dp) + P1 (no path value + P1 wraps, by the same
+// bound).  A + c and c + P2 do not depend on mp.  The row minimum: the packed minimum of
 // the words, its halves swapped and min-ed (both halves then hold it), four DPP steps as u32
 // minima (a value splatted into both halves orders as u32 exactly as its u16) -- no split, and
 // no splat before the next step.
