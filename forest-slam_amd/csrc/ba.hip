@@ -73,8 +73,11 @@ static_assert(64 * kLinWavesDefault / (kLinLPC64 / 2) <= 64 && 64 * kLinWavesDef
 // k_ba_lin runs 16 waves per block: its LDS slice (up to 150 KB) allows one block per CU, so
 // the block's own waves are all the latency hiding the CU gets
 constexpr int kLinWaves = kLinWavesDefault, kLinBlock = 64 * kLinWaves;
-constexpr int kLinMaxTiles = (36 + kLinWaves - 1) / kLinWaves;  // 16x16 tiles per wave: 36 upper tiles at NR = 128
-static_assert(10 <= kLinWaves, "NR = 64 (10 upper tiles): one tile per wave");
+// r6: the block's waves split into producers (the landmark blocks and Y rows of half a chunk,
+// VALU) and consumers (the MFMA contraction of the previous half) over a double-buffered Y
+constexpr int kLinProd = kLinWaves / 2, kLinCons = kLinWaves - kLinProd;
+constexpr int kLinMaxTiles = (36 + kLinCons - 1) / kLinCons;  // 16x16 tiles per consumer wave: 36 upper tiles at NR = 128
+constexpr int kLinTiles64 = (10 + kLinCons - 1) / kLinCons;   // 10 upper tiles at NR = 64
 constexpr double kD2Mono = 5.991, kD2Stereo = 7.815, kMinZ = 0.01, kLam0 = 1e-3;
 
 struct BaState {
@@ -936,7 +939,11 @@ __device__ __forceinline__ void lin_tile(int k, int ntu, int NT, int& I, int& J)
 // The next chunk's landmark starts / observation / position are loaded during this chunk
 // (starts before its arithmetic, the observation record before its MFMA phase), so its
 // arithmetic starts from registers.
-// MAXT: 16x16 tiles per wave (1 at NR = 64: 10 tiles over 16 waves; 3 at NR = 128: 36 tiles)
+// r6: each chunk in two halves of LPC / 2 landmarks, (1) by the producer waves into one half of a
+// double-buffered Y while the consumer waves run (2) over the previous half -- the VALU phase and
+// the MFMA phase overlap instead of alternating between barriers, and each tile still accumulates
+// the chunk's rows in order (bit-identical to the alternating schedule).
+// MAXT: 16x16 tiles per consumer wave (2 at NR = 64: 10 tiles over 8 waves; 5 at NR = 128: 36)
 // Sum / OR of a value over an aligned group of GL lanes (2 <= GL <= 32, a power of two), every
 // lane receiving the same result: within a DPP row by quad permutes (xor 1, xor 2), the half-row
 // mirror and the row mirror (each pairs lanes whose partial sums are equal, so both ends of a
@@ -980,189 +987,203 @@ __device__ __forceinline__ void group_sum_or(double (&v)[N], uint32_t& fm) {
 
 template <int MAXT>
 __global__ __launch_bounds__(kLinBlock) void k_ba_lin(BaIn in, void* ws, BaDims dm, BaCam cam) {
-  extern __shared__ double sY[];  // [3 LPC][NR + 2]
+  extern __shared__ double sY[];    // [2][3 LPC / 2][NR + 2]: the two half-chunk buffers
   __shared__ double sT[kKMax][12];  // the window's current poses
-  __shared__ uint32_t s_tm[64];     // per landmark of the chunk: bit I = its rows reach tile I's columns
+  __shared__ uint32_t s_tm[2][32];  // per landmark of a half chunk: bit I = its rows reach tile I's columns
   const BaWin v = view(ws, dm, blockIdx.x);
   const BaState* S = v.st;
   if (!S->active) return;
-  const int L = S->L, part = blockIdx.y, LPC = dm.LPC;
+  const int L = S->L, part = blockIdx.y, LPC = dm.LPC, LPH = LPC / 2;
   if (part * LPC >= L) return;  // no chunk for this partial (k_ba_solve sums only the used ones)
   const int n = S->n;
   const int np = 6 * (n - 1);
-  const int NR = dm.NR, NRP = NR + 2, rows = 3 * LPC;
-  const double lam = S->lam;
-  const double* X = cur_X(v, S);
+  const int NR = dm.NR, NRP = NR + 2, rows = 3 * LPH;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int NT = NR / 16, ntu = (np + 15) / 16;  // tiles covering the pose rows
-  int ntiles = 0;
-  for (int i = 0; i < ntu; ++i) ntiles += (ntu - i) + (ntu < NT ? 1 : 0);
   for (int i = threadIdx.x; i < n * 12; i += kLinBlock) sT[i / 12][i % 12] = S->T[i / 12][i % 12];
-  typedef double d4 __attribute__((ext_vector_type(4)));
-  d4 acc[MAXT];
-#pragma unroll
-  for (int lt = 0; lt < MAXT; ++lt) acc[lt] = d4{0.0, 0.0, 0.0, 0.0};
-  // this wave's tiles (fixed for the kernel)
-  int tI[MAXT], tJ[MAXT];
-#pragma unroll
-  for (int lt = 0; lt < MAXT; ++lt) {
-    const int k = kLinWaves * lt + wid;
-    tI[lt] = tJ[lt] = -1;
-    if (k < ntiles) lin_tile(k, ntu, NT, tI[lt], tJ[lt]);
-  }
-  const int GL = kLinBlock / LPC, t = threadIdx.x / GL, j = threadIdx.x % GL;
-  // one chunk ahead: the landmark's observation range, its observation j, its position
-  int ns0 = 0, ns1 = 0;
-  BaObs onext{};
-  double xn[3] = {0.0, 0.0, 0.0};
-  auto fetch_start = [&](int c) {
-    const int l = c * LPC + t;
-    ns0 = ns1 = 0;
-    if (c * LPC < L && l < L) {
-      ns0 = v.lstart[l];
-      ns1 = v.lstart[l + 1];
-      xn[0] = X[3 * l];
-      xn[1] = X[3 * l + 1];
-      xn[2] = X[3 * l + 2];
-    }
-  };
-  auto fetch_obs = [&]() {
-    if (j < ns1 - ns0) onext = v.obs[ns0 + j];
-  };
-  fetch_start(part);
-  fetch_obs();
+  // the block's chunks c = part, part + NPART, ... (c LPC < L), each as two halves of LPH landmarks
+  const int nch = ((L + LPC - 1) / LPC - part + dm.NPART - 1) / dm.NPART, nh = 2 * nch;
+  auto half_l0 = [&](int h) { return (part + (h >> 1) * dm.NPART) * LPC + (h & 1) * LPH; };
   __syncthreads();  // sT
-  for (int c = part; c * LPC < L; c += dm.NPART) {
-    const BaObs o = onext;
-    const int cnt = ns1 - ns0;
-    const double xl[3] = {xn[0], xn[1], xn[2]};
-    const int lc0 = c * LPC, l = lc0 + t;
-    const bool live = l < L, has = live && j < cnt;
-    // (a) lane j: observation j's landmark-block terms w Jl^T Jl (upper 6) and w Jl^T r (3), and
-    // its coupling block W; (b) their sum over the group (every lane ends with the same sums),
-    // the damped 3x3 Cholesky and z = L^-1 g; (c) lane j: rows 6 (f-1) .. 6 (f-1) + 5 of W L^-T
-    double hg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    BaCoupling cpl{};
-    const int f = has ? (int)o.frame : 0;
-    if (has) {
-      double r[3], rho, Jl[3][3];
-      ba_eval_lw(sT[f], xl, o, cam, obs_is2(in, o), r, rho, Jl, cpl);
-      const double w = cpl.w;
-      int q = 0;
-      for (int a2 = 0; a2 < 3; ++a2) {
-        for (int b2 = a2; b2 < 3; ++b2) hg[q++] = w * (Jl[0][a2] * Jl[0][b2] + Jl[1][a2] * Jl[1][b2] + Jl[2][a2] * Jl[2][b2]);
-        hg[6 + a2] = w * (Jl[0][a2] * r[0] + Jl[1][a2] * r[1] + Jl[2][a2] * r[2]);
+  if (wid < kLinProd) {
+    // ---- producers: half chunk h into buffer h & 1 while the consumers multiply half h - 1
+    const double lam = S->lam;
+    const double* X = cur_X(v, S);
+    const int GL = kLinBlock / LPC, t = threadIdx.x / GL, j = threadIdx.x % GL;
+    // one half ahead: the landmark's observation range, its observation j, its position
+    int ns0 = 0, ns1 = 0;
+    BaObs onext{};
+    double xn[3] = {0.0, 0.0, 0.0};
+    auto fetch_start = [&](int h) {
+      const int l = half_l0(h) + t;
+      ns0 = ns1 = 0;
+      if (h < nh && l < L) {
+        ns0 = v.lstart[l];
+        ns1 = v.lstart[l + 1];
+        xn[0] = X[3 * l];
+        xn[1] = X[3 * l + 1];
+        xn[2] = X[3 * l + 2];
       }
-    }
-    uint32_t fm = has && f > 0 ? 1u << f : 0u;  // frames with pose columns that see the landmark
-    if (GL == 32) group_sum_or<32>(hg, fm);
-    else if (GL == 16) group_sum_or<16>(hg, fm);
-    else
-      for (int m = GL >> 1; m >= 1; m >>= 1) {
+    };
+    auto fetch_obs = [&]() {
+      if (j < ns1 - ns0) onext = v.obs[ns0 + j];
+    };
+    fetch_start(0);
+    fetch_obs();
+    for (int h = 0; h <= nh; ++h) {
+      if (h < nh) {
+        const BaObs o = onext;
+        const int cnt = ns1 - ns0;
+        const double xl[3] = {xn[0], xn[1], xn[2]};
+        const int l = half_l0(h) + t;
+        const bool live = l < L, has = live && j < cnt;
+        fetch_start(h + 1);  // the next half's landmark starts / position
+        // (a) lane j: observation j's landmark-block terms w Jl^T Jl (upper 6) and w Jl^T r (3), and
+        // its coupling block W; (b) their sum over the group (every lane ends with the same sums),
+        // the damped 3x3 Cholesky and z = L^-1 g; (c) lane j: rows 6 (f-1) .. 6 (f-1) + 5 of W L^-T
+        double hg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        BaCoupling cpl{};
+        const int f = has ? (int)o.frame : 0;
+        if (has) {
+          double r[3], rho, Jl[3][3];
+          ba_eval_lw(sT[f], xl, o, cam, obs_is2(in, o), r, rho, Jl, cpl);
+          const double w = cpl.w;
+          int q = 0;
+          for (int a2 = 0; a2 < 3; ++a2) {
+            for (int b2 = a2; b2 < 3; ++b2) hg[q++] = w * (Jl[0][a2] * Jl[0][b2] + Jl[1][a2] * Jl[1][b2] + Jl[2][a2] * Jl[2][b2]);
+            hg[6 + a2] = w * (Jl[0][a2] * r[0] + Jl[1][a2] * r[1] + Jl[2][a2] * r[2]);
+          }
+        }
+        fetch_obs();  // the next half's observation record
+        uint32_t fm = has && f > 0 ? 1u << f : 0u;  // frames with pose columns that see the landmark
+        if (GL == 32) group_sum_or<32>(hg, fm);
+        else if (GL == 16) group_sum_or<16>(hg, fm);
+        else
+          for (int m = GL >> 1; m >= 1; m >>= 1) {
 #pragma unroll
-        for (int q = 0; q < 9; ++q) hg[q] += __shfl_xor(hg[q], m, 64);
-        fm |= (uint32_t)__shfl_xor((int)fm, m, 64);
-      }
-    const double* H = hg;
-    const double a00 = H[0] + lam * H[0] + 1e-6, a11 = H[3] + lam * H[3] + 1e-6, a22 = H[5] + lam * H[5] + 1e-6;
-    const double i00 = rsq_r(a00), l00 = a00 * i00;
-    const double l10 = H[1] * i00, l20 = H[2] * i00;
-    const double d11 = a11 - l10 * l10, i11 = rsq_r(d11), l11 = d11 * i11;
-    const double l21 = (H[4] - l20 * l10) * i11;
-    const double d22 = a22 - l20 * l20 - l21 * l21, i22 = rsq_r(d22), l22 = d22 * i22;
-    double* Y0 = sY + 3 * t * NRP;
-    if (j == 0) {
-      double z0 = 0.0, z1 = 0.0, z2 = 0.0;
-      if (live) {
-        double* Lf = v.Lf + 6 * l;
-        Lf[0] = l00; Lf[1] = l10; Lf[2] = l11; Lf[3] = l20; Lf[4] = l21; Lf[5] = l22;
-        v.gl[3 * l] = H[6]; v.gl[3 * l + 1] = H[7]; v.gl[3 * l + 2] = H[8];
-        z0 = H[6] * i00;
-        z1 = (H[7] - l10 * z0) * i11;
-        z2 = (H[8] - l20 * z0 - l21 * z1) * i22;
-      }
-      Y0[NR - 1] = z0;
-      Y0[NRP + NR - 1] = z1;
-      Y0[2 * NRP + NR - 1] = z2;
-      uint32_t tm = 0;
-      for (uint32_t mm = fm; mm; mm &= mm - 1) {
-        const int ff = __builtin_ctz(mm);
-        tm |= (1u << (6 * (ff - 1) / 16)) | (1u << ((6 * (ff - 1) + 5) / 16));
-      }
-      s_tm[t] = tm;
-    }
-    if (f > 0) {
-      for (int pp = 0; pp < 6; ++pp) {
-        double wr[3];
-        ba_wrow(cpl, pp, wr);
-        const double y0 = wr[0] * i00;
-        const double y1 = (wr[1] - l10 * y0) * i11;
-        const double y2 = (wr[2] - l20 * y0 - l21 * y1) * i22;
-        const int col = 6 * (f - 1) + pp;
-        Y0[col] = y0;
-        Y0[NRP + col] = y1;
-        Y0[2 * NRP + col] = y2;
-      }
-    }
-    // zeros: the pose column blocks of frames that do not see the landmark, and the padding
-    // columns np .. NR-2 (column NR-1 is z)
-    for (int fb = 1 + j; fb < n; fb += GL)
-      if (!((fm >> fb) & 1u))
-        for (int pp = 0; pp < 6; ++pp) {
-          const int col = 6 * (fb - 1) + pp;
+            for (int q = 0; q < 9; ++q) hg[q] += __shfl_xor(hg[q], m, 64);
+            fm |= (uint32_t)__shfl_xor((int)fm, m, 64);
+          }
+        const double* H = hg;
+        const double a00 = H[0] + lam * H[0] + 1e-6, a11 = H[3] + lam * H[3] + 1e-6, a22 = H[5] + lam * H[5] + 1e-6;
+        const double i00 = rsq_r(a00), l00 = a00 * i00;
+        const double l10 = H[1] * i00, l20 = H[2] * i00;
+        const double d11 = a11 - l10 * l10, i11 = rsq_r(d11), l11 = d11 * i11;
+        const double l21 = (H[4] - l20 * l10) * i11;
+        const double d22 = a22 - l20 * l20 - l21 * l21, i22 = rsq_r(d22), l22 = d22 * i22;
+        double* Y0 = sY + (h & 1) * rows * NRP + 3 * t * NRP;
+        if (j == 0) {
+          double z0 = 0.0, z1 = 0.0, z2 = 0.0;
+          if (live) {
+            double* Lf = v.Lf + 6 * l;
+            Lf[0] = l00; Lf[1] = l10; Lf[2] = l11; Lf[3] = l20; Lf[4] = l21; Lf[5] = l22;
+            v.gl[3 * l] = H[6]; v.gl[3 * l + 1] = H[7]; v.gl[3 * l + 2] = H[8];
+            z0 = H[6] * i00;
+            z1 = (H[7] - l10 * z0) * i11;
+            z2 = (H[8] - l20 * z0 - l21 * z1) * i22;
+          }
+          Y0[NR - 1] = z0;
+          Y0[NRP + NR - 1] = z1;
+          Y0[2 * NRP + NR - 1] = z2;
+          uint32_t tm = 0;
+          for (uint32_t mm = fm; mm; mm &= mm - 1) {
+            const int ff = __builtin_ctz(mm);
+            tm |= (1u << (6 * (ff - 1) / 16)) | (1u << ((6 * (ff - 1) + 5) / 16));
+          }
+          s_tm[h & 1][t] = tm;
+        }
+        if (f > 0) {
+          for (int pp = 0; pp < 6; ++pp) {
+            double wr[3];
+            ba_wrow(cpl, pp, wr);
+            const double y0 = wr[0] * i00;
+            const double y1 = (wr[1] - l10 * y0) * i11;
+            const double y2 = (wr[2] - l20 * y0 - l21 * y1) * i22;
+            const int col = 6 * (f - 1) + pp;
+            Y0[col] = y0;
+            Y0[NRP + col] = y1;
+            Y0[2 * NRP + col] = y2;
+          }
+        }
+        // zeros: the pose column blocks of frames that do not see the landmark, and the padding
+        // columns np .. NR-2 (column NR-1 is z)
+        for (int fb = 1 + j; fb < n; fb += GL)
+          if (!((fm >> fb) & 1u))
+            for (int pp = 0; pp < 6; ++pp) {
+              const int col = 6 * (fb - 1) + pp;
+              Y0[col] = 0.0;
+              Y0[NRP + col] = 0.0;
+              Y0[2 * NRP + col] = 0.0;
+            }
+        for (int col = np + j; col < NR - 1; col += GL) {
           Y0[col] = 0.0;
           Y0[NRP + col] = 0.0;
           Y0[2 * NRP + col] = 0.0;
         }
-    for (int col = np + j; col < NR - 1; col += GL) {
-      Y0[col] = 0.0;
-      Y0[NRP + col] = 0.0;
-      Y0[2 * NRP + col] = 0.0;
-    }
-    fetch_start(c + dm.NPART);  // the next chunk's landmark starts / position
-    __syncthreads();
-    fetch_obs();  // the next chunk's observation record, in flight during the MFMA phase
-    // G += Yt^T Yt on MFMA: A[i][k] = Yt[k][16I + i], B[k][j] = Yt[k][16J + j], lane holds k = lane >> 4.
-    // A 4-row step g (rows 4g .. 4g+3: landmarks 4g/3 and (4g+3)/3) of tile (I, J) is skipped
-    // when those rows are zero in tile I's or J's columns (the z column tile NT-1 always
-    // counts); each tile's steps ascend into its own accumulator (fixed order) and step g+1's
-    // operands are loaded before step g's MFMA is issued.  (Walking the union of the wave's
-    // tiles' steps with every active tile issued back to back -- independent accumulators in
-    // flight -- measured slower: 1080p BA 5.0 -> 6.8 ms, 600p 1.87 -> 2.21 ms, the operand
-    // arrays spilling at 128 VGPRs.)
-    const uint32_t actl = lane < rows / 4 ? (s_tm[(4 * lane) / 3] | s_tm[(4 * lane + 3) / 3]) : 0u;
-#pragma unroll
-    for (int lt = 0; lt < MAXT; ++lt) {
-      const int I = tI[lt], J = tJ[lt];
-      if (I < 0) continue;
-      const double* ya = sY + (lane >> 4) * NRP + 16 * I + (lane & 15);
-      const double* yb = sY + (lane >> 4) * NRP + 16 * J + (lane & 15);
-      uint64_t m = __ballot(((actl >> I) & 1u) && (((actl >> J) & 1u) || J == NT - 1));
-      if (!m) continue;
-      // operands loaded two active steps ahead of the MFMA that uses them (the phase waits on
-      // its LDS loads, not on the matrix core); the steps still ascend into one accumulator
-      int g = __builtin_ctzll(m);
-      m &= m - 1;
-      double a0 = ya[4 * g * NRP], b0 = yb[4 * g * NRP];
-      bool h1 = m != 0;
-      if (h1) {
-        g = __builtin_ctzll(m);
-        m &= m - 1;
       }
-      double a1 = ya[4 * g * NRP], b1 = yb[4 * g * NRP];
-      while (h1) {
-        const bool h2 = m != 0;
-        if (h2) {
+      __syncthreads();  // half h complete / half h - 1 consumed
+    }
+    return;
+  }
+  // ---- consumers: G += Yt^T Yt of half h - 1 on MFMA while the producers fill half h.
+  // Tile k of the enumeration goes to consumer wave k mod kLinCons.  A[i][k] = Yt[k][16I + i],
+  // B[k][j] = Yt[k][16J + j], lane holds k = lane >> 4.  A 4-row step g (rows 4g .. 4g+3:
+  // landmarks 4g/3 and (4g+3)/3) of tile (I, J) is skipped when those rows are zero in tile I's
+  // or J's columns (the z column tile NT-1 always counts); each tile's steps ascend into its own
+  // accumulator -- half 0's steps then half 1's, i.e. the chunk's rows in order -- and the
+  // operands are loaded two active steps ahead of the MFMA that uses them.  (Walking the union of
+  // the wave's tiles' steps with every active tile issued back to back -- independent
+  // accumulators in flight -- measured slower: 1080p BA 5.0 -> 6.8 ms, 600p 1.87 -> 2.21 ms, the
+  // operand arrays spilling at 128 VGPRs.)
+  const int wc = wid - kLinProd;
+  int ntiles = 0;
+  for (int i = 0; i < ntu; ++i) ntiles += (ntu - i) + (ntu < NT ? 1 : 0);
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  d4 acc[MAXT];
+  int tI[MAXT], tJ[MAXT];
+#pragma unroll
+  for (int lt = 0; lt < MAXT; ++lt) {
+    acc[lt] = d4{0.0, 0.0, 0.0, 0.0};
+    const int k = kLinCons * lt + wc;
+    tI[lt] = tJ[lt] = -1;
+    if (k < ntiles) lin_tile(k, ntu, NT, tI[lt], tJ[lt]);
+  }
+  for (int h = 0; h <= nh; ++h) {
+    if (h > 0) {
+      const int hb = (h - 1) & 1;
+      const double* Yb = sY + hb * rows * NRP;
+      const uint32_t actl = lane < rows / 4 ? (s_tm[hb][(4 * lane) / 3] | s_tm[hb][(4 * lane + 3) / 3]) : 0u;
+#pragma unroll
+      for (int lt = 0; lt < MAXT; ++lt) {
+        const int I = tI[lt], J = tJ[lt];
+        if (I < 0) continue;
+        const double* ya = Yb + (lane >> 4) * NRP + 16 * I + (lane & 15);
+        const double* yb = Yb + (lane >> 4) * NRP + 16 * J + (lane & 15);
+        uint64_t m = __ballot(((actl >> I) & 1u) && (((actl >> J) & 1u) || J == NT - 1));
+        if (!m) continue;
+        int g = __builtin_ctzll(m);
+        m &= m - 1;
+        double a0 = ya[4 * g * NRP], b0 = yb[4 * g * NRP];
+        bool h1 = m != 0;
+        if (h1) {
           g = __builtin_ctzll(m);
           m &= m - 1;
         }
-        const double a2 = ya[4 * g * NRP], b2 = yb[4 * g * NRP];
+        double a1 = ya[4 * g * NRP], b1 = yb[4 * g * NRP];
+        while (h1) {
+          const bool h2 = m != 0;
+          if (h2) {
+            g = __builtin_ctzll(m);
+            m &= m - 1;
+          }
+          const double a2 = ya[4 * g * NRP], b2 = yb[4 * g * NRP];
+          acc[lt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[lt], 0, 0, 0);
+          a0 = a1, b0 = b1, a1 = a2, b1 = b2, h1 = h2;
+        }
         acc[lt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[lt], 0, 0, 0);
-        a0 = a1, b0 = b1, a1 = a2, b1 = b2, h1 = h2;
       }
-      acc[lt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[lt], 0, 0, 0);
     }
-    __syncthreads();  // sY / s_tm are rewritten by the next chunk
+    __syncthreads();  // half h complete / half h - 1 consumed
   }
   // f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
   double* Gc = v.Gp + (int64_t)part * NR * NR;
@@ -1738,7 +1759,7 @@ int ba_init(fvo_ctx* ctx) {
     FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_emit, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)build_shm(d)));
   }
-  FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_lin<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_lin<kLinTiles64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lin_shm(d)));
   FVO_HIP(ctx, hipFuncSetAttribute((const void*)k_ba_lin<kLinMaxTiles>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lin_shm(d)));
@@ -1784,7 +1805,7 @@ void ba_windows_launch(fvo_ctx* ctx, const BaIn& in, const BaCam& cam, const BaD
       hipLaunchKernelGGL(k_ba_setcost, dim3(nw), dim3(64), 0, s, ws, d, 0);
     }
     hipLaunchKernelGGL(k_ba_pp, gfr, dim3(kBlock), 0, s, in, ws, d, cam);
-    if (d.NR == 64) hipLaunchKernelGGL(k_ba_lin<1>, gch, dim3(kLinBlock), shl, s, in, ws, d, cam);
+    if (d.NR == 64) hipLaunchKernelGGL(k_ba_lin<kLinTiles64>, gch, dim3(kLinBlock), shl, s, in, ws, d, cam);
     else hipLaunchKernelGGL(k_ba_lin<kLinMaxTiles>, gch, dim3(kLinBlock), shl, s, in, ws, d, cam);
     if (d.NPART >= kGsumParts)
       hipLaunchKernelGGL(k_ba_gsum, dim3(nw, (d.NR * d.NR / 2 + 255) / 256), dim3(256), 0, s, ws, d);
