@@ -174,8 +174,10 @@ def test_gpu_frontend_local_ba_matches_oracle(oracle_mod):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not gpu_available(), reason="needs a ROCm GPU")
-def test_gpu_ba_window_20():
-    """Config 5's K = 20 (reduced system 114 x 114, 128-row MFMA tiles)."""
-    p = ba_synth.clean_problem(n=20, seed=5, n_pts=2500)
-    Tout, stats = _gpu_ba(p, first_end=19, n_windows=1, window=20)
-    _check(p, Tout[0], stats[0], 0, 19)
+@pytest.mark.parametrize("K", [20, 21])
+def test_gpu_ba_window_20(K):
+    """Config 5's K = 20 (reduced system 114 x 114, 128-row MFMA tiles) and the largest window
+    (K = 21: 120 x 120, the solve's LDS at its largest -- S, the diagonal tiles' inverses)."""
+    p = ba_synth.clean_problem(n=K, seed=5, n_pts=2500)
+    Tout, stats = _gpu_ba(p, first_end=K - 1, n_windows=1, window=K)
+    _check(p, Tout[0], stats[0], 0, K - 1)
