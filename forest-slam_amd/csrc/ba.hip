@@ -78,6 +78,11 @@ constexpr int kLinWaves = kLinWavesDefault, kLinBlock = 64 * kLinWaves;
 constexpr int kLinProd = kLinWaves / 2, kLinCons = kLinWaves - kLinProd;
 constexpr int kLinMaxTiles = (36 + kLinCons - 1) / kLinCons;  // 16x16 tiles per consumer wave: 36 upper tiles at NR = 128
 constexpr int kLinTiles64 = (10 + kLinCons - 1) / kLinCons;   // 10 upper tiles at NR = 64
+// a half chunk (LPC / 2 landmarks, 3 Y rows each) fits s_tm's 32 slots, its 4-row MFMA steps one
+// lane each, and its lane groups the producer waves
+static_assert(kLinLPC64 / 2 <= 32 && (3 * (kLinLPC64 / 4)) % 4 == 0 && 3 * (kLinLPC64 / 2) / 4 <= 64,
+              "half-chunk shape");
+static_assert((64 * kLinProd) % (kLinLPC64 / 2) == 0, "producer lanes split evenly over a half chunk");
 constexpr double kD2Mono = 5.991, kD2Stereo = 7.815, kMinZ = 0.01, kLam0 = 1e-3;
 
 struct BaState {
