@@ -1260,6 +1260,7 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
   double* rinv = rhs + NP;  // reciprocal pivots of the factor
   constexpr int LS = 17;      // row stride of linvT (16 + 1: a column of stores hits 16 bank pairs)
   double* linvT = rinv + NP;  // per panel p: row j = column j of L_pp^-1 (the blocked solves below)
+  double* dcol = linvT + 17 * NP;  // [16]: the diagonal tile's current column of L (factor_diag)
   if (tid == 0) s_fail = 0;
   // padding: identity rows / columns past np
   for (int t = tid; t < NP * NP; t += kSolveBlock) {
@@ -1345,9 +1346,13 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
       const double lic = r[c] * rp;  // L[i][c] (the diagonal piv rp on row c)
       // r6: every entry updated (one FMA, no select): a lane's entries right of its diagonal
       // become garbage that nothing reads (pivots and multipliers come from lanes at or below
-      // their column) and are zeroed as each column completes
+      // their column) and are zeroed as each column completes.  The next column's multiplier
+      // (the chain to the next pivot) by v_readlane; the rest of the column through LDS (one
+      // store, broadcast reads: ~8 instead of ~28 readlanes), needed a column or more later.
+      if (lane < 16) dcol[lane] = lic;
+      if (c + 1 < 16) r[c + 1] = fma(-lic, rl_f64(lic, c + 1), r[c + 1]);
 #pragma unroll
-      for (int j = c + 1; j < 16; ++j) r[j] = fma(-lic, rl_f64(lic, j), r[j]);
+      for (int j = c + 2; j < 16; ++j) r[j] = fma(-lic, dcol[j], r[j]);
       r[c] = i >= c ? lic : 0.0;
       if (lane == 0) rinv[c0 + c] = rp;
     }
@@ -1739,7 +1744,7 @@ size_t build_shm(const BaDims& d) {
 size_t lin_shm(const BaDims& d) { return (size_t)8 * 3 * d.LPC * (d.NR + 2); }
 size_t solve_shm(int K) {
   const int np = 6 * (K - 1), NP = ba_np16(np);
-  return (size_t)8 * (NP * ba_sstride(NP) + 2 * NP + 17 * NP);  // S / L (padded), rhs, reciprocal pivots, L_pp^-1
+  return (size_t)8 * (NP * ba_sstride(NP) + 2 * NP + 17 * NP + 16);  // S / L (padded), rhs, reciprocal pivots, L_pp^-1, a column
 }
 
 }  // namespace
