@@ -1262,11 +1262,22 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
   double* linvT = rinv + NP;  // per panel p: row j = column j of L_pp^-1 (the blocked solves below)
   double* dcol = linvT + 17 * NP;  // [16]: the diagonal tile's current column of L (factor_diag)
   if (tid == 0) s_fail = 0;
-  // padding: identity rows / columns past np
-  for (int t = tid; t < NP * NP; t += kSolveBlock) {
-    const int a = t / NP, b = t - a * NP;
-    if (a >= np || b >= np) sS[a * STR + b] = a == b ? 1.0 : 0.0;
+  // the right-hand side's global reads first (issued beside the assembly's below; r6: they
+  // were a second round trip after its LDS stores)
+  double rhs_v = 0.0;
+  if (tid < np) {
+    double gs = 0.0;
+    const double* gp = v.Gp + tid * NR + NR - 1;
+    for (int c = 0; c < nch; ++c) gs += gp[(int64_t)c * NR * NR];
+    rhs_v = -S->Hpp[tid / 6 + 1][21 + tid % 6] + gs;
   }
+  // padding: identity rows / columns past np (r6: only those entries, not a pass over NP x NP)
+  const int pad = NP - np;
+  for (int t = tid; t < pad * NP; t += kSolveBlock) {
+    const int a = np + t / NP, b = t % NP;
+    sS[a * STR + b] = a == b ? 1.0 : 0.0;
+  }
+  for (int t = tid; t < np * pad; t += kSolveBlock) sS[(t / pad) * STR + np + t % pad] = 0.0;
   // S = H_pp + lam diag + 1e-6 I - sum_c G_c (upper triangle, mirrored), G summed by
   // k_ba_gsum (nch == 1 whenever NPART > 1).  A thread takes 4 consecutive columns b0..b0+3 of
   // a row a (b0 from the row's diagonal 16 x 16 tile, which k_ba_lin writes in full).  r6: all of
@@ -1315,17 +1326,8 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
       sS[bb * STR + a] = hv - gq[k][u];
     }
   }
-  for (int a = tid; a < NP; a += kSolveBlock) {
-    double gs = 0.0;
-    if (a < np) {
-      const double* gp = v.Gp + a * NR + NR - 1;
-#pragma unroll 8
-      for (int c = 0; c < nch; ++c) gs += gp[(int64_t)c * NR * NR];
-      rhs[a] = -S->Hpp[a / 6 + 1][21 + a % 6] + gs;
-    } else {
-      rhs[a] = 0.0;
-    }
-  }
+  static_assert(kSolveBlock >= 128, "one thread per row of the reduced system (np <= 120)");
+  if (tid < NP) rhs[tid] = rhs_v;
   __syncthreads();
   typedef double d4 __attribute__((ext_vector_type(4)));
   // (A) the diagonal tile of panel p on wave 0: lane i (< 16; lanes 16..63 mirror row i & 15)
