@@ -63,7 +63,10 @@ constexpr int kBlock = 256;
 // BA 1080p 3.99-4.05 -> 3.74 ms in order (16 / 15 / 14 / 12 / 10 / 8 / 6 parts: 4.03 / 3.82 / 3.77
 // / 3.74 / 3.87 / 3.93 / 4.43 ms), overlapped 1080p bench 1542-1544 -> 1545-1555 frames/s; 600p
 // (4 parts) unchanged, 3 / 2 parts slower there (1.82 / 2.29 vs 1.63 ms)
-constexpr int kLinParts = 12, kLinChunksPerPart = 16;
+// r6, after the producer/consumer split: 8 chunks per part (600p: 8 parts instead of 4; 1080p
+// still clamped at 12): 600p BA 1.52 -> 1.48-1.49 ms, overlapped 5757-5759 -> 5766-5772 frames/s
+// (11 chunks per part, 5 parts: 1.48-1.50 ms)
+constexpr int kLinParts = 12, kLinChunksPerPart = 8;
 // landmarks per k_ba_lin chunk at NR = 64 (half at NR = 128); measured: 32 / 16 per chunk
 // (4610 / 4404 frames/s) and two 8-wave blocks per CU (4796) lose to one 16-wave block with 64
 constexpr int kLinLPC64 = 64, kLinWavesDefault = 16;
