@@ -65,7 +65,7 @@ constexpr int kBlock = 256;
 // (4 parts) unchanged, 3 / 2 parts slower there (1.82 / 2.29 vs 1.63 ms)
 // r6, after the producer/consumer split: 8 chunks per part (600p: 8 parts instead of 4; 1080p
 // still clamped at 12): 600p BA 1.52 -> 1.48-1.49 ms, overlapped 5757-5759 -> 5766-5772 frames/s
-// (11 chunks per part, 5 parts: 1.48-1.50 ms)
+// (11 / 6 / 4 chunks per part: 1.48-1.50 / 1.66 / 1.59-1.60 ms)
 constexpr int kLinParts = 12, kLinChunksPerPart = 8;
 // landmarks per k_ba_lin chunk at NR = 64 (half at NR = 128); measured: 32 / 16 per chunk
 // (4610 / 4404 frames/s) and two 8-wave blocks per CU (4796) lose to one 16-wave block with 64
