@@ -1537,7 +1537,9 @@ __global__ __launch_bounds__(kSolveBlock) void k_ba_solve(void* ws, BaDims dm) {
 // 1.80 -> 1.75 ms against 1 lane, 4: 1.76 ms), kUpdGluLong = 8 at K > 16 (up to 3 observations
 // each of a 20-frame track; BA 1080p / K = 20 4.53 -> 4.27 ms against 32 lanes, which sat mostly
 // idle on tracks of a few observations; 16: 4.43, 4: 4.26 ms).
-constexpr int kUpdGluShort = 2, kUpdGluLong = 8;
+// r6 (after the solve / k_ba_lin changes): 4 lanes at K > 16, 1080p BA 3.32-3.33 -> 3.23 ms (2 / 4
+// lanes at K <= 16: 1.50-1.52 vs 1.51-1.52 ms, unchanged)
+constexpr int kUpdGluShort = 2, kUpdGluLong = 4;
 template <int GLU>
 __global__ __launch_bounds__(kBlock) void k_ba_upd(BaIn in, void* ws, BaDims dm, BaCam cam) {
   constexpr int LPU = kBlock / GLU;
