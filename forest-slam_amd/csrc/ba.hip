@@ -592,7 +592,9 @@ __global__ __launch_bounds__(kBuildBlock) void k_ba_build(BaIn in, void* ws, BaD
 // lists per observed frame from a scan over the landmarks.  Creation stops at the first
 // candidate in (frame, row) order that does not fit: both prefix sums are monotone, so a
 // candidate is created iff its all-candidate prefixes fit -- the same set as the serial stop.
-constexpr int kBirthBlock = 256;
+// r6: 512 threads (half the row passes over a birth frame's matches in k_ba_emit; bit-identical):
+// 1080p BA 3.24 -> 3.17-3.19 ms; 600p BA and overlapped bench within noise (two A/Bs: +0.8 %, -0.3 %)
+constexpr int kBirthBlock = 512;
 
 struct BirthFrame {
   int e, s, n, f, M;
